@@ -1,0 +1,166 @@
+/*
+ * mvtv.h — C ABI of the MI355X-native mesh-TV ADMM solver (libmvtv.so).
+ *
+ * This is the drop-in boundary for the reference's ADMM hot path. Every entry
+ * point replaces one reference interface (cited as path:line under
+ * /root/reference) and uses only plain pointers, sizes and PODs: no Armadillo,
+ * Rcpp or torch types. Host buffers are caller-owned; device buffers are owned
+ * by the opaque mvtv_problem handle (one handle per GPU; handles are
+ * thread-safe with respect to each other, a single handle is not).
+ *
+ * Layouts (identical to the reference):
+ *   theta  [N]  mesh values, column-major, dim 0 fastest (cpp-code/utils.cpp:40-52)
+ *   u      [E]  scaled dual, blocks concatenated in the D row order of the
+ *               caller (C++ create_D: all-ones block first; Python create_D:
+ *               b = 1..), each block a column-major reduced grid
+ *               (cpp-code/utils.cpp:103-134, 245-269; code/utils.py:138-149)
+ *
+ * Errors never cross the ABI as exceptions: every call returns mvtv_status and
+ * leaves a message readable through mvtv_last_error() (thread-local).
+ */
+#ifndef MVTV_MVTV_H
+#define MVTV_MVTV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVTV_MAX_DIMS 4
+#define MVTV_MAX_BLOCKS 15
+
+typedef enum mvtv_status {
+    MVTV_OK = 0,
+    MVTV_MAXITER = 1,        /* A: "Failed to converge!" (cpp-code/solvers.cpp:122-124); B: max_counter break (rcpp…/solvers.cpp:129-132) */
+    MVTV_BAD_ARG = 2,
+    MVTV_DIM_MISMATCH = 3,   /* reference's mixed-partial product fails for this mesh */
+    MVTV_HIP_ERROR = 4,
+    MVTV_NO_DEVICE = 5,
+    MVTV_OUT_OF_MEMORY = 6,
+    MVTV_PCG_NOT_CONVERGED = 7 /* only reported when opts.pcg_strict != 0 */
+} mvtv_status;
+
+/* Which reference implementation's ADMM semantics to follow. */
+typedef enum mvtv_variant {
+    MVTV_VARIANT_RCPP = 0,   /* B: rcpp-code/MultivarTV/src/solvers.cpp:96-136 (released package) */
+    MVTV_VARIANT_CPP = 1,    /* A: cpp-code/solvers.cpp:90-130 (int rho, theta-change stop) */
+    MVTV_VARIANT_PY = 2      /* C: code/solvers.py:53-76 (fixed rho = lambda, threshold 1) */
+} mvtv_variant;
+
+/* Row-block order of D. */
+typedef enum mvtv_block_order {
+    MVTV_ORDER_CPP = 0,      /* C++ create_D: [all-ones, w=1] + b=1..2^p-2 (cpp-code/utils.cpp:245-269) */
+    MVTV_ORDER_PY = 1        /* Python create_D: b=1..2^p-1 unweighted, or b=1..2^p-2 weighted (code/utils.py:138-149) */
+} mvtv_block_order;
+
+/* Replaces the mbs_cache / mbs_one_inits bundles (rcpp…/solvers.hpp:30-50,
+ * cpp-code/solvers.hpp:25-43): instead of sparse O, D, D^T D the problem is the
+ * mesh shape, the block weights and the diagonal W = O^T O with O^T y. */
+typedef struct mvtv_problem_desc {
+    int32_t p;                       /* 1..4 dimensions */
+    int64_t m[MVTV_MAX_DIMS];        /* mesh points per dimension (each >= 2) */
+    int32_t block_order;             /* mvtv_block_order */
+    int32_t weighted;                /* 1: w_b = prod_{j not in b} deltas_j; 0: every w = 1 */
+    double deltas[MVTV_MAX_DIMS];    /* mesh widths (create_deltas, rcpp…/utils.cpp:256-263) */
+    const double* oty;               /* [N] O^T y (required) */
+    const double* wdiag;             /* [N] diag(O^T O), or NULL for W = I (mesh == data) */
+    int32_t device;                  /* HIP device ordinal */
+} mvtv_problem_desc;
+
+typedef struct mvtv_admm_opts {
+    int32_t variant;        /* mvtv_variant */
+    double tol;             /* <= 0: variant default (B 1e-4 rcpp…/solvers.hpp:19; A 1e-3 cpp-code/solvers.hpp:14; C 1e-3) */
+    int32_t max_counter;    /* <= 0: variant default (B 3000, A 2000, C 1000000 — the reference's C guard is dead) */
+    int32_t fixed_iters;    /* > 0: run exactly this many iterations, stopping test disabled (trajectory / bench mode) */
+    double sigma;           /* solve-matrix scalar W + sigma D^T D at entry; NaN: variant default (B rho, A lambda, C lambda) */
+    double ymean;           /* mean(y): A and C initialise theta_old from it (cpp-code/solvers.cpp:103, code/solvers.py:63) */
+    double pcg_rtol;        /* <= 0: 1e-10 (relative to ||b||) */
+    int32_t pcg_max_iter;   /* <= 0: 20000 */
+    int32_t pcg_strict;     /* != 0: report MVTV_PCG_NOT_CONVERGED when a theta-solve stops at pcg_max_iter */
+    int32_t verbose;        /* != 0: print "Lambda= .., Counter = .." like rcpp…/solvers.cpp:134 */
+} mvtv_admm_opts;
+
+typedef struct mvtv_admm_stats {
+    int32_t iters;          /* ADMM iterations executed */
+    int32_t status;         /* mvtv_status of the run */
+    double r_norm, s_norm;  /* last primal / dual residual norms */
+    double eps_pri, eps_dual;
+    double rho;             /* final rho (after the last adaptation) */
+    double dtheta_max;      /* last max|theta - theta_old| (A, C) */
+    int64_t pcg_iters;      /* total PCG iterations */
+    int32_t pcg_iters_max;  /* max PCG iterations in one theta-solve */
+    int32_t pcg_unconverged;/* theta-solves that hit pcg_max_iter */
+    double seconds;         /* wall time of the call */
+} mvtv_admm_stats;
+
+typedef struct mvtv_problem mvtv_problem;
+
+/* ---- library -------------------------------------------------------------------- */
+const char* mvtv_version(void);
+const char* mvtv_status_string(int32_t status);
+const char* mvtv_last_error(void);
+int32_t mvtv_device_count(void);
+void mvtv_default_opts(mvtv_admm_opts* opts, int32_t variant);
+
+/* ---- problem (replaces create_cache_objects / fill_cache / use_cache,
+ *      rcpp…/solvers.cpp:36-69; cpp-code/solvers.cpp:31-62) ------------------------ */
+mvtv_status mvtv_problem_create(const mvtv_problem_desc* desc, mvtv_problem** out);
+void mvtv_problem_destroy(mvtv_problem* prob);
+int64_t mvtv_problem_nodes(const mvtv_problem* prob);   /* N = ntheta (rcpp…/solvers.hpp:36) */
+int64_t mvtv_problem_edges(const mvtv_problem* prob);   /* E = rowsD (rcpp…/solvers.hpp:35) */
+int32_t mvtv_problem_blocks(const mvtv_problem* prob);
+/* block k's binary code, effective difference set S' (bit j = dim j) and weight */
+mvtv_status mvtv_problem_block_info(const mvtv_problem* prob, int32_t k, int32_t* code, int32_t* sprime, double* weight);
+/* new O^T y and W for the same mesh (CV folds re-run create_cache_objects, rcpp…/solvers.cpp:347-348) */
+mvtv_status mvtv_problem_set_data(mvtv_problem* prob, const double* oty, const double* wdiag);
+
+/* ---- the hot path ------------------------------------------------------------------ */
+/* Drop-in for admm_update:
+ *   B: void admm_update(vec y, mbs_one_inits, vec& theta_init, double lambda, bool verbose,
+ *                       vec& u_init, double& rho_init, admm_out&)   rcpp…/solvers.hpp:100
+ *   A: vec admm_update(vec y, mbs_one_inits, vec* theta_init, double lambda)  cpp-code/solvers.hpp:85
+ *   C: the while-loop of mbs_one                                     code/solvers.py:53-76
+ * theta_inout [N]: theta_init in, theta out. u_inout [E]: u_init in / u out, or NULL for the
+ * variant's own u0 (B 0, A and C 1/lambda) with u not returned. rho_inout: rho_init in /
+ * rho out (B; A and C derive rho from lambda and return the final one). */
+mvtv_status mvtv_admm(mvtv_problem* prob, const mvtv_admm_opts* opts, double lambda,
+                      double* theta_inout, double* u_inout, double* rho_inout, mvtv_admm_stats* stats);
+
+/* Resident form of the same loop for callers that keep the state in HBM across calls
+ * (lambda paths with warm start rcpp…/solvers.cpp:212-220, benchmarks). */
+mvtv_status mvtv_state_set(mvtv_problem* prob, const double* theta, const double* u, double rho);
+mvtv_status mvtv_state_get(mvtv_problem* prob, double* theta, double* u, double* rho);
+mvtv_status mvtv_admm_run(mvtv_problem* prob, const mvtv_admm_opts* opts, double lambda, mvtv_admm_stats* stats);
+/* fitted values O theta for n points given their mesh index (fill_output_mbs_one, rcpp…/solvers.cpp:73) */
+mvtv_status mvtv_fitted(mvtv_problem* prob, const int64_t* mesh_index, int64_t n, double* fitted);
+
+/* ---- operators (inits.D*theta, inits.Dt*v, spcrosses*x, spsolve(spcrosses, b):
+ *      rcpp…/solvers.cpp:112-126) ----------------------------------------------------- */
+mvtv_status mvtv_apply_D(mvtv_problem* prob, const double* theta, double* d_out);        /* [N] -> [E] */
+mvtv_status mvtv_apply_Dt(mvtv_problem* prob, const double* v, double* g_out);           /* [E] -> [N] */
+mvtv_status mvtv_apply_A(mvtv_problem* prob, double sigma, const double* x, double* q_out); /* (W + sigma D^T D) x */
+mvtv_status mvtv_solve(mvtv_problem* prob, double sigma, const double* b, double* x_inout,
+                       double rtol, int32_t max_iter, int32_t* iters, double* relres);
+
+/* ---- instrumentation (HIP events on the solver's stream) ---------------------------- */
+typedef enum mvtv_kernel_id {
+    MVTV_K_EDGE_UPDATE = 0,   /* D theta, soft-threshold, dual update, |r|,|D theta|,|alpha| */
+    MVTV_K_GATHER = 1,        /* D^T alpha, D^T u and the dual-residual norms */
+    MVTV_K_PCG_INIT = 2,      /* b and r0 = b - A theta */
+    MVTV_K_PCG_APPLY = 3,     /* q = A p, p.q */
+    MVTV_K_PCG_UPDATE = 4,    /* x += a p, r -= a q, r.z */
+    MVTV_K_PCG_DIRECTION = 5, /* p = z + b p */
+    MVTV_K_REDUCE = 6,        /* partial-sum finalisation / PCG scalars */
+    MVTV_K_OTHER = 7,
+    MVTV_K_COUNT = 8
+} mvtv_kernel_id;
+mvtv_status mvtv_timing_enable(mvtv_problem* prob, int32_t on);
+mvtv_status mvtv_timing_get(mvtv_problem* prob, int32_t kernel_id, double* total_ms, int64_t* launches,
+                            double* bytes_per_launch);
+const char* mvtv_kernel_name(int32_t kernel_id);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MVTV_MVTV_H */

@@ -1,0 +1,10 @@
+"""multivartv_amd — MI355X-native mesh-TV ADMM solver (the hot path of brayano/MultivarTV).
+
+The numerical work runs in hand-written HIP kernels for gfx950 behind the C ABI
+in include/mvtv/mvtv.h (libmvtv.so). This package is the host-side mirror of
+the reference's Python interface (code/solvers.py, code/utils.py) over that ABI.
+"""
+from ._lib import (ORDER_CPP, ORDER_PY, VARIANT_CPP, VARIANT_PY, VARIANT_RCPP, DimMismatchError,  # noqa: F401
+                   MaxIterError, MvtvError, Problem, device_count, lib)
+
+__version__ = "0.1.0"

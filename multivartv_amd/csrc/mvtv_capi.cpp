@@ -1,0 +1,828 @@
+// mvtv_capi.cpp — host driver of the ADMM hot path and the C ABI declared in include/mvtv/mvtv.h.
+//
+// One mvtv_problem = one GPU, one HIP stream, all vectors resident in HBM. The ADMM loop
+// follows the reference variants line by line at the level of scalars (adapt_step, stopping
+// tests, counters); every vector operation is a kernel from mvtv_kernels.hip:
+//   B  rcpp-code/MultivarTV/src/solvers.cpp:96-136   (admm_update, adapt_step :77-94)
+//   A  cpp-code/solvers.cpp:90-130                    (admm_update, adapt_step :70-88)
+//   C  code/solvers.py:53-76                          (mbs_one's loop)
+// Per ADMM iteration the host reads back 7 scalars (one stream sync); the PCG theta-solve
+// keeps its scalars on the device and is polled every few iterations.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mvtv/mvtv.h"
+#include "mvtv_internal.h"
+
+using namespace mvtv;
+
+namespace {
+thread_local std::string g_last_error;
+
+mvtv_status fail(mvtv_status s, const std::string& msg) {
+    g_last_error = msg;
+    return s;
+}
+
+#define HIP_TRY(expr)                                                                                 \
+    do {                                                                                              \
+        hipError_t _e = (expr);                                                                       \
+        if (_e != hipSuccess)                                                                         \
+            return fail(_e == hipErrorOutOfMemory ? MVTV_OUT_OF_MEMORY : MVTV_HIP_ERROR,              \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                           \
+    } while (0)
+
+#define MVTV_TRY(expr)                        \
+    do {                                      \
+        mvtv_status _s = (expr);              \
+        if (_s != MVTV_OK) return _s;         \
+    } while (0)
+
+constexpr int kPcgPoll = 8;   // PCG iterations enqueued between host polls of the done flag
+
+struct DevBuf {
+    double* p = nullptr;
+    size_t n = 0;
+};
+}  // namespace
+
+struct mvtv_problem {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Geom g{};
+    int order = 0, weighted = 1, wmode = W_IDENTITY;
+    double deltas[MVTV_MAX_DIMS] = {0, 0, 0, 0};
+    int codes[kMaxBlocks] = {0};
+    int sprime[kMaxBlocks] = {0};
+    uint64_t blk_len[kMaxBlocks] = {0};
+    int64_t E = 0;
+    int grid = 1;
+
+    double *oty = nullptr, *wdiag = nullptr;
+    double *theta = nullptr, *edges = nullptr, *ga = nullptr, *gu = nullptr, *guprev = nullptr;
+    double *r = nullptr, *p = nullptr, *q = nullptr, *thold = nullptr;
+    double *partials = nullptr, *red = nullptr;
+    PcgState* st = nullptr;
+    double* stage = nullptr;
+    size_t stage_n = 0;
+    double* host_red = nullptr;   // pinned: reductions + PcgState mirror
+    PcgState* host_st = nullptr;
+
+    // resident ADMM state
+    bool have_state = false;
+    bool u_default = true;
+    int edge_mode = U_EXPLICIT;
+    double t_z = 0.0, c_state = 1.0, rho = 0.0;
+
+    // instrumentation
+    bool timing = false;
+    struct Pending {
+        hipEvent_t a, b;
+        int kid;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> ev_pool;
+    double ms[MVTV_K_COUNT] = {0};
+    int64_t launches[MVTV_K_COUNT] = {0};
+
+    Launch L() const { return Launch{stream, grid}; }
+
+    hipEvent_t get_event() {
+        if (!ev_pool.empty()) {
+            hipEvent_t e = ev_pool.back();
+            ev_pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    int tstart(int kid) {
+        if (!timing) return -1;
+        Pending pd{get_event(), get_event(), kid};
+        (void)hipEventRecord(pd.a, stream);
+        pending.push_back(pd);
+        return int(pending.size()) - 1;
+    }
+    void tstop(int h) {
+        if (h >= 0) (void)hipEventRecord(pending[h].b, stream);
+    }
+    void harvest() {  // call after a stream sync
+        for (auto& pd : pending) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, pd.a, pd.b) == hipSuccess) {
+                ms[pd.kid] += t;
+                launches[pd.kid] += 1;
+            }
+            ev_pool.push_back(pd.a);
+            ev_pool.push_back(pd.b);
+        }
+        pending.clear();
+    }
+    mvtv_status sync() {
+        HIP_TRY(hipStreamSynchronize(stream));
+        harvest();
+        return MVTV_OK;
+    }
+};
+
+namespace {
+
+int popcount(int x) { return __builtin_popcount(unsigned(x)); }
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+mvtv_status alloc(double** ptr, size_t n) {
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(ptr), std::max<size_t>(n, 1) * sizeof(double)));
+    return MVTV_OK;
+}
+
+void free_all(mvtv_problem* P) {
+    double** bufs[] = {&P->oty, &P->wdiag, &P->theta, &P->edges, &P->ga, &P->gu, &P->guprev, &P->r,
+                       &P->p, &P->q, &P->thold, &P->partials, &P->red, &P->stage};
+    for (double** b : bufs)
+        if (*b) {
+            (void)hipFree(*b);
+            *b = nullptr;
+        }
+    if (P->st) (void)hipFree(P->st);
+    if (P->host_red) (void)hipHostFree(P->host_red);
+    for (auto& pd : P->pending) {
+        (void)hipEventDestroy(pd.a);
+        (void)hipEventDestroy(pd.b);
+    }
+    for (auto e : P->ev_pool) (void)hipEventDestroy(e);
+    if (P->stream) (void)hipStreamDestroy(P->stream);
+}
+
+double variant_tol(const mvtv_admm_opts& o) {
+    if (o.tol > 0) return o.tol;
+    return o.variant == MVTV_VARIANT_RCPP ? 1e-4 : 1e-3;
+}
+int variant_maxc(const mvtv_admm_opts& o) {
+    if (o.max_counter > 0) return o.max_counter;
+    return o.variant == MVTV_VARIANT_RCPP ? 3000 : (o.variant == MVTV_VARIANT_CPP ? 2000 : 1000000);
+}
+
+// Copy a compact [E] edge vector (reference block layout) into the padded device layout.
+mvtv_status import_edges(mvtv_problem* P, const double* host_u, double* padded) {
+    HIP_TRY(hipMemsetAsync(padded, 0, size_t(P->g.nb) * P->g.N * sizeof(double), P->stream));
+    if (!P->stage) {
+        P->stage_n = std::min<size_t>(size_t(P->E), size_t(1) << 24);
+        MVTV_TRY(alloc(&P->stage, P->stage_n));
+    }
+    uint64_t off = 0;
+    for (int k = 0; k < P->g.nb; ++k) {
+        for (uint64_t e0 = 0; e0 < P->blk_len[k]; e0 += P->stage_n) {
+            const uint64_t cnt = std::min<uint64_t>(P->stage_n, P->blk_len[k] - e0);
+            HIP_TRY(hipMemcpyAsync(P->stage, host_u + off + e0, cnt * sizeof(double), hipMemcpyHostToDevice, P->stream));
+            HIP_TRY(launch_edges_import(P->g, P->order, P->stream, k, e0, cnt, P->stage, padded));
+        }
+        off += P->blk_len[k];
+    }
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    return MVTV_OK;
+}
+
+mvtv_status export_edges(mvtv_problem* P, const double* padded, double* host_u, int umode, double t, double c) {
+    if (!P->stage) {
+        P->stage_n = std::min<size_t>(size_t(P->E), size_t(1) << 24);
+        MVTV_TRY(alloc(&P->stage, P->stage_n));
+    }
+    uint64_t off = 0;
+    for (int k = 0; k < P->g.nb; ++k) {
+        for (uint64_t e0 = 0; e0 < P->blk_len[k]; e0 += P->stage_n) {
+            const uint64_t cnt = std::min<uint64_t>(P->stage_n, P->blk_len[k] - e0);
+            HIP_TRY(launch_edges_export(P->g, P->order, P->stream, k, e0, cnt, padded, P->stage, umode, t, c));
+            HIP_TRY(hipMemcpyAsync(host_u + off + e0, P->stage, cnt * sizeof(double), hipMemcpyDeviceToHost, P->stream));
+            HIP_TRY(hipStreamSynchronize(P->stream));
+        }
+        off += P->blk_len[k];
+    }
+    return MVTV_OK;
+}
+
+// Solve (W + sigma D^T D) x = b, b = oty + ca*ga + cb*gb, by Jacobi-PCG warm-started at x.
+mvtv_status pcg_solve(mvtv_problem* P, double sigma, const double* oty, const double* ga, double ca,
+                      const double* gb, double cb, double* x, double rtol, int maxit, int* iters, double* relres) {
+    const Launch L = P->L();
+    const double* w = P->wdiag;
+    int h = P->tstart(MVTV_K_PCG_INIT);
+    HIP_TRY(launch_pcg_init(P->g, L, sigma, P->wmode, w, oty, ga, ca, gb, cb, x, P->r, P->p, P->partials));
+    P->tstop(h);
+    h = P->tstart(MVTV_K_REDUCE);
+    HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, PR_N, 0, 1, nullptr, P->st, rtol * rtol, maxit));
+    P->tstop(h);
+    for (int enq = 0;; enq += kPcgPoll) {
+        for (int b = 0; b < kPcgPoll && enq + b < maxit; ++b) {
+            h = P->tstart(MVTV_K_PCG_APPLY);
+            HIP_TRY(launch_apply_A(P->g, L, sigma, P->wmode, w, P->p, P->q, P->partials, P->st));
+            P->tstop(h);
+            h = P->tstart(MVTV_K_REDUCE);
+            HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 0, 2, nullptr, P->st));
+            P->tstop(h);
+            h = P->tstart(MVTV_K_PCG_UPDATE);
+            HIP_TRY(launch_pcg_update(P->g, L, sigma, P->wmode, w, x, P->r, P->p, P->q, P->st, P->partials));
+            P->tstop(h);
+            h = P->tstart(MVTV_K_REDUCE);
+            HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 2, 0, 3, nullptr, P->st));
+            P->tstop(h);
+            h = P->tstart(MVTV_K_PCG_DIRECTION);
+            HIP_TRY(launch_pcg_pupdate(P->g, L, sigma, P->wmode, w, P->r, P->p, P->st));
+            P->tstop(h);
+        }
+        HIP_TRY(hipMemcpyAsync(P->host_st, P->st, sizeof(PcgState), hipMemcpyDeviceToHost, P->stream));
+        MVTV_TRY(P->sync());
+        if (P->host_st->done || enq + kPcgPoll >= maxit) break;
+    }
+    *iters = P->host_st->iter;
+    *relres = P->host_st->bnorm2 > 0 ? std::sqrt(P->host_st->rnorm2 / P->host_st->bnorm2) : 0.0;
+    return MVTV_OK;
+}
+
+mvtv_status ensure_state(mvtv_problem* P) {
+    if (!P->have_state) return fail(MVTV_BAD_ARG, "no ADMM state: call mvtv_state_set first");
+    return MVTV_OK;
+}
+
+}  // namespace
+
+// =================================================================================== C ABI
+extern "C" {
+
+const char* mvtv_version(void) { return "multivartv_amd 0.1.0 (gfx950)"; }
+
+const char* mvtv_status_string(int32_t s) {
+    switch (s) {
+        case MVTV_OK: return "ok";
+        case MVTV_MAXITER: return "maximum ADMM iterations reached";
+        case MVTV_BAD_ARG: return "bad argument";
+        case MVTV_DIM_MISMATCH: return "dimension mismatch (mixed-partial construction)";
+        case MVTV_HIP_ERROR: return "HIP error";
+        case MVTV_NO_DEVICE: return "no HIP device";
+        case MVTV_OUT_OF_MEMORY: return "out of device memory";
+        case MVTV_PCG_NOT_CONVERGED: return "PCG theta-solve did not converge";
+        default: return "unknown status";
+    }
+}
+
+const char* mvtv_last_error(void) { return g_last_error.c_str(); }
+
+int32_t mvtv_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void mvtv_default_opts(mvtv_admm_opts* o, int32_t variant) {
+    std::memset(o, 0, sizeof(*o));
+    o->variant = variant;
+    o->sigma = std::nan("");
+    o->ymean = 0.0;
+}
+
+mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) {
+    if (!d || !out) return fail(MVTV_BAD_ARG, "null descriptor/output");
+    *out = nullptr;
+    if (d->p < 1 || d->p > MVTV_MAX_DIMS) return fail(MVTV_BAD_ARG, "p must be in 1..4");
+    if (!d->oty) return fail(MVTV_BAD_ARG, "oty is required");
+    if (d->block_order != MVTV_ORDER_CPP && d->block_order != MVTV_ORDER_PY) return fail(MVTV_BAD_ARG, "block_order");
+    const int p = d->p;
+    uint64_t N = 1;
+    for (int j = 0; j < p; ++j) {
+        if (d->m[j] < 2) return fail(MVTV_BAD_ARG, "every m_j must be >= 2");
+        N *= uint64_t(d->m[j]);
+    }
+    if (N >= (uint64_t(1) << 31)) return fail(MVTV_BAD_ARG, "N >= 2^31 nodes on one GPU");
+    const int full = (1 << p) - 1;
+    int nb;
+    if (d->block_order == MVTV_ORDER_CPP) nb = full;
+    else nb = d->weighted ? full - 1 : full;
+    if (nb <= 0) return fail(MVTV_BAD_ARG, "empty D (Python create_D with deltas at p = 1)");
+    int ndev = mvtv_device_count();
+    if (ndev <= 0) return fail(MVTV_NO_DEVICE, "no HIP device visible");
+    if (d->device < 0 || d->device >= ndev) return fail(MVTV_BAD_ARG, "device ordinal out of range");
+
+    auto* P = new mvtv_problem();
+    P->device = d->device;
+    P->order = d->block_order;
+    P->weighted = d->weighted;
+    Geom& g = P->g;
+    g.p = p;
+    g.nb = nb;
+    g.N = uint32_t(N);
+    uint32_t stride = 1;
+    for (int j = 0; j < MVTV_MAX_DIMS; ++j) {
+        g.m[j] = j < p ? uint32_t(d->m[j]) : 1u;
+        g.stride[j] = stride;
+        if (j < p) stride *= g.m[j];
+        P->deltas[j] = j < p ? d->deltas[j] : 0.0;
+    }
+    for (int j = 0; j < MVTV_MAX_DIMS - 1; ++j) g.fd[j] = FastDiv(g.m[j]);
+    for (int S = 0; S < 16; ++S) g.cS[S] = 0.0;
+    P->E = 0;
+    for (int k = 0; k < nb; ++k) {
+        const int b = block_code(k, p, P->order);
+        const int S = sprime_mask(b, p);
+        // reference mixedpartial: a mixed block with min S > 0 multiplies incompatible
+        // matrices unless m_0 == m_{min S} (code/utils.py:102-129)
+        int nominal = 0;
+        for (int j = 0; j < p; ++j)
+            if ((b >> (p - 1 - j)) & 1) nominal |= 1 << j;
+        if (popcount(nominal) >= 2 && !(nominal & 1)) {
+            int lo = 0;
+            while (!((nominal >> lo) & 1)) ++lo;
+            if (d->m[0] != d->m[lo]) {
+                delete P;
+                return fail(MVTV_DIM_MISMATCH, "mixed partial of block " + std::to_string(b) +
+                                                   ": m[0] != m[" + std::to_string(lo) + "]");
+            }
+        }
+        double w = 1.0;
+        if (d->weighted)
+            for (int j = 0; j < p; ++j)
+                if (!((b >> (p - 1 - j)) & 1)) w *= d->deltas[j];
+        g.w[k] = w;
+        g.cS[S] += w * w;
+        P->codes[k] = b;
+        P->sprime[k] = S;
+        uint64_t len = 1;
+        for (int j = 0; j < p; ++j) len *= uint64_t(g.m[j] - ((S >> j) & 1));
+        P->blk_len[k] = len;
+        P->E += int64_t(len);
+    }
+    for (int k = nb; k < kMaxBlocks; ++k) g.w[k] = 0.0;
+    P->grid = int(std::min<uint64_t>((N + kThreads - 1) / kThreads, kMaxGrid));
+
+    DeviceGuard dg(P->device);
+    mvtv_status s = MVTV_OK;
+    auto A = [&](double** ptr, size_t n) {
+        if (s == MVTV_OK) s = alloc(ptr, n);
+    };
+    if (hipStreamCreateWithFlags(&P->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete P;
+        return fail(MVTV_HIP_ERROR, "hipStreamCreate failed");
+    }
+    A(&P->oty, N);
+    A(&P->theta, N);
+    A(&P->edges, size_t(nb) * N);
+    A(&P->ga, N);
+    A(&P->gu, N);
+    A(&P->guprev, N);
+    A(&P->r, N);
+    A(&P->p, N);
+    A(&P->q, N);
+    A(&P->partials, size_t(kMaxGrid) * kMaxRed);
+    A(&P->red, 16);
+    if (s == MVTV_OK && hipMalloc(reinterpret_cast<void**>(&P->st), sizeof(PcgState)) != hipSuccess)
+        s = fail(MVTV_OUT_OF_MEMORY, "hipMalloc(PcgState)");
+    if (s == MVTV_OK && hipHostMalloc(reinterpret_cast<void**>(&P->host_red), 16 * sizeof(double) + sizeof(PcgState)) != hipSuccess)
+        s = fail(MVTV_OUT_OF_MEMORY, "hipHostMalloc");
+    if (s != MVTV_OK) {
+        free_all(P);
+        delete P;
+        return s;
+    }
+    P->host_st = reinterpret_cast<PcgState*>(P->host_red + 16);
+    s = mvtv_problem_set_data(P, d->oty, d->wdiag);
+    if (s != MVTV_OK) {
+        free_all(P);
+        delete P;
+        return s;
+    }
+    *out = P;
+    return MVTV_OK;
+}
+
+void mvtv_problem_destroy(mvtv_problem* P) {
+    if (!P) return;
+    DeviceGuard dg(P->device);
+    (void)hipStreamSynchronize(P->stream);
+    free_all(P);
+    delete P;
+}
+
+int64_t mvtv_problem_nodes(const mvtv_problem* P) { return P ? int64_t(P->g.N) : 0; }
+int64_t mvtv_problem_edges(const mvtv_problem* P) { return P ? P->E : 0; }
+int32_t mvtv_problem_blocks(const mvtv_problem* P) { return P ? P->g.nb : 0; }
+
+mvtv_status mvtv_problem_block_info(const mvtv_problem* P, int32_t k, int32_t* code, int32_t* sprime, double* weight) {
+    if (!P || k < 0 || k >= P->g.nb) return fail(MVTV_BAD_ARG, "block index");
+    if (code) *code = P->codes[k];
+    if (sprime) *sprime = P->sprime[k];
+    if (weight) *weight = P->g.w[k];
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_problem_set_data(mvtv_problem* P, const double* oty, const double* wdiag) {
+    if (!P || !oty) return fail(MVTV_BAD_ARG, "null problem/oty");
+    DeviceGuard dg(P->device);
+    const size_t bytes = size_t(P->g.N) * sizeof(double);
+    HIP_TRY(hipMemcpyAsync(P->oty, oty, bytes, hipMemcpyHostToDevice, P->stream));
+    if (wdiag) {
+        if (!P->wdiag) MVTV_TRY(alloc(&P->wdiag, P->g.N));
+        HIP_TRY(hipMemcpyAsync(P->wdiag, wdiag, bytes, hipMemcpyHostToDevice, P->stream));
+        P->wmode = W_DIAG;
+    } else {
+        P->wmode = W_IDENTITY;
+    }
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_state_set(mvtv_problem* P, const double* theta, const double* u, double rho) {
+    if (!P || !theta) return fail(MVTV_BAD_ARG, "null problem/theta");
+    DeviceGuard dg(P->device);
+    HIP_TRY(hipMemcpyAsync(P->theta, theta, size_t(P->g.N) * sizeof(double), hipMemcpyHostToDevice, P->stream));
+    if (u) {
+        MVTV_TRY(import_edges(P, u, P->edges));
+        P->u_default = false;
+    } else {
+        P->u_default = true;
+    }
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    P->edge_mode = U_EXPLICIT;
+    P->t_z = 0.0;
+    P->c_state = 1.0;
+    P->rho = rho;
+    P->have_state = true;
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_state_get(mvtv_problem* P, double* theta, double* u, double* rho) {
+    if (!P) return fail(MVTV_BAD_ARG, "null problem");
+    MVTV_TRY(ensure_state(P));
+    DeviceGuard dg(P->device);
+    if (theta) {
+        HIP_TRY(hipMemcpyAsync(theta, P->theta, size_t(P->g.N) * sizeof(double), hipMemcpyDeviceToHost, P->stream));
+        HIP_TRY(hipStreamSynchronize(P->stream));
+    }
+    if (u) {
+        if (P->u_default) return fail(MVTV_BAD_ARG, "u is the variant default and has not been formed yet");
+        MVTV_TRY(export_edges(P, P->edges, u, P->edge_mode, P->t_z, P->c_state));
+    }
+    if (rho) *rho = P->rho;
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double lambda, mvtv_admm_stats* stats) {
+    if (!P || !opts_in) return fail(MVTV_BAD_ARG, "null problem/opts");
+    MVTV_TRY(ensure_state(P));
+    if (!(lambda >= 0.0)) return fail(MVTV_BAD_ARG, "lambda must be >= 0");
+    const auto t0 = std::chrono::steady_clock::now();
+    DeviceGuard dg(P->device);
+    const mvtv_admm_opts& o = *opts_in;
+    const int variant = o.variant;
+    if (variant < 0 || variant > 2) return fail(MVTV_BAD_ARG, "variant");
+    const double tol = variant_tol(o);
+    const int max_counter = variant_maxc(o);
+    const double rtol = o.pcg_rtol > 0 ? o.pcg_rtol : 1e-10;
+    const int pcg_maxit = o.pcg_max_iter > 0 ? o.pcg_max_iter : 20000;
+    const Launch L = P->L();
+    const double N = double(P->g.N), E = double(P->E);
+
+    // ---- initial state: u explicit in the edge buffer, alpha_0 = D theta_0 ------------------
+    double rho;
+    if (variant == MVTV_VARIANT_RCPP) rho = P->rho;                      // rho_init (:100)
+    else if (variant == MVTV_VARIANT_CPP) rho = double(int(lambda));     // int rho = lambda (:108)
+    else rho = lambda;                                                   // rho = tune (py :55)
+    double sigma = std::isnan(o.sigma) ? (variant == MVTV_VARIANT_RCPP ? rho : lambda) : o.sigma;
+    if (P->edge_mode == U_FROM_Z) {
+        HIP_TRY(launch_edges_z_to_u(P->stream, P->edges, uint64_t(P->g.nb) * P->g.N, P->t_z, P->c_state));
+        P->edge_mode = U_EXPLICIT;
+        P->c_state = 1.0;
+    }
+    if (P->u_default) {
+        const double u0 = variant == MVTV_VARIANT_RCPP ? 0.0 : 1.0 / lambda;   // A :101, C :62
+        HIP_TRY(launch_edges_fill_valid(P->g, P->order, L, P->edges, u0));
+        P->u_default = false;
+    }
+    double* gprev = P->guprev;
+    double* gnew = P->gu;
+    // g_uprev = D^T u0, g_alpha = D^T D theta0  ->  b_1 = oty + rho D^T (alpha0 + u0)
+    int h = P->tstart(MVTV_K_GATHER);
+    HIP_TRY(launch_gather(P->g, P->order, U_EXPLICIT, L, P->edges, 0.0, nullptr, gprev, nullptr, 1.0, P->partials));
+    P->tstop(h);
+    h = P->tstart(MVTV_K_OTHER);
+    HIP_TRY(launch_apply_A(P->g, L, 1.0, W_NONE, nullptr, P->theta, P->ga, nullptr, nullptr));
+    P->tstop(h);
+    double c_prev = 1.0, t_z = 0.0;
+    int mode = U_EXPLICIT;
+
+    const bool track_theta = variant != MVTV_VARIANT_RCPP;
+    double dtheta = 0.0;
+    if (track_theta) {
+        if (!P->thold) MVTV_TRY(alloc(&P->thold, P->g.N));
+        HIP_TRY(launch_fill(P->stream, P->thold, o.ymean - (variant == MVTV_VARIANT_CPP ? 0.1 : 1.0), P->g.N));
+        HIP_TRY(launch_maxabsdiff(P->g, L, P->theta, P->thold, P->partials));
+        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 1, 0, P->red, P->st));
+        HIP_TRY(hipMemcpyAsync(P->host_red, P->red, sizeof(double), hipMemcpyDeviceToHost, P->stream));
+        MVTV_TRY(P->sync());
+        dtheta = P->host_red[0];
+    }
+
+    mvtv_admm_stats S{};
+    S.status = MVTV_OK;
+    double dual_norm = 1.0, primal_norm = 1.0, eps_dual = tol, eps_primal = tol;
+    int counter = 1, it = 0;
+    mvtv_status status = MVTV_OK;
+    for (;;) {
+        // ---- loop condition, evaluated at the top as in the reference -----------------------
+        if (o.fixed_iters > 0) {
+            if (it >= o.fixed_iters) break;
+        } else if (variant == MVTV_VARIANT_RCPP) {
+            if (!(dual_norm > eps_dual || primal_norm > eps_primal)) break;   // :110
+        } else {
+            if (!(dtheta > tol)) break;   // any(|theta - thetaold| > TOL): A :113, C :69
+            if (variant == MVTV_VARIANT_PY && it >= max_counter) {
+                status = MVTV_MAXITER;
+                break;
+            }
+        }
+        if (track_theta) HIP_TRY(hipMemcpyAsync(P->thold, P->theta, size_t(P->g.N) * sizeof(double),
+                                                hipMemcpyDeviceToDevice, P->stream));
+        // ---- theta-update: (W + sigma D^T D) theta = oty + rho D^T (alpha + u) ----------------
+        int pit = 0;
+        double relres = 0.0;
+        MVTV_TRY(pcg_solve(P, sigma, P->oty, P->ga, rho, gprev, rho * c_prev, P->theta, rtol, pcg_maxit, &pit, &relres));
+        S.pcg_iters += pit;
+        S.pcg_iters_max = std::max(S.pcg_iters_max, pit);
+        if (pit >= pcg_maxit && !(relres <= rtol)) {
+            S.pcg_unconverged += 1;
+            if (o.pcg_strict) {
+                status = MVTV_PCG_NOT_CONVERGED;
+                fail(status, "PCG hit pcg_max_iter");
+                break;
+            }
+        }
+        // ---- z-update (soft threshold) and dual update over all edges -----------------------
+        const double t_new = rho != 0.0 ? lambda / rho : INFINITY;
+        h = P->tstart(MVTV_K_EDGE_UPDATE);
+        HIP_TRY(launch_edge_update(P->g, P->order, mode, L, P->theta, P->edges, t_z, c_prev, t_new,
+                                   track_theta ? P->thold : nullptr, P->partials));
+        P->tstop(h);
+        h = P->tstart(MVTV_K_REDUCE);
+        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, ER_N, 1, 0, P->red, P->st));
+        P->tstop(h);
+        mode = U_FROM_Z;
+        t_z = t_new;
+        // ---- D^T alpha, D^T u and the dual residual norms ---------------------------------------
+        h = P->tstart(MVTV_K_GATHER);
+        HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, L, P->edges, t_z, P->ga, gnew, gprev, c_prev, P->partials));
+        P->tstop(h);
+        h = P->tstart(MVTV_K_REDUCE);
+        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, GR_N, 0, 0, P->red + ER_N, P->st));
+        P->tstop(h);
+        HIP_TRY(hipMemcpyAsync(P->host_red, P->red, (ER_N + GR_N) * sizeof(double), hipMemcpyDeviceToHost, P->stream));
+        MVTV_TRY(P->sync());
+        const double* R = P->host_red;
+        const double r_norm = std::sqrt(R[ER_R2]);
+        it += 1;
+        counter += 1;
+        double c_next = 1.0, rho_next = rho;
+        if (variant == MVTV_VARIANT_RCPP) {
+            // :117-125
+            dual_norm = std::fabs(rho) * std::sqrt(R[ER_N + GR_S2B]);
+            primal_norm = r_norm;
+            eps_dual = tol * (std::sqrt(N) + std::sqrt(R[ER_N + GR_GU2]));
+            eps_primal = tol * (std::sqrt(E) + std::max(std::sqrt(R[ER_D2]), std::sqrt(R[ER_A2])));
+            const double tau = 2.0;
+            if (primal_norm > 10 * dual_norm) {
+                rho_next = tau * rho;
+                c_next = 1.0 / tau;
+            } else if (dual_norm > 10 * primal_norm) {
+                rho_next = 1.0 / tau * rho;
+                c_next = tau;
+            }
+            S.s_norm = dual_norm;
+            S.eps_pri = eps_primal;
+            S.eps_dual = eps_dual;
+        } else if (variant == MVTV_VARIANT_CPP) {
+            // :118-126 — s uses the new alpha and the old u; rho is an int
+            const double s_norm = std::fabs(rho) * std::sqrt(R[ER_N + GR_S2A]);
+            dtheta = R[ER_DTH];
+            S.s_norm = s_norm;
+            if (o.fixed_iters <= 0 && counter > max_counter) {
+                status = MVTV_MAXITER;
+                fail(status, "Failed to converge!");
+                rho_next = rho;
+            } else {
+                if (r_norm > 20 * s_norm) {
+                    rho_next = 20 * rho;
+                    c_next = 0.05;
+                } else if (s_norm > 20 * r_norm) {
+                    rho_next = 0.1 * rho;
+                    c_next = 10.0;
+                }
+                rho_next = double(int(rho_next));
+            }
+        } else {
+            dtheta = R[ER_DTH];
+        }
+        S.r_norm = r_norm;
+        S.dtheta_max = dtheta;
+        std::swap(gprev, gnew);
+        c_prev = c_next;
+        rho = rho_next;
+        if (variant == MVTV_VARIANT_RCPP) sigma = rho;   // spcrosses = crossO + rho crossD (:126)
+        if (status == MVTV_MAXITER) break;
+        if (variant == MVTV_VARIANT_RCPP && o.fixed_iters <= 0 && counter > max_counter) {
+            if (o.verbose) std::printf("ADMM reached max_counter at lambda = %g\n", lambda);
+            status = MVTV_MAXITER;
+            break;
+        }
+    }
+    if (o.verbose) std::printf("Lambda= %g, Counter = %d\n", lambda, counter);
+    // keep the resident state consistent: g_uprev buffer is P->guprev
+    if (gprev != P->guprev) std::swap(P->guprev, P->gu);
+    P->edge_mode = mode;
+    P->t_z = t_z;
+    P->c_state = c_prev;
+    P->rho = rho;
+    S.iters = it;
+    S.rho = rho;
+    S.status = status;
+    S.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = S;
+    return status;
+}
+
+mvtv_status mvtv_admm(mvtv_problem* P, const mvtv_admm_opts* opts, double lambda, double* theta_inout,
+                      double* u_inout, double* rho_inout, mvtv_admm_stats* stats) {
+    if (!P || !opts || !theta_inout) return fail(MVTV_BAD_ARG, "null problem/opts/theta");
+    const double rho0 = rho_inout ? *rho_inout : lambda / 5.0;
+    MVTV_TRY(mvtv_state_set(P, theta_inout, u_inout, rho0));
+    mvtv_status s = mvtv_admm_run(P, opts, lambda, stats);
+    if (s != MVTV_OK && s != MVTV_MAXITER) return s;
+    mvtv_status g = mvtv_state_get(P, theta_inout, u_inout, rho_inout);
+    if (g != MVTV_OK) return g;
+    return s;
+}
+
+mvtv_status mvtv_fitted(mvtv_problem* P, const int64_t* mesh_index, int64_t n, double* fitted) {
+    if (!P || (n > 0 && (!mesh_index || !fitted))) return fail(MVTV_BAD_ARG, "null argument");
+    if (n == 0) return MVTV_OK;
+    DeviceGuard dg(P->device);
+    int64_t* didx = nullptr;
+    double* dout = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&didx), size_t(n) * sizeof(int64_t)));
+    if (hipMalloc(reinterpret_cast<void**>(&dout), size_t(n) * sizeof(double)) != hipSuccess) {
+        (void)hipFree(didx);
+        return fail(MVTV_OUT_OF_MEMORY, "hipMalloc");
+    }
+    mvtv_status s = MVTV_OK;
+    for (int64_t t = 0; t < n; ++t)
+        if (mesh_index[t] < 0 || mesh_index[t] >= int64_t(P->g.N)) s = fail(MVTV_BAD_ARG, "mesh index out of range");
+    if (s == MVTV_OK) {
+        if (hipMemcpyAsync(didx, mesh_index, size_t(n) * sizeof(int64_t), hipMemcpyHostToDevice, P->stream) != hipSuccess ||
+            launch_gather_index(P->stream, P->theta, didx, n, dout) != hipSuccess ||
+            hipMemcpyAsync(fitted, dout, size_t(n) * sizeof(double), hipMemcpyDeviceToHost, P->stream) != hipSuccess ||
+            hipStreamSynchronize(P->stream) != hipSuccess)
+            s = fail(MVTV_HIP_ERROR, "fitted: HIP failure");
+    }
+    (void)hipFree(didx);
+    (void)hipFree(dout);
+    return s;
+}
+
+// ------------------------------------------------------------------------------ operators
+mvtv_status mvtv_apply_D(mvtv_problem* P, const double* theta, double* d_out) {
+    if (!P || !theta || !d_out) return fail(MVTV_BAD_ARG, "null argument");
+    DeviceGuard dg(P->device);
+    double *x = nullptr, *e = nullptr;
+    MVTV_TRY(alloc(&x, P->g.N));
+    mvtv_status s = alloc(&e, size_t(P->g.nb) * P->g.N);
+    if (s == MVTV_OK) {
+        if (hipMemcpyAsync(x, theta, size_t(P->g.N) * sizeof(double), hipMemcpyHostToDevice, P->stream) != hipSuccess ||
+            launch_apply_D_padded(P->g, P->order, P->L(), x, e) != hipSuccess)
+            s = fail(MVTV_HIP_ERROR, "apply_D");
+        if (s == MVTV_OK) s = export_edges(P, e, d_out, U_EXPLICIT, 0.0, 1.0);
+    }
+    (void)hipFree(x);
+    if (e) (void)hipFree(e);
+    return s;
+}
+
+mvtv_status mvtv_apply_Dt(mvtv_problem* P, const double* v, double* g_out) {
+    if (!P || !v || !g_out) return fail(MVTV_BAD_ARG, "null argument");
+    DeviceGuard dg(P->device);
+    double *gq = nullptr, *e = nullptr;
+    MVTV_TRY(alloc(&gq, P->g.N));
+    mvtv_status s = alloc(&e, size_t(P->g.nb) * P->g.N);
+    if (s == MVTV_OK) s = import_edges(P, v, e);
+    if (s == MVTV_OK) {
+        if (launch_gather(P->g, P->order, U_EXPLICIT, P->L(), e, 0.0, nullptr, gq, nullptr, 1.0, P->partials) != hipSuccess ||
+            hipMemcpyAsync(g_out, gq, size_t(P->g.N) * sizeof(double), hipMemcpyDeviceToHost, P->stream) != hipSuccess ||
+            hipStreamSynchronize(P->stream) != hipSuccess)
+            s = fail(MVTV_HIP_ERROR, "apply_Dt");
+    }
+    (void)hipFree(gq);
+    if (e) (void)hipFree(e);
+    return s;
+}
+
+mvtv_status mvtv_apply_A(mvtv_problem* P, double sigma, const double* x, double* q_out) {
+    if (!P || !x || !q_out) return fail(MVTV_BAD_ARG, "null argument");
+    DeviceGuard dg(P->device);
+    double *dx = nullptr, *dq = nullptr;
+    MVTV_TRY(alloc(&dx, P->g.N));
+    mvtv_status s = alloc(&dq, P->g.N);
+    if (s == MVTV_OK) {
+        const size_t bytes = size_t(P->g.N) * sizeof(double);
+        if (hipMemcpyAsync(dx, x, bytes, hipMemcpyHostToDevice, P->stream) != hipSuccess ||
+            launch_apply_A(P->g, P->L(), sigma, P->wmode, P->wdiag, dx, dq, nullptr, nullptr) != hipSuccess ||
+            hipMemcpyAsync(q_out, dq, bytes, hipMemcpyDeviceToHost, P->stream) != hipSuccess ||
+            hipStreamSynchronize(P->stream) != hipSuccess)
+            s = fail(MVTV_HIP_ERROR, "apply_A");
+    }
+    (void)hipFree(dx);
+    if (dq) (void)hipFree(dq);
+    return s;
+}
+
+mvtv_status mvtv_solve(mvtv_problem* P, double sigma, const double* b, double* x_inout, double rtol, int32_t max_iter,
+                       int32_t* iters, double* relres) {
+    if (!P || !b || !x_inout) return fail(MVTV_BAD_ARG, "null argument");
+    DeviceGuard dg(P->device);
+    double *db = nullptr, *dx = nullptr;
+    MVTV_TRY(alloc(&db, P->g.N));
+    mvtv_status s = alloc(&dx, P->g.N);
+    int it = 0;
+    double rr = 0.0;
+    if (s == MVTV_OK) {
+        const size_t bytes = size_t(P->g.N) * sizeof(double);
+        if (hipMemcpyAsync(db, b, bytes, hipMemcpyHostToDevice, P->stream) != hipSuccess ||
+            hipMemcpyAsync(dx, x_inout, bytes, hipMemcpyHostToDevice, P->stream) != hipSuccess)
+            s = fail(MVTV_HIP_ERROR, "solve upload");
+        if (s == MVTV_OK)
+            s = pcg_solve(P, sigma, db, db, 0.0, db, 0.0, dx, rtol > 0 ? rtol : 1e-10, max_iter > 0 ? max_iter : 20000,
+                          &it, &rr);
+        if (s == MVTV_OK && (hipMemcpyAsync(x_inout, dx, bytes, hipMemcpyDeviceToHost, P->stream) != hipSuccess ||
+                             hipStreamSynchronize(P->stream) != hipSuccess))
+            s = fail(MVTV_HIP_ERROR, "solve download");
+    }
+    if (iters) *iters = it;
+    if (relres) *relres = rr;
+    (void)hipFree(db);
+    if (dx) (void)hipFree(dx);
+    return s;
+}
+
+// ------------------------------------------------------------------------------ instrumentation
+mvtv_status mvtv_timing_enable(mvtv_problem* P, int32_t on) {
+    if (!P) return fail(MVTV_BAD_ARG, "null problem");
+    DeviceGuard dg(P->device);
+    MVTV_TRY(P->sync());
+    P->timing = on != 0;
+    for (int k = 0; k < MVTV_K_COUNT; ++k) {
+        P->ms[k] = 0.0;
+        P->launches[k] = 0;
+    }
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int64_t* launches, double* bytes) {
+    if (!P || kid < 0 || kid >= MVTV_K_COUNT) return fail(MVTV_BAD_ARG, "kernel id");
+    DeviceGuard dg(P->device);
+    MVTV_TRY(P->sync());
+    const double N = double(P->g.N), E = double(P->E), w = P->wmode == W_DIAG ? 1.0 : 0.0;
+    // algorithmic bytes per launch (each array element read or written once)
+    double b = 0.0;
+    switch (kid) {
+        case MVTV_K_EDGE_UPDATE: b = 8.0 * (N + 2.0 * E); break;        // theta in, z in/out
+        case MVTV_K_GATHER: b = 8.0 * (E + 3.0 * N); break;             // z in, g_uprev in, g_alpha/g_u out
+        case MVTV_K_PCG_INIT: b = 8.0 * ((6.0 + w) * N); break;         // oty, ga, gb, x (+W) in, r, p out
+        case MVTV_K_PCG_APPLY: b = 8.0 * ((2.0 + w) * N); break;        // p (+W) in, q out
+        case MVTV_K_PCG_UPDATE: b = 8.0 * ((6.0 + w) * N); break;       // x, r, p, q (+W) in, x, r out
+        case MVTV_K_PCG_DIRECTION: b = 8.0 * ((3.0 + w) * N); break;    // r, p (+W) in, p out
+        default: b = 0.0;
+    }
+    if (total_ms) *total_ms = P->ms[kid];
+    if (launches) *launches = P->launches[kid];
+    if (bytes) *bytes = b;
+    return MVTV_OK;
+}
+
+const char* mvtv_kernel_name(int32_t kid) {
+    static const char* names[MVTV_K_COUNT] = {"edge_update", "gather_Dt", "pcg_init", "pcg_apply_A",
+                                               "pcg_update", "pcg_direction", "reduce", "other"};
+    return (kid >= 0 && kid < MVTV_K_COUNT) ? names[kid] : "?";
+}
+
+}  // extern "C"

@@ -1,0 +1,140 @@
+// mvtv_internal.h — device-side geometry, block tables and launcher declarations.
+//
+// The difference operator D of the reference (create_D, cpp-code/utils.cpp:245-269;
+// rcpp-code/MultivarTV/src/utils.cpp:218-232; code/utils.py:138-149) is never
+// materialised. It is described by the mesh shape plus, per row block k, its
+// binary code b (MSB = dim 0), the effective difference set S'(b) (the
+// dim-0-first mixed-partial quirk) and its weight w_k.
+// D^T D is then the sum over subsets S of cS[S] * (tensor product of 1-D Neumann
+// Laplacians over S), cS[S] = sum of w_k^2 over blocks with S'_k == S.
+#pragma once
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+namespace mvtv {
+
+// Unsigned 32-bit division by an invariant divisor (Granlund-Montgomery):
+// q = (umulhi(n, mul) + n) >> shift, evaluated with a 64-bit add so it holds for every n < 2^32.
+struct FastDiv {
+    uint32_t d, mul, shift;
+    __host__ __device__ FastDiv() : d(1), mul(0), shift(0) {}
+    __host__ explicit FastDiv(uint32_t div) : d(div) {
+        shift = 0;
+        while ((uint64_t(1) << shift) < div) ++shift;
+        mul = uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << shift) - div)) / div + 1);
+        if (div == 1) { mul = 0; shift = 0; }
+    }
+    __host__ __device__ inline uint32_t div(uint32_t n) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        uint32_t hi = __umulhi(n, mul);
+#else
+        uint32_t hi = uint32_t((uint64_t(n) * mul) >> 32);
+#endif
+        return uint32_t((uint64_t(hi) + n) >> shift);
+    }
+};
+
+constexpr int kMaxDims = 4;
+constexpr int kMaxBlocks = 15;
+
+// Effective difference set of binary code b in p dims, as a dim-bit mask (bit j = dim j).
+__host__ __device__ constexpr int sprime_mask(int b, int p) {
+    int S = 0, cnt = 0;
+    for (int j = 0; j < p; ++j)
+        if ((b >> (p - 1 - j)) & 1) { S |= 1 << j; ++cnt; }
+    if (cnt <= 1 || (S & 1)) return S;
+    int lo = 0;
+    while (!((S >> lo) & 1)) ++lo;
+    return (S & ~(1 << lo)) | 1;
+}
+
+// Binary code of row block k for a given order (0 = C++ create_D, 1 = Python create_D).
+__host__ __device__ constexpr int block_code(int k, int p, int order) {
+    return order == 0 ? (k == 0 ? (1 << p) - 1 : k) : k + 1;
+}
+
+struct Geom {
+    int32_t p;
+    int32_t nb;            // number of row blocks of D
+    uint32_t N;            // nodes
+    uint32_t m[kMaxDims];
+    uint32_t stride[kMaxDims];
+    FastDiv fd[kMaxDims - 1];  // division by m0, m1, m2
+    double w[kMaxBlocks];      // block weights, in block order
+    double cS[16];             // D^T D coefficient per subset mask S of dims
+};
+
+// Per-node multi-index decode (column-major, dim 0 fastest).
+template <int P>
+__device__ __forceinline__ void decode(const Geom& g, uint32_t i, uint32_t (&c)[kMaxDims]) {
+    uint32_t rest = i;
+#pragma unroll
+    for (int j = 0; j < P - 1; ++j) {
+        uint32_t q = g.fd[j].div(rest);
+        c[j] = rest - q * g.m[j];
+        rest = q;
+    }
+    c[P - 1] = rest;
+}
+
+// Reductions produced by each kernel family (indices into the reduction vector).
+enum EdgeRed { ER_R2 = 0, ER_D2 = 1, ER_A2 = 2, ER_DTH = 3, ER_N = 4 };          // ER_DTH is a max
+enum GatherRed { GR_GU2 = 0, GR_S2B = 1, GR_S2A = 2, GR_N = 3 };
+enum PcgRed { PR_B2 = 0, PR_RZ = 1, PR_R2 = 2, PR_N = 3 };
+
+struct PcgState {
+    double gamma;    // r.z
+    double alpha, beta;
+    double rnorm2, bnorm2;
+    double rtol2;
+    int32_t iter, maxit;
+    int32_t done;
+    int32_t pad;
+};
+
+enum UMode { U_EXPLICIT = 0, U_FROM_Z = 1 };
+enum WMode { W_NONE = 0, W_IDENTITY = 1, W_DIAG = 2 };
+
+constexpr int kThreads = 256;
+constexpr int kMaxGrid = 2048;   // grid-stride cap for streaming kernels (8 workgroups per CU)
+constexpr int kMaxRed = 4;
+
+// ------------------------------------------------------------------ launchers
+struct Launch {
+    hipStream_t stream;
+    int grid;
+};
+
+hipError_t launch_edge_update(const Geom& g, int order, int umode, const Launch& L, const double* theta,
+                              double* edges, double t_old, double c_old, double t_new, const double* theta_old,
+                              double* partials);
+hipError_t launch_gather(const Geom& g, int order, int umode, const Launch& L, const double* edges, double t,
+                         double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials);
+hipError_t launch_apply_A(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
+                          const double* x, double* q, double* partials, const PcgState* st);
+hipError_t launch_pcg_init(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
+                           const double* oty, const double* ga, double ca, const double* gb, double cb,
+                           const double* x, double* r, double* p, double* partials);
+hipError_t launch_pcg_update(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
+                             double* x, double* r, const double* p, const double* q, const PcgState* st,
+                             double* partials);
+hipError_t launch_pcg_pupdate(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
+                              const double* r, double* p, const PcgState* st);
+// op: 0 plain (sums, ER_DTH-style max in the last nmax slots), 1 pcg-init, 2 pcg-after-Ap, 3 pcg-after-update
+hipError_t launch_finalize(hipStream_t s, const double* partials, int nparts, int nr, int nmax, int op, double* out,
+                           PcgState* st, double rtol2 = 0.0, int maxit = 0);
+hipError_t launch_maxabsdiff(const Geom& g, const Launch& L, const double* a, const double* b, double* partials);
+hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n);
+// compact <-> padded edge layouts for one block segment [e0, e0+cnt) of block k
+hipError_t launch_edges_import(const Geom& g, int order, hipStream_t s, int k, uint64_t e0, uint64_t cnt,
+                               const double* compact, double* padded);
+hipError_t launch_edges_export(const Geom& g, int order, hipStream_t s, int k, uint64_t e0, uint64_t cnt,
+                               const double* padded, double* compact, int umode, double t, double c);
+hipError_t launch_edges_z_to_u(hipStream_t s, double* edges, uint64_t n, double t, double c);
+// edges = value on every real edge, 0 on padding (variant u0 fills: B 0, A and C 1/lambda)
+hipError_t launch_edges_fill_valid(const Geom& g, int order, const Launch& L, double* edges, double value);
+hipError_t launch_apply_D_padded(const Geom& g, int order, const Launch& L, const double* theta, double* edges);
+hipError_t launch_gather_index(hipStream_t s, const double* theta, const int64_t* idx, int64_t n, double* out);
+
+}  // namespace mvtv

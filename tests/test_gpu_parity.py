@@ -1,0 +1,154 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the golden fixtures.
+
+Tolerances (fp64): operators D, D^T, A agree with the oracle's sparse products to
+1e-13 relative (summation order differs); PCG theta-solves run at rtol 1e-12, so
+ADMM iterates agree with the SuperLU oracle to 1e-8 relative of max|theta| and
+iteration counts / final rho must match exactly.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import mvtv_oracle as O
+
+mv = pytest.importorskip("multivartv_amd")
+pytestmark = pytest.mark.gpu
+
+RTOL_OP = 1e-13
+RTOL_THETA = 1e-8
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / max(1e-300, np.max(np.abs(b))))
+
+
+SHAPES = [([9], None, "cpp", False), ([7, 5], [0.3, 0.7], "cpp", False), ([6, 6, 6], [0.5, 0.25, 0.125], "cpp", False),
+          ([5, 5, 7], [0.2, 0.3, 0.4], "cpp", True), ([4, 4, 4, 5], [0.5, 0.25, 0.125, 0.3], "cpp", False),
+          ([6, 5], None, "py", False), ([5, 5, 5], [0.5, 0.25, 0.125], "py", False), ([4, 4, 4, 4], None, "py", False)]
+
+
+def _problem(m, deltas, order, unit, wdiag=None, seed=0):
+    rng = np.random.default_rng(seed)
+    N = int(np.prod(m))
+    oty = rng.standard_normal(N)
+    o = mv.ORDER_CPP if order == "cpp" else mv.ORDER_PY
+    weighted = (deltas is not None) and not unit
+    P = mv.Problem(m, oty, wdiag=wdiag, deltas=deltas if deltas is not None else [1.0] * len(m), order=o,
+                   weighted=weighted)
+    D = O.build_D(m, O.block_table(len(m), deltas if weighted else None, order, unit_weights=unit))
+    return P, D, oty
+
+
+@pytest.mark.parametrize("m,deltas,order,unit", SHAPES)
+def test_operators(m, deltas, order, unit):
+    rng = np.random.default_rng(1)
+    N = int(np.prod(m))
+    w = rng.uniform(0.0, 3.0, N).round()
+    P, D, _ = _problem(m, deltas, order, unit, wdiag=w)
+    assert P.E == D.shape[0]
+    th = rng.standard_normal(N)
+    assert _rel(P.apply_D(th), D @ th) <= RTOL_OP
+    v = rng.standard_normal(D.shape[0])
+    assert _rel(P.apply_Dt(v), D.T @ v) <= RTOL_OP
+    for sigma in (0.0, 0.37, 25.6):
+        assert _rel(P.apply_A(sigma, th), O.apply_A(D, w, sigma, th)) <= RTOL_OP
+    P.close()
+
+
+@pytest.mark.parametrize("m,deltas,order,unit", SHAPES[:6])
+def test_pcg_solve(m, deltas, order, unit):
+    rng = np.random.default_rng(2)
+    N = int(np.prod(m))
+    P, D, _ = _problem(m, deltas, order, unit)
+    b = rng.standard_normal(N)
+    sigma = 3.2
+    ref = O._solver(np.ones(N), (D.T @ D).tocsc(), sigma).solve(b)
+    x, it, rr = P.solve(sigma, b, rtol=1e-13)
+    assert rr <= 1e-13
+    assert _rel(x, ref) <= 1e-10
+    P.close()
+
+
+def test_dim_mismatch_raises():
+    with pytest.raises(mv.DimMismatchError):
+        mv.Problem([4, 3, 5], np.zeros(60), deltas=[1, 1, 1])
+    mv.Problem([4, 4, 5], np.zeros(80), deltas=[1, 1, 1]).close()
+
+
+RCPP = ["rcpp_1d_200", "rcpp_2d_32", "rcpp_2d_24x40", "rcpp_3d_12", "rcpp_3d_8x8x11", "rcpp_4d_5", "rcpp_2d_scat"]
+
+
+def _rcpp_problem(meta, g):
+    W = g["W"]
+    wdiag = None if np.all(W == 1.0) else W
+    return mv.Problem(meta["m"], g["Oty"], wdiag=wdiag, deltas=meta["deltas"], order=mv.ORDER_CPP)
+
+
+@pytest.mark.parametrize("name", RCPP)
+def test_rcpp_trajectory(name):
+    meta, g = load_golden(name)
+    P = _rcpp_problem(meta, g)
+    for k in (1, 5, 20):
+        th, u, rho, st = P.admm(meta["lam"], g["theta0"], u=np.zeros(P.E), rho=meta["rho0"],
+                                fixed_iters=k, pcg_rtol=1e-13)
+        assert _rel(th, g[f"snap{k}"]) <= RTOL_THETA, k
+        assert st["iters"] == k
+    assert rho == float(g["fixed_rho"])
+    assert np.max(np.abs(u - g["fixed_u"])) <= RTOL_THETA * max(1.0, np.max(np.abs(g["fixed_u"])))
+    hist = g["fixed_hist"][-1]
+    assert st["r_norm"] == pytest.approx(hist[0], rel=1e-6, abs=1e-12)
+    assert st["s_norm"] == pytest.approx(hist[1], rel=1e-6, abs=1e-12)
+    assert st["eps_pri"] == pytest.approx(hist[2], rel=1e-10)
+    assert st["eps_dual"] == pytest.approx(hist[3], rel=1e-10)
+    P.close()
+
+
+@pytest.mark.parametrize("name", RCPP)
+def test_rcpp_converged(name):
+    meta, g = load_golden(name)
+    P = _rcpp_problem(meta, g)
+    th, u, rho, st = P.admm(meta["lam"], g["theta0"], u=np.zeros(P.E), rho=meta["rho0"], pcg_rtol=1e-13)
+    assert st["iters"] == meta["iters"]
+    assert rho == meta["rho"]
+    assert _rel(th, g["theta"]) <= RTOL_THETA
+    assert np.max(np.abs(u - g["u"])) <= RTOL_THETA * max(1.0, np.max(np.abs(g["u"])))
+    P.close()
+
+
+def test_rcpp_warm_path_resident():
+    meta, g = load_golden("rcpp_path_2d_16")
+    y = g["y"]
+    P = mv.Problem(meta["m"], y, deltas=meta["deltas"], order=mv.ORDER_CPP)
+    P.state_set(np.full(256, y.mean()), np.zeros(P.E), meta["lams"][0] / 5.0)
+    for k, lam in enumerate(meta["lams"]):
+        st = P.run(lam, pcg_rtol=1e-13)
+        th, u, rho = P.state_get()
+        assert st["iters"] == int(g[f"iters{k}"])
+        assert rho == float(g[f"rho{k}"])
+        assert _rel(th, g[f"theta{k}"]) <= RTOL_THETA
+        assert np.max(np.abs(u - g[f"u{k}"])) <= RTOL_THETA * max(1.0, np.max(np.abs(g[f"u{k}"])))
+    P.close()
+
+
+@pytest.mark.parametrize("name", ["cpp_2d_16", "cpp_3d_8_unit", "cpp_2d_12_frac"])
+def test_cpp_variant(name):
+    meta, g = load_golden(name)
+    P = mv.Problem(meta["m"], g["y"], deltas=meta["deltas"], order=mv.ORDER_CPP, weighted=not meta["unit"])
+    th, u, rho, st = P.admm(meta["lam"], g["theta0"], variant=mv.VARIANT_CPP, ymean=meta["ymean"], pcg_rtol=1e-13)
+    assert st["iters"] == meta["iters"]
+    assert rho == meta["rho"]
+    assert _rel(th, g["theta"]) <= RTOL_THETA
+    assert np.max(np.abs(u - g["u"])) <= RTOL_THETA * max(1.0, np.max(np.abs(g["u"])))
+    P.close()
+
+
+@pytest.mark.parametrize("name", ["py_1d_n1000_m1000_lam2", "py_1d_n1000_m250_lam2", "py_1d_n1000_m1000_lam0.5"])
+def test_py_config1(name):
+    """Config 1: 1D n = 1000 against the reference's own solvers.mbs_one output."""
+    meta, g = load_golden(name)
+    P = mv.Problem(meta["m"], g["Oty"], wdiag=g["W"], order=mv.ORDER_PY, weighted=False)
+    ym = float(g["y"].mean())
+    th, _, _, st = P.admm(meta["lam"], np.full(meta["m"][0], ym), variant=mv.VARIANT_PY, ymean=ym,
+                          pcg_rtol=1e-13, return_u=False)
+    assert _rel(th, g["theta"]) <= RTOL_THETA
+    P.close()
