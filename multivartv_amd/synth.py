@@ -13,6 +13,9 @@ cpp-code/utils.cpp:40-52).
 """
 from __future__ import annotations
 
+import os
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
 
 SEED = 0x4D565456
@@ -51,14 +54,19 @@ def lattice_coords(m) -> list[np.ndarray]:
     return [np.arange(mj, dtype=np.float64) / max(mj - 1, 1) for mj in m]
 
 
-def towers(m, sigma: float = 0.5, seed: int = SEED, chunk: int = 1 << 24) -> np.ndarray:
-    """y = towers(x) + sigma * xi on the column-major lattice of shape m (float64, length prod(m))."""
+def towers(m, sigma: float = 0.5, seed: int = SEED, chunk: int = 1 << 22, threads: int = 0) -> np.ndarray:
+    """y = towers(x) + sigma * xi on the column-major lattice of shape m (float64, length prod(m)).
+
+    Chunks are independent (counter-based noise), so large meshes are generated on a
+    thread pool; the result does not depend on ``threads``.
+    """
     m = [int(v) for v in m]
     n = int(np.prod(m))
     y = np.empty(n, dtype=np.float64)
     coords = lattice_coords(m)
     strides = np.cumprod([1] + m[:-1])
-    for start in range(0, n, chunk):
+
+    def work(start):
         cnt = min(chunk, n - start)
         flat = np.arange(start, start + cnt, dtype=np.int64)
         hi = np.ones(cnt, dtype=bool)
@@ -69,6 +77,15 @@ def towers(m, sigma: float = 0.5, seed: int = SEED, chunk: int = 1 << 24) -> np.
             lo &= xj < 0.2
         f = np.where(hi, 1.0, np.where(lo, 0.5, 0.0))
         y[start:start + cnt] = f + sigma * normal_noise(start, cnt, seed)
+
+    starts = range(0, n, chunk)
+    nthreads = threads or min(16, os.cpu_count() or 1)
+    if nthreads > 1 and n > chunk:
+        with ThreadPoolExecutor(nthreads) as ex:
+            list(ex.map(work, starts))
+    else:
+        for s in starts:
+            work(s)
     return y
 
 

@@ -1,0 +1,23 @@
+"""Pin the C oracle (CPU baseline of bench.py) against the SuperLU oracle / golden fixtures."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+c_oracle = pytest.importorskip("oracle.c_oracle")
+
+
+@pytest.mark.parametrize("name", ["rcpp_1d_200", "rcpp_2d_32", "rcpp_2d_scat", "rcpp_3d_12", "rcpp_4d_5"])
+def test_c_oracle_matches_golden(name):
+    meta, g = load_golden(name)
+    W = None if np.all(g["W"] == 1.0) else g["W"]
+    E = c_oracle.num_edges(meta["m"])
+    assert E == meta["E"]
+    th = g["theta0"].copy()
+    u = np.zeros(E)
+    st = c_oracle.admm_rcpp(meta["m"], g["Oty"], meta["lam"], th, u, meta["rho0"], meta["deltas"], W=W,
+                            pcg_rtol=1e-13)
+    assert st["iters"] == meta["iters"]
+    assert st["rho"] == meta["rho"]
+    assert np.max(np.abs(th - g["theta"])) <= 1e-8 * np.max(np.abs(g["theta"]))
+    assert np.max(np.abs(u - g["u"])) <= 1e-8 * max(1.0, np.max(np.abs(g["u"])))
