@@ -153,7 +153,8 @@ typedef enum mvtv_kernel_id {
     MVTV_K_PCG_DIRECTION = 5, /* p = z + b p */
     MVTV_K_REDUCE = 6,        /* partial-sum finalisation / PCG scalars */
     MVTV_K_OTHER = 7,
-    MVTV_K_COUNT = 8
+    MVTV_K_PCG_FUSED = 8,     /* 3-D fused Chronopoulos-Gear iteration: p, A p, r, A M^-1 r, x in one pass */
+    MVTV_K_COUNT = 9
 } mvtv_kernel_id;
 mvtv_status mvtv_timing_enable(mvtv_problem* prob, int32_t on);
 mvtv_status mvtv_timing_get(mvtv_problem* prob, int32_t kernel_id, double* total_ms, int64_t* launches,

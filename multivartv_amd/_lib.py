@@ -18,7 +18,8 @@ MVTV_OK, MVTV_MAXITER, MVTV_BAD_ARG, MVTV_DIM_MISMATCH = 0, 1, 2, 3
 MVTV_HIP_ERROR, MVTV_NO_DEVICE, MVTV_OUT_OF_MEMORY, MVTV_PCG_NOT_CONVERGED = 4, 5, 6, 7
 VARIANT_RCPP, VARIANT_CPP, VARIANT_PY = 0, 1, 2
 ORDER_CPP, ORDER_PY = 0, 1
-KERNELS = ["edge_update", "gather_Dt", "pcg_init", "pcg_apply_A", "pcg_update", "pcg_direction", "reduce", "other"]
+KERNELS = ["edge_update", "gather_Dt", "pcg_init", "pcg_apply_A", "pcg_update", "pcg_direction", "reduce", "other",
+           "pcg_fused3d"]
 
 _dp = C.POINTER(C.c_double)
 

@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -64,10 +65,11 @@ struct mvtv_problem {
     uint64_t blk_len[kMaxBlocks] = {0};
     int64_t E = 0;
     int grid = 1;
+    bool fused3d = true;   // fused Chronopoulos-Gear PCG for p = 3 (MVTV_PCG=classic disables)
 
     double *oty = nullptr, *wdiag = nullptr;
     double *theta = nullptr, *edges = nullptr, *ga = nullptr, *gu = nullptr, *guprev = nullptr;
-    double *r = nullptr, *p = nullptr, *q = nullptr, *thold = nullptr;
+    double *r = nullptr, *p = nullptr, *q = nullptr, *thold = nullptr, *p2 = nullptr;
     double *partials = nullptr, *red = nullptr;
     PcgState* st = nullptr;
     double* stage = nullptr;
@@ -155,7 +157,7 @@ mvtv_status alloc(double** ptr, size_t n) {
 
 void free_all(mvtv_problem* P) {
     double** bufs[] = {&P->oty, &P->wdiag, &P->theta, &P->edges, &P->ga, &P->gu, &P->guprev, &P->r,
-                       &P->p, &P->q, &P->thold, &P->partials, &P->red, &P->stage};
+                       &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage};
     for (double** b : bufs)
         if (*b) {
             (void)hipFree(*b);
@@ -223,6 +225,39 @@ mvtv_status pcg_solve(mvtv_problem* P, double sigma, const double* oty, const do
                       const double* gb, double cb, double* x, double rtol, int maxit, int* iters, double* relres) {
     const Launch L = P->L();
     const double* w = P->wdiag;
+    if (P->g.p == 3 && P->fused3d && P->wmode != W_NONE) {
+        // r and p ping-pong between two buffers: a launch reads neighbour halos of r_i and p_{i-1}
+        // that the owning workgroups overwrite, so the outputs must not alias the inputs.
+        if (!P->p2) MVTV_TRY(alloc(&P->p2, P->g.N));
+        double* rb[2] = {P->r, P->q};
+        double* pb[2] = {P->p, P->p2};
+        int nb = 0;
+        int h = P->tstart(MVTV_K_PCG_INIT);
+        HIP_TRY(launch_cg3d(P->g, P->stream, 0, sigma, P->wmode, w, x, nullptr, nullptr, rb[0], nullptr, oty, ga, ca,
+                            gb, cb, P->st, P->partials, &nb));
+        P->tstop(h);
+        h = P->tstart(MVTV_K_REDUCE);
+        HIP_TRY(launch_finalize(P->stream, P->partials, nb, 4, 0, 4, nullptr, P->st, rtol * rtol, maxit));
+        P->tstop(h);
+        for (int enq = 0;; enq += kPcgPoll) {
+            for (int b = 0; b < kPcgPoll && enq + b < maxit; ++b) {
+                const int j = enq + b;
+                h = P->tstart(MVTV_K_PCG_FUSED);
+                HIP_TRY(launch_cg3d(P->g, P->stream, j == 0 ? 1 : 2, sigma, P->wmode, w, x, rb[j & 1], pb[j & 1],
+                                    rb[(j + 1) & 1], pb[(j + 1) & 1], oty, ga, ca, gb, cb, P->st, P->partials, &nb));
+                P->tstop(h);
+                h = P->tstart(MVTV_K_REDUCE);
+                HIP_TRY(launch_finalize(P->stream, P->partials, nb, 4, 0, 5, nullptr, P->st));
+                P->tstop(h);
+            }
+            HIP_TRY(hipMemcpyAsync(P->host_st, P->st, sizeof(PcgState), hipMemcpyDeviceToHost, P->stream));
+            MVTV_TRY(P->sync());
+            if (P->host_st->done || enq + kPcgPoll >= maxit) break;
+        }
+        *iters = P->host_st->iter;
+        *relres = P->host_st->bnorm2 > 0 ? std::sqrt(P->host_st->rnorm2 / P->host_st->bnorm2) : 0.0;
+        return MVTV_OK;
+    }
     int h = P->tstart(MVTV_K_PCG_INIT);
     HIP_TRY(launch_pcg_init(P->g, L, sigma, P->wmode, w, oty, ga, ca, gb, cb, x, P->r, P->p, P->partials));
     P->tstop(h);
@@ -369,6 +404,7 @@ mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) 
     }
     for (int k = nb; k < kMaxBlocks; ++k) g.w[k] = 0.0;
     P->grid = int(std::min<uint64_t>((N + kThreads - 1) / kThreads, kMaxGrid));
+    if (const char* env = std::getenv("MVTV_PCG")) P->fused3d = std::strcmp(env, "classic") != 0;
 
     DeviceGuard dg(P->device);
     mvtv_status s = MVTV_OK;
@@ -388,7 +424,7 @@ mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) 
     A(&P->r, N);
     A(&P->p, N);
     A(&P->q, N);
-    A(&P->partials, size_t(kMaxGrid) * kMaxRed);
+    A(&P->partials, size_t(std::max(kMaxGrid, kMaxCgBlocks)) * kMaxRed);
     A(&P->red, 16);
     if (s == MVTV_OK && hipMalloc(reinterpret_cast<void**>(&P->st), sizeof(PcgState)) != hipSuccess)
         s = fail(MVTV_OUT_OF_MEMORY, "hipMalloc(PcgState)");
@@ -807,10 +843,13 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
     switch (kid) {
         case MVTV_K_EDGE_UPDATE: b = 8.0 * (N + 2.0 * E); break;        // theta in, z in/out
         case MVTV_K_GATHER: b = 8.0 * (E + 3.0 * N); break;             // z in, g_uprev in, g_alpha/g_u out
-        case MVTV_K_PCG_INIT: b = 8.0 * ((6.0 + w) * N); break;         // oty, ga, gb, x (+W) in, r, p out
+        case MVTV_K_PCG_INIT:   // classic: oty, ga, gb, x (+W) in, r, p out; fused 3-D: r out only
+            b = 8.0 * (((P->g.p == 3 && P->fused3d) ? 5.0 : 6.0) + w) * N;
+            break;
         case MVTV_K_PCG_APPLY: b = 8.0 * ((2.0 + w) * N); break;        // p (+W) in, q out
         case MVTV_K_PCG_UPDATE: b = 8.0 * ((6.0 + w) * N); break;       // x, r, p, q (+W) in, x, r out
         case MVTV_K_PCG_DIRECTION: b = 8.0 * ((3.0 + w) * N); break;    // r, p (+W) in, p out
+        case MVTV_K_PCG_FUSED: b = 8.0 * ((6.0 + w) * N); break;        // x, r, p (+W) in, x, r, p out
         default: b = 0.0;
     }
     if (total_ms) *total_ms = P->ms[kid];
@@ -821,7 +860,7 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
 
 const char* mvtv_kernel_name(int32_t kid) {
     static const char* names[MVTV_K_COUNT] = {"edge_update", "gather_Dt", "pcg_init", "pcg_apply_A",
-                                               "pcg_update", "pcg_direction", "reduce", "other"};
+                                               "pcg_update", "pcg_direction", "reduce", "other", "pcg_fused3d"};
     return (kid >= 0 && kid < MVTV_K_COUNT) ? names[kid] : "?";
 }
 

@@ -99,6 +99,7 @@ enum WMode { W_NONE = 0, W_IDENTITY = 1, W_DIAG = 2 };
 constexpr int kThreads = 256;
 constexpr int kMaxGrid = 2048;   // grid-stride cap for streaming kernels (8 workgroups per CU)
 constexpr int kMaxRed = 4;
+constexpr int kMaxCgBlocks = 8192;   // workgroups of the fused 3-D PCG (partials buffer rows)
 
 // ------------------------------------------------------------------ launchers
 struct Launch {
@@ -121,9 +122,16 @@ hipError_t launch_pcg_update(const Geom& g, const Launch& L, double sigma, int w
                              double* partials);
 hipError_t launch_pcg_pupdate(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
                               const double* r, double* p, const PcgState* st);
-// op: 0 plain (sums, ER_DTH-style max in the last nmax slots), 1 pcg-init, 2 pcg-after-Ap, 3 pcg-after-update
+// op: 0 plain (sums, ER_DTH-style max in the last nmax slots), 1 pcg-init, 2 pcg-after-Ap, 3 pcg-after-update,
+// 4 cg3d prologue, 5 cg3d iteration
 hipError_t launch_finalize(hipStream_t s, const double* partials, int nparts, int nr, int nmax, int op, double* out,
                            PcgState* st, double rtol2 = 0.0, int maxit = 0);
+// fused 3-D Chronopoulos-Gear PCG (mvtv_cg3d.hip): mode 0 prologue, 1 first iteration, 2 iteration;
+// partials get 4 values per workgroup (gamma, delta, |r|^2, |b|^2), *nblocks_out workgroups
+hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int wmode, const double* wdiag,
+                       double* x, const double* r_in, const double* p_in, double* r_out, double* p_out,
+                       const double* oty, const double* ga, double ca,
+                       const double* gb, double cb, const PcgState* st, double* partials, int* nblocks_out);
 hipError_t launch_maxabsdiff(const Geom& g, const Launch& L, const double* a, const double* b, double* partials);
 hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n);
 // compact <-> padded edge layouts for one block segment [e0, e0+cnt) of block k

@@ -14,50 +14,9 @@
 // single edge array z = D theta - u_old (one E-vector instead of alpha and u):
 //   alpha = soft(z, t) = z - clamp(z, -t, t),   u = -c * clamp(z, -t, t)
 // where t = lambda/rho at the time z was formed and c is the accumulated adapt_step scale.
-#include <type_traits>
-
-#include "mvtv_internal.h"
+#include "mvtv_device.h"
 
 namespace mvtv {
-
-template <int K, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (K < N) {
-        f(std::integral_constant<int, K>{});
-        static_for<K + 1, N>(f);
-    }
-}
-
-__device__ __forceinline__ double clampd(double z, double t) { return fmin(fmax(z, -t), t); }
-
-// Wave (64-lane) shuffle reduction, then across the block's waves through LDS. The last NMAX
-// slots are max-reductions, the others sums. Thread 0 writes this block's partials.
-template <int NR, int NMAX>
-__device__ __forceinline__ void block_reduce_store(double (&v)[NR], double* __restrict__ partials) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            double o = __shfl_down(v[k], off, 64);
-            v[k] = (k < NR - NMAX) ? v[k] + o : fmax(v[k], o);
-        }
-    }
-    __shared__ double sm[kThreads / 64][NR];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < NR; ++k) sm[wid][k] = v[k];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            double acc = sm[0][k];
-            for (int w = 1; w < kThreads / 64; ++w) acc = (k < NR - NMAX) ? acc + sm[w][k] : fmax(acc, sm[w][k]);
-            partials[blockIdx.x * NR + k] = acc;
-        }
-    }
-}
 
 // Jacobi diagonal of W + sigma * sum_S cS[S] (x)_{j in S} L_j at a node with multi-index c:
 // the 1-D Neumann Laplacian's diagonal is (c > 0) + (c < m - 1).
@@ -369,7 +328,7 @@ __global__ __launch_bounds__(kThreads) void k_pcg_pupdate(Geom g, double sigma, 
 __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ partials, int nparts, int nr,
                                                    int nmax, int op, double* __restrict__ out, PcgState* st,
                                                    double rtol2, int maxit) {
-    if ((op == 2 || op == 3) && st->done) return;
+    if ((op == 2 || op == 3 || op == 5) && st->done) return;
     __shared__ double sm[1024];
     __shared__ double res[kMaxRed];
     for (int k = 0; k < nr; ++k) {
@@ -410,6 +369,25 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
         st->rnorm2 = res[1];
         st->iter += 1;
         st->done = (res[1] <= st->rtol2 * st->bnorm2) || st->iter >= st->maxit;
+    } else if (op == 4) {   // fused 3-D PCG prologue: gamma0, delta0, |r0|^2, |b|^2
+        st->bnorm2 = res[3];
+        st->gamma = res[0];
+        st->rnorm2 = res[2];
+        st->alpha = res[0] / res[1];
+        st->beta = 0.0;
+        st->rtol2 = rtol2;
+        st->maxit = maxit;
+        st->iter = 0;
+        st->done = (res[2] <= rtol2 * res[3]) || maxit <= 0;
+    } else if (op == 5) {   // Chronopoulos-Gear scalar recurrences
+        const double gnew = res[0], dnew = res[1];
+        const double beta = gnew / st->gamma;
+        st->alpha = gnew / (dnew - beta * gnew / st->alpha);
+        st->beta = beta;
+        st->gamma = gnew;
+        st->rnorm2 = res[2];
+        st->iter += 1;
+        st->done = (res[2] <= st->rtol2 * st->bnorm2) || st->iter >= st->maxit;
     }
 }
 

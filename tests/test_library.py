@@ -1,0 +1,76 @@
+"""CPU-only checks of the C-ABI library: it loads, exports every symbol include/mvtv/mvtv.h declares,
+and its host-side bindings agree with the header (no compute calls, no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import multivartv_amd as mv
+from multivartv_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mvtv", "mvtv.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mvtv_[A-Za-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    for n in ("mvtv_problem_create", "mvtv_admm", "mvtv_admm_run", "mvtv_apply_D", "mvtv_apply_Dt",
+              "mvtv_apply_A", "mvtv_solve", "mvtv_state_set", "mvtv_state_get", "mvtv_timing_get"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = mv.lib()
+    missing = [n for n in declared_functions() if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_the_header():
+    assert set(declared_functions()) == set(_lib.SIGNATURES)
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """ctypes mirrors of the ABI structs have the C compiler's sizes and field offsets."""
+    structs = {"mvtv_problem_desc": _lib.ProblemDesc, "mvtv_admm_opts": _lib.AdmmOpts,
+               "mvtv_admm_stats": _lib.AdmmStats}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mvtv/mvtv.h"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = dict(line.split() for line in subprocess.check_output([str(exe)]).decode().splitlines())
+    for cname, cls in structs.items():
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
+
+
+def test_host_only_calls():
+    L = mv.lib()
+    assert L.mvtv_version().startswith(b"multivartv_amd")
+    assert L.mvtv_status_string(3) == b"dimension mismatch (mixed-partial construction)"
+    o = _lib.default_opts(mv.VARIANT_CPP, fixed_iters=3)
+    assert o.variant == mv.VARIANT_CPP and o.fixed_iters == 3 and np.isnan(o.sigma)
+    assert L.mvtv_kernel_name(8) == b"pcg_fused3d"
+    assert [L.mvtv_kernel_name(k).decode() for k in range(len(_lib.KERNELS))] == _lib.KERNELS
+
+
+def test_no_device_fails_loudly():
+    if mv.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(mv.MvtvError):
+        mv.Problem([4, 4], np.zeros(16))
