@@ -1,0 +1,97 @@
+// solvers.hpp — C++ host API with the reference's solver entry points, over the mvtv C ABI.
+//
+// Mirrors rcpp-code/MultivarTV/src/solvers.hpp (variant B, the released package) and
+// cpp-code/solvers.hpp (variant A) with Armadillo types replaced by std::vector and a small
+// column-major matrix. Every numerical step of the ADMM loop runs in libmvtv.so on the GPU;
+// this layer only does the reference's host bookkeeping (mesh, nearest-mesh index O,
+// warm-started lambda path, MSE bookkeeping).
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mvtv/mvtv.h"
+
+namespace mvtv {
+
+using vec = std::vector<double>;
+
+// Column-major matrix (Armadillo's layout): element (i, j) at v[i + j * n_rows].
+struct mat {
+    int64_t n_rows = 0, n_cols = 0;
+    std::vector<double> v;
+    mat() = default;
+    mat(int64_t r, int64_t c) : n_rows(r), n_cols(c), v(size_t(r * c), 0.0) {}
+    double& operator()(int64_t i, int64_t j) { return v[size_t(i + j * n_rows)]; }
+    double operator()(int64_t i, int64_t j) const { return v[size_t(i + j * n_rows)]; }
+};
+
+class mvtv_error : public std::runtime_error {
+   public:
+    mvtv_error(int status, const std::string& what) : std::runtime_error(what), status(status) {}
+    int status;
+};
+
+// ---- setup: rcpp-code/MultivarTV/src/utils.cpp -------------------------------------------
+vec create_deltas(const mat& data, const vec& m, double eps = 1e-4);          // :256-263
+mat create_mesh(const mat& data, const vec& m, double eps = 1e-4);            // :234-254
+// nearest1 (:280-287) as an index map: row i of O has its 1 in column oidx[i]
+std::vector<int64_t> nearest_index(const mat& data, const mat& mesh);
+vec softthresh(const vec& z, double lam);                                     // solvers.cpp:29-34
+
+// ---- cache: replaces mbs_cache / mbs_one_inits (rcpp…/solvers.hpp:30-50) -------------------
+struct mbs_cache {
+    mvtv_problem* prob = nullptr;   // GPU-resident D (as a stencil), W = O^T O, O^T y
+    std::vector<int64_t> oidx;      // O as nearest-mesh indices
+    vec oty, w;
+    int64_t ntheta = 0, rowsD = 0;
+    mbs_cache() = default;
+    mbs_cache(const mbs_cache&) = delete;
+    mbs_cache& operator=(const mbs_cache&) = delete;
+    ~mbs_cache();
+};
+
+// create_cache_objects (rcpp…/solvers.cpp:36-44): O, D, D^T D, O^T O, O^T y for (data, y, mesh)
+void create_cache_objects(const mat& data, const vec& y, const mat& mesh, const vec& m, const vec& deltas,
+                          mbs_cache& cache, int device = 0);
+
+struct admm_out {
+    double rho = 0.0;
+    vec theta, u;
+    mvtv_admm_stats stats{};
+};
+
+// B: rcpp…/solvers.hpp:100 (y is unused by the loop, kept for signature parity)
+void admm_update(const vec& y, mbs_cache& inits, vec& theta_init, double lambda, bool verbose, vec& u_init,
+                 double& rho_init, admm_out& out);
+// A: cpp-code/solvers.hpp:85 — throws std::invalid_argument("Failed to converge!") past 2000 iterations
+vec admm_update_cpp(const vec& y, mbs_cache& inits, const vec* theta_init, double lambda);
+
+struct mbs_one_object {   // rcpp…/solvers.hpp:52-61
+    mat mesh;
+    vec theta_hat, fitted;
+    mat data;
+    vec y, m;
+    double rhohat = 0.0;
+    vec uhat;
+};
+
+struct mbs_object {       // rcpp…/solvers.hpp:65-72
+    mbs_one_object minmse_model;
+    std::vector<mbs_one_object> models;
+    double minmse = 0.0, minmse_lambda = 0.0;
+    vec mses;
+};
+
+// rcpp…/solvers.cpp:140-159 (cache path)
+void mbs_one(const mat& data, const vec& y, const vec& m, mbs_one_object& output, const mat& mesh, vec& u,
+             double& rho, vec& theta_init, double lambda, mbs_cache& cache, bool verbose = false);
+vec mbs_predict(const mbs_one_object& model, const mat& data);   // :161-165
+double mse(const vec& fits, const vec& y);                       // :167-170
+double mbs_mse(const mbs_one_object& model, const vec& y);       // :172-175
+// rcpp…/solvers.cpp:204-222: warm-started path over lambdas (theta, u, rho carried)
+void mbs_path(const mat& data, const vec& y, const vec& m, const mat& mesh, const vec& lambdas, const vec& ftrue,
+              mbs_object& output, mbs_cache& cache, bool verbose = false);
+
+}  // namespace mvtv

@@ -15,13 +15,16 @@
 //   next (k_finalize op 5): beta = gamma'/gamma, alpha = gamma' / (delta' - beta gamma'/alpha)
 //
 // HBM traffic per iteration is 6N words (read x, r, p; write x, r, p) against 11N for the
-// three-kernel PCG. A 512-thread workgroup owns a 64 x 16 column of the (dim 0, dim 1) plane
-// over a chunk of dim-2 planes and marches through dim 2: each plane is loaded once into LDS
-// (with a 2-cell halo). D^T D's 27-point stencil is reflection-symmetric per axis, so it has 8
-// distinct weights K(|dx|,|dy|,|dz|) and its dz = -1 and dz = +1 layers are equal: a plane
-// contributes one in-plane 9-point sum k0 to output z and one sum k1 to outputs z-1 and z+1,
-// accumulated in register queues (9 LDS reads per cell per plane). Neighbours outside the mesh
-// are clamped (1-D Neumann Laplacians, x_{-1} := x_0), which is exactly the reference's D^T D.
+// three-kernel PCG. r and p ping-pong between two buffers: a launch reads neighbour halos of
+// r_i and p_{i-1} that their owning workgroups overwrite. A 512-thread workgroup owns a 64 x 16
+// column of the (dim 0, dim 1) plane over a chunk of dim-2 planes and marches through dim 2:
+// each plane is loaded once into LDS (with a 2-cell halo). D^T D's 27-point stencil is
+// reflection-symmetric per axis, so it has 8 distinct weights K(|dx|,|dy|,|dz|) and its
+// dz = -1 and dz = +1 layers are equal: a plane contributes one in-plane 9-point sum k0 to
+// output z and one sum k1 to outputs z-1 and z+1, accumulated in register queues (9 LDS reads
+// per cell per plane). Neighbours outside the mesh are clamped (1-D Neumann Laplacians,
+// x_{-1} := x_0), which is exactly the reference's D^T D. The Jacobi diagonal takes one of 8
+// values by boundary pattern (interior / face along each dimension), tabulated in LDS.
 #include <algorithm>
 
 #include "mvtv_device.h"
@@ -40,19 +43,23 @@ constexpr int SC = NC / NT;
 static_assert(NC % NT == 0, "tile must be a multiple of the block");
 }  // namespace cg3d
 
-struct Stencil8 {
-    double K[8];   // sigma * D^T D weight at |dx| + 2 |dy| + 4 |dz|
+struct Cg3dArgs {
+    const double* wdiag;
+    double* x;
+    const double* r_in;
+    const double* p_in;
+    double* r_out;
+    double* p_out;
+    const double* oty;
+    const double* ga;
+    const double* gb;
+    const PcgState* st;
+    double* partials;
+    double K[8];     // sigma * D^T D weight at |dx| + 2 |dy| + 4 |dz|
+    double acc[8];   // sigma * diag(D^T D) by boundary pattern (bit j: interior along dim j)
+    double ca, cb;
+    int m0, m1, m2, tiles_x, tiles_y, zchunk;
 };
-
-template <int WM>
-__device__ __forceinline__ double diag3(const Geom& g, double sigma, double wv, int gx, int gy, int gz) {
-    const double l0 = double(gx > 0) + double(gx + 1 < int(g.m[0]));
-    const double l1 = double(gy > 0) + double(gy + 1 < int(g.m[1]));
-    const double l2 = double(gz > 0) + double(gz + 1 < int(g.m[2]));
-    const double acc = g.cS[1] * l0 + g.cS[2] * l1 + g.cS[4] * l2 + g.cS[3] * l0 * l1 + g.cS[5] * l0 * l2 +
-                       g.cS[6] * l1 * l2 + g.cS[7] * l0 * l1 * l2;
-    return (WM == W_DIAG ? wv : 1.0) + sigma * acc;
-}
 
 // One cell of a RX-wide region with origin (ox, oy), reading neighbours from an LDS image of
 // row length IX with origin (iox, ioy); neighbour offsets are 0 where the mesh clamps them.
@@ -76,45 +83,49 @@ __device__ __forceinline__ Cell cell_of(int cell, int ox, int oy, int iox, int i
     return s;
 }
 
+__device__ __forceinline__ int bpat(int gx, int gy, int gz, int m0, int m1, int m2) {
+    return int(gx > 0 && gx + 1 < m0) | (int(gy > 0 && gy + 1 < m1) << 1) | (int(gz > 0 && gz + 1 < m2) << 2);
+}
+
 // In-plane sums of the dz = 0 layer (k0) and of the dz = +-1 layers (k1) around cell s.
-__device__ __forceinline__ void plane_sums(const double* img, const Cell& s, const Stencil8& k, double& k0,
+__device__ __forceinline__ void plane_sums(const double* img, const Cell& s, const double* K, double& k0,
                                            double& k1, double& centre) {
     const int r0 = s.c + s.yl, r2 = s.c + s.yr;
     const double c1 = img[s.c], h1 = img[s.c + s.xl] + img[s.c + s.xr];
     const double cv = img[r0] + img[r2];
     const double hv = img[r0 + s.xl] + img[r0 + s.xr] + img[r2 + s.xl] + img[r2 + s.xr];
     centre = c1;
-    k0 = fma(k.K[0], c1, fma(k.K[1], h1, fma(k.K[2], cv, k.K[3] * hv)));
-    k1 = fma(k.K[4], c1, fma(k.K[5], h1, fma(k.K[6], cv, k.K[7] * hv)));
+    k0 = fma(K[0], c1, fma(K[1], h1, fma(K[2], cv, K[3] * hv)));
+    k1 = fma(K[4], c1, fma(K[5], h1, fma(K[6], cv, K[7] * hv)));
 }
 
 // MODE 0: prologue (r0 = b - A x0 with b = oty + ca ga + cb gb; reductions gamma0, delta0,
 // |r0|^2, |b|^2); MODE 1: first iteration (beta = 0, p_{-1} not read); MODE 2: iteration.
 template <int WM, int MODE>
-__global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(Geom g, Stencil8 sk, double sigma,
-                                                      const double* __restrict__ wdiag, double* __restrict__ x,
-                                                      const double* __restrict__ r_in, const double* __restrict__ p_in,
-                                                      double* __restrict__ r_out, double* __restrict__ p_out,
-                                                      const double* __restrict__ oty, const double* __restrict__ ga,
-                                                      double ca, const double* __restrict__ gb, double cb,
-                                                      const PcgState* __restrict__ st, double* __restrict__ partials,
-                                                      int tiles_x, int tiles_y, int zchunk) {
+__global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(const Cg3dArgs a) {
     using namespace cg3d;
     __shared__ double sP[NA];      // plane z of p_i (x_0 in the prologue), tile + 2
     __shared__ double sR[2][NB];   // r_i of planes z-1, z (ping-pong), tile + 1
     __shared__ double sU[NB];      // u_{i+1} of one plane, tile + 1
-    if (MODE != 0 && st->done) return;
-    const double alpha = MODE == 0 ? 0.0 : st->alpha;
-    const double beta = MODE == 2 ? st->beta : 0.0;
-
-    const int m0 = int(g.m[0]), m1 = int(g.m[1]), m2 = int(g.m[2]);
-    const int nt = tiles_x * tiles_y;
-    const int tz = blockIdx.x / nt, trem = blockIdx.x - tz * nt;
-    const int ty = trem / tiles_x, tx = trem - ty * tiles_x;
-    const int X0 = tx * TX, Y0 = ty * TY;
-    const int z0 = tz * zchunk, z1 = min(m2, z0 + zchunk);
-    const size_t pl = size_t(m0) * size_t(m1);
+    __shared__ double sD[8];       // 1 / diag (W = I) or sigma diag(D^T D) (W diagonal), by pattern
+    if (MODE != 0 && a.st->done) return;
+    const double alpha = MODE == 0 ? 0.0 : a.st->alpha;
+    const double beta = MODE == 2 ? a.st->beta : 0.0;
     const int tid = threadIdx.x;
+    if (tid < 8) sD[tid] = WM == W_DIAG ? a.acc[tid] : 1.0 / (1.0 + a.acc[tid]);
+
+    const int m0 = a.m0, m1 = a.m1, m2 = a.m2;
+    const int nt = a.tiles_x * a.tiles_y;
+    const int tz = blockIdx.x / nt, trem = blockIdx.x - tz * nt;
+    const int ty = trem / a.tiles_x, tx = trem - ty * a.tiles_x;
+    const int X0 = tx * TX, Y0 = ty * TY;
+    const int z0 = tz * a.zchunk, z1 = min(m2, z0 + a.zchunk);
+    const size_t pl = size_t(m0) * size_t(m1);
+
+    // M^-1 v at a cell (W = I: table of reciprocals; W diagonal: one division)
+    auto minv = [&](double v, double wv, int pat) {
+        return WM == W_DIAG ? v / (wv + sD[pat]) : v * sD[pat];
+    };
 
     double bm1[SB], b0[SB], pcm1[SB], pc0[SB];   // s accumulators and p centres, outputs z-1, z
     double cm1[SC], c0[SC], ucm1[SC];            // w accumulators (outputs e-1, e), u centre at e-1
@@ -126,6 +137,7 @@ __global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(Geom g, Stencil8 sk, doubl
 
     const int zs = max(0, z0 - 2), ze = min(m2 - 1, z1 + 1);
     const int ulo = max(0, z0 - 1), uhi = min(m2 - 1, z1);   // planes of s and u formed here
+    __syncthreads();
 
     // s of plane e is complete: r_{i+1}, u_{i+1} on tile + 1, then accumulate w = A u.
     auto finish_plane = [&](int e, bool last) {
@@ -137,21 +149,21 @@ __global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(Geom g, Stencil8 sk, doubl
             const Cell s = cell_of<BX, NB, AX>(bc, X0 - 1, Y0 - 1, X0 - 2, Y0 - 2, m0, m1);
             if (s.in) {
                 const size_t gi = eoff + size_t(s.gy) * m0 + s.gx;
-                const double wv = WM == W_DIAG ? wdiag[gi] : 1.0;
+                const double wv = WM == W_DIAG ? a.wdiag[gi] : 1.0;
                 const double se = fma(wv, last ? pc0[k] : pcm1[k], last ? b0[k] : bm1[k]);
                 const bool tile = own && s.gx >= X0 && s.gx < X0 + TX && s.gy >= Y0 && s.gy < Y0 + TY;
                 double rn;
                 if (MODE == 0) {
-                    const double b = fma(cb, gb[gi], fma(ca, ga[gi], oty[gi]));
+                    const double b = fma(a.cb, a.gb[gi], fma(a.ca, a.ga[gi], a.oty[gi]));
                     rn = b - se;
                     if (tile) red[3] = fma(b, b, red[3]);
                 } else {
                     rn = fma(-alpha, se, sR[e & 1][bc]);
                 }
-                const double un = rn / diag3<WM>(g, sigma, wv, s.gx, s.gy, e);
+                const double un = minv(rn, wv, bpat(s.gx, s.gy, e, m0, m1, m2));
                 sU[bc] = un;
                 if (tile) {
-                    r_out[gi] = rn;
+                    a.r_out[gi] = rn;
                     red[0] = fma(rn, un, red[0]);
                     red[2] = fma(rn, rn, red[2]);
                 }
@@ -162,16 +174,16 @@ __global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(Geom g, Stencil8 sk, doubl
         for (int k = 0; k < SC; ++k) {
             const Cell s = cell_of<TX, NC, BX>(tid + k * NT, X0, Y0, X0 - 1, Y0 - 1, m0, m1);
             double k0v = 0.0, k1v = 0.0, ctr = 0.0;
-            if (s.in) plane_sums(sU, s, sk, k0v, k1v, ctr);
+            if (s.in) plane_sums(sU, s, a.K, k0v, k1v, ctr);
             cm1[k] += k1v;
             c0[k] += k0v + (e == 0 ? k1v : 0.0) + (e == m2 - 1 ? k1v : 0.0);
             if (s.in) {
                 if (e - 1 >= z0 && e - 1 < z1) {   // w(e-1) is complete
-                    const double wv = WM == W_DIAG ? wdiag[size_t(e - 1) * pl + size_t(s.gy) * m0 + s.gx] : 1.0;
+                    const double wv = WM == W_DIAG ? a.wdiag[size_t(e - 1) * pl + size_t(s.gy) * m0 + s.gx] : 1.0;
                     red[1] = fma(fma(wv, ucm1[k], cm1[k]), ucm1[k], red[1]);
                 }
                 if (e == m2 - 1 && own) {          // last mesh plane: w(e) is complete too
-                    const double wv = WM == W_DIAG ? wdiag[eoff + size_t(s.gy) * m0 + s.gx] : 1.0;
+                    const double wv = WM == W_DIAG ? a.wdiag[eoff + size_t(s.gy) * m0 + s.gx] : 1.0;
                     red[1] = fma(fma(wv, ctr, c0[k]), ctr, red[1]);
                 }
             }
@@ -194,17 +206,17 @@ __global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(Geom g, Stencil8 sk, doubl
                 if (gx >= 0 && gx < m0 && gy >= 0 && gy < m1) {
                     const size_t gi = zoff + size_t(gy) * m0 + gx;
                     if (MODE == 0) {
-                        sP[cell] = x[gi];
+                        sP[cell] = a.x[gi];
                     } else {
-                        const double ri = r_in[gi];
-                        const double wv = WM == W_DIAG ? wdiag[gi] : 1.0;
-                        double pi = ri / diag3<WM>(g, sigma, wv, gx, gy, z);
-                        if (MODE == 2) pi = fma(beta, p_in[gi], pi);
+                        const double ri = a.r_in[gi];
+                        const double wv = WM == W_DIAG ? a.wdiag[gi] : 1.0;
+                        double pi = minv(ri, wv, bpat(gx, gy, z, m0, m1, m2));
+                        if (MODE == 2) pi = fma(beta, a.p_in[gi], pi);
                         sP[cell] = pi;
                         if (lx >= 1 && lx <= BX && ly >= 1 && ly <= BY) sR[z & 1][(ly - 1) * BX + (lx - 1)] = ri;
                         if (lx >= 2 && lx < TX + 2 && ly >= 2 && ly < TY + 2 && z >= z0 && z < z1) {
-                            p_out[gi] = pi;
-                            x[gi] = fma(alpha, pi, x[gi]);
+                            a.p_out[gi] = pi;
+                            a.x[gi] = fma(alpha, pi, a.x[gi]);
                         }
                     }
                 }
@@ -218,7 +230,7 @@ __global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(Geom g, Stencil8 sk, doubl
         for (int k = 0; k < SB; ++k) {
             const Cell s = cell_of<BX, NB, AX>(tid + k * NT, X0 - 1, Y0 - 1, X0 - 2, Y0 - 2, m0, m1);
             double k0v = 0.0, k1v = 0.0, ctr = 0.0;
-            if (s.in) plane_sums(sP, s, sk, k0v, k1v, ctr);
+            if (s.in) plane_sums(sP, s, a.K, k0v, k1v, ctr);
             bm1[k] += k1v;
             b0[k] += k0v + (z == 0 ? k1v : 0.0) + (z == m2 - 1 ? k1v : 0.0);
             bp1[k] = k1v;
@@ -241,42 +253,61 @@ __global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(Geom g, Stencil8 sk, doubl
             pcm1[k] = pc0[k];
         }
     }
-    block_reduce_store<4, 0, NT>(red, partials);
+    block_reduce_store<4, 0, NT>(red, a.partials);
 }
 
 // ------------------------------------------------------------------------------------ launcher
 hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int wmode, const double* wdiag,
                        double* x, const double* r_in, const double* p_in, double* r_out, double* p_out,
-                       const double* oty, const double* ga, double ca,
-                       const double* gb, double cb, const PcgState* st, double* partials, int* nblocks_out) {
+                       const double* oty, const double* ga, double ca, const double* gb, double cb,
+                       const PcgState* st, double* partials, int* nblocks_out) {
     using namespace cg3d;
-    const int tiles_x = int((g.m[0] + TX - 1) / TX), tiles_y = int((g.m[1] + TY - 1) / TY);
-    const int tiles = tiles_x * tiles_y;
-    int nz = std::max(1, std::min(int(g.m[2]) / 16, (1024 + tiles - 1) / tiles));
-    const int zchunk = int((g.m[2] + nz - 1) / nz);
-    nz = int((g.m[2] + zchunk - 1) / zchunk);
+    Cg3dArgs a{};
+    a.m0 = int(g.m[0]);
+    a.m1 = int(g.m[1]);
+    a.m2 = int(g.m[2]);
+    a.tiles_x = (a.m0 + TX - 1) / TX;
+    a.tiles_y = (a.m1 + TY - 1) / TY;
+    const int tiles = a.tiles_x * a.tiles_y;
+    int nz = std::max(1, std::min(a.m2 / 16, (1024 + tiles - 1) / tiles));
+    a.zchunk = (a.m2 + nz - 1) / nz;
+    nz = (a.m2 + a.zchunk - 1) / a.zchunk;
     const int nblocks = tiles * nz;
     if (nblocks > kMaxCgBlocks) return hipErrorInvalidValue;
     if (nblocks_out) *nblocks_out = nblocks;
     // K(o) = sum_S cS[S] prod_j f_j(o_j) with f = (j in S) ? (o == 0 ? 2 : -1) : (o == 0 ? 1 : 0):
-    // even in every o_j, so it depends on |o_j| only.
-    Stencil8 sk;
+    // even in every o_j, so it depends on |o_j| only. diag: l_j = 1 on a face, 2 inside.
     for (int t = 0; t < 8; ++t) {
-        double acc = 0.0;
+        double kk = 0.0, dd = 0.0;
         for (int S = 1; S < 8; ++S) {
-            double prod = g.cS[S];
+            double prod = g.cS[S], dprod = g.cS[S];
             for (int j = 0; j < 3; ++j) {
                 const bool off = (t >> j) & 1;
                 const bool inS = (S >> j) & 1;
                 prod *= inS ? (off ? -1.0 : 2.0) : (off ? 0.0 : 1.0);
+                if (inS) dprod *= ((t >> j) & 1) ? 2.0 : 1.0;
             }
-            acc += prod;
+            kk += prod;
+            dd += dprod;
         }
-        sk.K[t] = sigma * acc;
+        a.K[t] = sigma * kk;
+        a.acc[t] = sigma * dd;
     }
+    a.wdiag = wdiag;
+    a.x = x;
+    a.r_in = r_in;
+    a.p_in = p_in;
+    a.r_out = r_out;
+    a.p_out = p_out;
+    a.oty = oty;
+    a.ga = ga;
+    a.gb = gb;
+    a.ca = ca;
+    a.cb = cb;
+    a.st = st;
+    a.partials = partials;
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(nblocks), dim3(NT), 0, s, g, sk, sigma, wdiag, x, r_in, p_in, r_out, p_out, oty, ga, ca, gb, cb, st,
-                           partials, tiles_x, tiles_y, zchunk);
+        hipLaunchKernelGGL(kern, dim3(nblocks), dim3(NT), 0, s, a);
         return hipGetLastError();
     };
     if (wmode == W_DIAG) {
