@@ -161,6 +161,8 @@ class Problem:
             d.deltas[j] = float(deltas[j]) if (deltas is not None and j < p) else 0.0
         d.block_order = order
         d.weighted = int(deltas is not None) if weighted is None else int(weighted)
+        self.deltas = None if deltas is None else [float(v) for v in deltas]
+        self.order, self.weighted, self.device = order, bool(d.weighted), device
         self._oty = _f64(oty, self.N)
         self._w = None if wdiag is None else _f64(wdiag, self.N)
         d.oty = _ptr(self._oty)

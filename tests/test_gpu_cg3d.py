@@ -10,8 +10,10 @@ mv = pytest.importorskip("multivartv_amd")
 pytestmark = pytest.mark.gpu
 
 # m0 == m1 (the reference's D construction requires it at p = 3); sizes straddle the 64 x 16
-# tile, single and multiple dim-2 chunks, and thin meshes
-SHAPES = [[8, 8, 8], [70, 70, 9], [64, 64, 40], [37, 37, 33], [130, 130, 3], [20, 20, 70]]
+# tile, single and multiple dim-2 chunks, and thin meshes. SuperLU (the oracle) only on small
+# meshes: its fill-in on 3-D 27-point matrices makes larger factorisations take minutes.
+SHAPES = [[8, 8, 8], [70, 70, 3], [20, 20, 34], [17, 17, 40], [130, 130, 2]]
+BIG = [[64, 64, 40], [96, 96, 70], [200, 200, 17]]
 
 
 @pytest.mark.parametrize("m", SHAPES)
@@ -30,6 +32,22 @@ def test_fused_solve_matches_superlu(m, wdiag):
     x, it, rr = P.solve(sigma, b, x0=x0, rtol=1e-13, max_iter=3000)
     assert rr <= 1e-13, (it, rr)
     assert np.max(np.abs(x - ref)) <= 1e-10 * np.max(np.abs(ref))
+    P.close()
+
+
+@pytest.mark.parametrize("m", BIG)
+def test_fused_solve_residual_large(m):
+    """Larger meshes: the true residual |b - (W + sigma D^T D) x| / |b| from the oracle's sparse D."""
+    rng = np.random.default_rng(11)
+    N = int(np.prod(m))
+    W = rng.integers(0, 4, N).astype(float)
+    deltas = [0.3, 0.2, 0.5]
+    D = O.build_D(m, O.block_table(3, deltas, "cpp"))
+    P = mv.Problem(m, rng.standard_normal(N), wdiag=W, deltas=deltas)
+    b = rng.standard_normal(N)
+    x, it, rr = P.solve(3.0, b, rtol=1e-12, max_iter=5000)
+    true_res = np.linalg.norm(b - O.apply_A(D, W, 3.0, x)) / np.linalg.norm(b)
+    assert rr <= 1e-12 and true_res <= 1e-10, (it, rr, true_res)
     P.close()
 
 
