@@ -18,7 +18,7 @@ def test_config1_through_mbs_one_cache_path(name):
     """BASELINE config 1 via the reference's own API shape (code/solvers.py:mbs_one, cache path)."""
     meta, g = load_golden(name)
     m = np.array(meta["m"])
-    cache = solvers.make_cache(g["data"], g["y"], m, sigma=meta["lam"])   # D = create_D(m, None)
+    cache = solvers.make_cache(g["data"], g["y"], m, sigma=meta["lam"], weighted=False)  # create_D(m, None)
     np.testing.assert_array_equal(cache.mesh, g["mesh"])
     out = solvers.mbs_one(g["data"], g["y"], m, tune=meta["lam"], cache=cache)
     assert set(out) == {"mesh", "theta.hat", "fitted", "data", "y", "eps", "m", "counter"}

@@ -1,0 +1,74 @@
+"""Summarise rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) into per-launch HBM bytes per kernel.
+
+Usage: python tools/pmc_summary.py gpurun_out [profiles/<round>/pmc_traffic.json]
+
+FETCH_SIZE / WRITE_SIZE are in KiB and come from the L2's memory-side request counters
+(MI355X_MICROARCH.md §HBM). gfx950 under-reports wide streaming reads (FETCH_SIZE = 1/2 of the
+bytes for 16-B lanes), and other widths are uncalibrated there, so the factors are measured here
+with tools/pmc_calib.hip: known-size copies with 8-B and 16-B lanes. The mvtv kernels move
+8-B lanes, so the 8-B factors are applied.
+"""
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+NAMES = {"k_cg3d": "pcg_fused3d", "k_edge_update": "edge_update", "k_gather": "gather_Dt",
+         "k_apply_A": "pcg_apply_A", "k_pcg_update": "pcg_update", "k_pcg_pupdate": "pcg_direction",
+         "k_pcg_init": "pcg_init", "copy8": "copy8", "copy16": "copy16"}
+
+
+def short(kname: str) -> str:
+    for k, v in NAMES.items():
+        if re.search(r"\b" + k + r"\b", kname):
+            if k == "k_cg3d" and re.search(r"k_cg3d<\d+, 0>", kname):
+                return "pcg_init"
+            return v
+    return kname.split("(")[0]
+
+
+def read_counter(d: str, counter: str):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    per = defaultdict(list)
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                per[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
+
+
+def main(out_dir: str, dest: str | None):
+    fetch, nf = read_counter(os.path.join(out_dir, "prof_fetch"), "FETCH_SIZE")
+    write, nw = read_counter(os.path.join(out_dir, "prof_write"), "WRITE_SIZE")
+    cf, _ = read_counter(os.path.join(out_dir, "calib_fetch"), "FETCH_SIZE")
+    cw, _ = read_counter(os.path.join(out_dir, "calib_write"), "WRITE_SIZE")
+    known = float(2 ** 28 * 8)   # bytes per launch of the calibration copies
+    f8 = known / (cf["copy8"] * 1024) if cf.get("copy8") else None
+    w8 = known / (cw["copy8"] * 1024) if cw.get("copy8") else None
+    f16 = known / (cf["copy16"] * 1024) if cf.get("copy16") else None
+    w16 = known / (cw["copy16"] * 1024) if cw.get("copy16") else None
+    out = {"calibration": {"fetch_factor_8B": f8, "write_factor_8B": w8, "fetch_factor_16B": f16,
+                           "write_factor_16B": w16},
+           "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        rd = fetch.get(k, 0.0) * 1024 * (f8 or 1.0)
+        wr = write.get(k, 0.0) * 1024 * (w8 or 1.0)
+        out["kernels"][k] = {"read_bytes": rd, "write_bytes": wr, "hbm_bytes": rd + wr,
+                             "launches_sampled": nf.get(k, 0)}
+        out[k] = rd + wr
+    txt = json.dumps(out, indent=1)
+    print(txt)
+    if dest:
+        with open(dest, "w") as fh:
+            fh.write(txt + "\n")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
