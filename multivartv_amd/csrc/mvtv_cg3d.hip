@@ -194,35 +194,70 @@ __global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(const Cg3dArgs a) {
         __syncthreads();
     };
 
-    for (int z = zs; z <= ze; ++z) {
-        // ---------------- stage A: plane z of p_i (x_0 in the prologue) on tile + 2, r_i on tile + 1
+    // Stage A is split: issue() loads plane z's inputs into registers one plane ahead, so the HBM
+    // latency of plane z+1 overlaps the stencil work of plane z; commit() forms p_i into LDS.
+    double qr[SA], qp[SA], qx[SA], qw[SA];
+#pragma unroll
+    for (int k = 0; k < SA; ++k) qr[k] = qp[k] = qx[k] = qw[k] = 0.0;
+    auto a_cell = [&](int k, int& lx, int& ly, int& gx, int& gy) {
+        const int cell = tid + k * NT;
+        ly = cell / AX;
+        lx = cell - ly * AX;
+        gx = X0 - 2 + lx;
+        gy = Y0 - 2 + ly;
+        return cell < NA && gx >= 0 && gx < m0 && gy >= 0 && gy < m1;
+    };
+    auto issue = [&](int z) {
         const size_t zoff = size_t(z) * pl;
+        const bool ownz = z >= z0 && z < z1;
 #pragma unroll
         for (int k = 0; k < SA; ++k) {
-            const int cell = tid + k * NT;
-            if (cell < NA) {
-                const int ly = cell / AX, lx = cell - ly * AX;
-                const int gx = X0 - 2 + lx, gy = Y0 - 2 + ly;
-                if (gx >= 0 && gx < m0 && gy >= 0 && gy < m1) {
-                    const size_t gi = zoff + size_t(gy) * m0 + gx;
-                    if (MODE == 0) {
-                        sP[cell] = a.x[gi];
-                    } else {
-                        const double ri = a.r_in[gi];
-                        const double wv = WM == W_DIAG ? a.wdiag[gi] : 1.0;
-                        double pi = minv(ri, wv, bpat(gx, gy, z, m0, m1, m2));
-                        if (MODE == 2) pi = fma(beta, a.p_in[gi], pi);
-                        sP[cell] = pi;
-                        if (lx >= 1 && lx <= BX && ly >= 1 && ly <= BY) sR[z & 1][(ly - 1) * BX + (lx - 1)] = ri;
-                        if (lx >= 2 && lx < TX + 2 && ly >= 2 && ly < TY + 2 && z >= z0 && z < z1) {
-                            a.p_out[gi] = pi;
-                            a.x[gi] = fma(alpha, pi, a.x[gi]);
-                        }
+            int lx, ly, gx, gy;
+            if (a_cell(k, lx, ly, gx, gy)) {
+                const size_t gi = zoff + size_t(gy) * m0 + gx;
+                if (MODE == 0) {
+                    qx[k] = a.x[gi];
+                } else {
+                    qr[k] = a.r_in[gi];
+                    if (MODE == 2) qp[k] = a.p_in[gi];
+                    if (WM == W_DIAG) qw[k] = a.wdiag[gi];
+                    if (ownz && lx >= 2 && lx < TX + 2 && ly >= 2 && ly < TY + 2) qx[k] = a.x[gi];
+                }
+            }
+        }
+    };
+    auto commit = [&](int z) {
+        const size_t zoff = size_t(z) * pl;
+        const bool ownz = z >= z0 && z < z1;
+#pragma unroll
+        for (int k = 0; k < SA; ++k) {
+            int lx, ly, gx, gy;
+            if (a_cell(k, lx, ly, gx, gy)) {
+                const int cell = tid + k * NT;
+                if (MODE == 0) {
+                    sP[cell] = qx[k];
+                } else {
+                    const double ri = qr[k];
+                    double pi = minv(ri, qw[k], bpat(gx, gy, z, m0, m1, m2));
+                    if (MODE == 2) pi = fma(beta, qp[k], pi);
+                    sP[cell] = pi;
+                    if (lx >= 1 && lx <= BX && ly >= 1 && ly <= BY) sR[z & 1][(ly - 1) * BX + (lx - 1)] = ri;
+                    if (ownz && lx >= 2 && lx < TX + 2 && ly >= 2 && ly < TY + 2) {
+                        const size_t gi = zoff + size_t(gy) * m0 + gx;
+                        a.p_out[gi] = pi;
+                        a.x[gi] = fma(alpha, pi, qx[k]);
                     }
                 }
             }
         }
+    };
+
+    issue(zs);
+    for (int z = zs; z <= ze; ++z) {
+        // ---------------- stage A: plane z of p_i (x_0 in the prologue) on tile + 2, r_i on tile + 1
+        commit(z);
         __syncthreads();
+        if (z + 1 <= ze) issue(z + 1);
         // ---------------- stage B: plane z feeds s at outputs z-1 (k1), z (k0), z+1 (k1); clamped
         // dim-2 neighbours: plane 0 is its own dz=-1 layer, plane m2-1 its own dz=+1 layer
         double bp1[SB];
