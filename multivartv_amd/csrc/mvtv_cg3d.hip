@@ -102,7 +102,7 @@ __device__ __forceinline__ void plane_sums(const double* img, const Cell& s, con
 // MODE 0: prologue (r0 = b - A x0 with b = oty + ca ga + cb gb; reductions gamma0, delta0,
 // |r0|^2, |b|^2); MODE 1: first iteration (beta = 0, p_{-1} not read); MODE 2: iteration.
 template <int WM, int MODE>
-__global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(const Cg3dArgs a) {
+__global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
     using namespace cg3d;
     __shared__ double sP[NA];      // plane z of p_i (x_0 in the prologue), tile + 2
     __shared__ double sR[2][NB];   // r_i of planes z-1, z (ping-pong), tile + 1
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(const Cg3dArgs a) {
     if (MODE != 0 && a.st->done) return;
     const double alpha = MODE == 0 ? 0.0 : a.st->alpha;
     const double beta = MODE == 2 ? a.st->beta : 0.0;
-    const int tid = threadIdx.x;
+    int tid = threadIdx.x;   // re-hidden from the optimiser every plane (see the z loop)
     if (tid < 8) sD[tid] = WM == W_DIAG ? a.acc[tid] : 1.0 / (1.0 + a.acc[tid]);
 
     const int m0 = a.m0, m1 = a.m1, m2 = a.m2;
@@ -254,6 +254,9 @@ __global__ __launch_bounds__(cg3d::NT, 1) void k_cg3d(const Cg3dArgs a) {
 
     issue(zs);
     for (int z = zs; z <= ze; ++z) {
+        // Make tid opaque per plane so the per-slot cell geometry is recomputed instead of hoisted
+        // out of the loop (hoisting it costs ~80 VGPRs and halves the workgroups per CU).
+        asm volatile("" : "+v"(tid));
         // ---------------- stage A: plane z of p_i (x_0 in the prologue) on tile + 2, r_i on tile + 1
         commit(z);
         __syncthreads();
