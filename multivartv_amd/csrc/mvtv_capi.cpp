@@ -66,6 +66,7 @@ struct mvtv_problem {
     int64_t E = 0;
     int grid = 1;
     bool fused3d = true;   // fused Chronopoulos-Gear PCG for p = 3 (MVTV_PCG=classic disables)
+    int pcg_hint = 0;      // PCG iterations of the last theta-solve (poll schedule)
 
     double *oty = nullptr, *wdiag = nullptr;
     double *theta = nullptr, *edges = nullptr, *ga = nullptr, *gu = nullptr, *guprev = nullptr;
@@ -119,7 +120,7 @@ struct mvtv_problem {
     void harvest() {  // call after a stream sync
         for (auto& pd : pending) {
             float t = 0.f;
-            if (hipEventElapsedTime(&t, pd.a, pd.b) == hipSuccess) {
+            if (pd.kid >= 0 && hipEventElapsedTime(&t, pd.a, pd.b) == hipSuccess) {
                 ms[pd.kid] += t;
                 launches[pd.kid] += 1;
             }
@@ -225,68 +226,77 @@ mvtv_status pcg_solve(mvtv_problem* P, double sigma, const double* oty, const do
                       const double* gb, double cb, double* x, double rtol, int maxit, int* iters, double* relres) {
     const Launch L = P->L();
     const double* w = P->wdiag;
-    if (P->g.p == 3 && P->fused3d && P->wmode != W_NONE) {
-        // r and p ping-pong between two buffers: a launch reads neighbour halos of r_i and p_{i-1}
-        // that the owning workgroups overwrite, so the outputs must not alias the inputs.
-        if (!P->p2) MVTV_TRY(alloc(&P->p2, P->g.N));
-        double* rb[2] = {P->r, P->q};
-        double* pb[2] = {P->p, P->p2};
-        int nb = 0;
-        int h = P->tstart(MVTV_K_PCG_INIT);
+    const bool fused = P->g.p == 3 && P->fused3d && P->wmode != W_NONE;
+    // fused 3-D: r and p ping-pong between two buffers (a launch reads neighbour halos of r_i and
+    // p_{i-1} that their owning workgroups overwrite, so outputs must not alias inputs)
+    if (fused && !P->p2) MVTV_TRY(alloc(&P->p2, P->g.N));
+    double* rb[2] = {P->r, P->q};
+    double* pb[2] = {P->p, P->p2};
+    int nb = 0;
+    int h = P->tstart(MVTV_K_PCG_INIT);
+    if (fused)
         HIP_TRY(launch_cg3d(P->g, P->stream, 0, sigma, P->wmode, w, x, nullptr, nullptr, rb[0], nullptr, oty, ga, ca,
                             gb, cb, P->st, P->partials, &nb));
-        P->tstop(h);
-        h = P->tstart(MVTV_K_REDUCE);
-        HIP_TRY(launch_finalize(P->stream, P->partials, nb, 4, 0, 4, nullptr, P->st, rtol * rtol, maxit));
-        P->tstop(h);
-        for (int enq = 0;; enq += kPcgPoll) {
-            for (int b = 0; b < kPcgPoll && enq + b < maxit; ++b) {
-                const int j = enq + b;
-                h = P->tstart(MVTV_K_PCG_FUSED);
-                HIP_TRY(launch_cg3d(P->g, P->stream, j == 0 ? 1 : 2, sigma, P->wmode, w, x, rb[j & 1], pb[j & 1],
-                                    rb[(j + 1) & 1], pb[(j + 1) & 1], oty, ga, ca, gb, cb, P->st, P->partials, &nb));
-                P->tstop(h);
-                h = P->tstart(MVTV_K_REDUCE);
-                HIP_TRY(launch_finalize(P->stream, P->partials, nb, 4, 0, 5, nullptr, P->st));
-                P->tstop(h);
-            }
-            HIP_TRY(hipMemcpyAsync(P->host_st, P->st, sizeof(PcgState), hipMemcpyDeviceToHost, P->stream));
-            MVTV_TRY(P->sync());
-            if (P->host_st->done || enq + kPcgPoll >= maxit) break;
-        }
-        *iters = P->host_st->iter;
-        *relres = P->host_st->bnorm2 > 0 ? std::sqrt(P->host_st->rnorm2 / P->host_st->bnorm2) : 0.0;
-        return MVTV_OK;
-    }
-    int h = P->tstart(MVTV_K_PCG_INIT);
-    HIP_TRY(launch_pcg_init(P->g, L, sigma, P->wmode, w, oty, ga, ca, gb, cb, x, P->r, P->p, P->partials));
+    else
+        HIP_TRY(launch_pcg_init(P->g, L, sigma, P->wmode, w, oty, ga, ca, gb, cb, x, P->r, P->p, P->partials));
     P->tstop(h);
     h = P->tstart(MVTV_K_REDUCE);
-    HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, PR_N, 0, 1, nullptr, P->st, rtol * rtol, maxit));
+    if (fused)
+        HIP_TRY(launch_finalize(P->stream, P->partials, nb, 4, 0, 4, nullptr, P->st, rtol * rtol, maxit));
+    else
+        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, PR_N, 0, 1, nullptr, P->st, rtol * rtol, maxit));
     P->tstop(h);
-    for (int enq = 0;; enq += kPcgPoll) {
-        for (int b = 0; b < kPcgPoll && enq + b < maxit; ++b) {
-            h = P->tstart(MVTV_K_PCG_APPLY);
-            HIP_TRY(launch_apply_A(P->g, L, sigma, P->wmode, w, P->p, P->q, P->partials, P->st));
-            P->tstop(h);
-            h = P->tstart(MVTV_K_REDUCE);
-            HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 0, 2, nullptr, P->st));
-            P->tstop(h);
-            h = P->tstart(MVTV_K_PCG_UPDATE);
-            HIP_TRY(launch_pcg_update(P->g, L, sigma, P->wmode, w, x, P->r, P->p, P->q, P->st, P->partials));
-            P->tstop(h);
-            h = P->tstart(MVTV_K_REDUCE);
-            HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 2, 0, 3, nullptr, P->st));
-            P->tstop(h);
-            h = P->tstart(MVTV_K_PCG_DIRECTION);
-            HIP_TRY(launch_pcg_pupdate(P->g, L, sigma, P->wmode, w, P->r, P->p, P->st));
-            P->tstop(h);
+
+    // one PCG iteration; kernels enqueued after convergence return at once (device done flag)
+    auto enqueue = [&](int j) -> mvtv_status {
+        if (fused) {
+            int hh = P->tstart(MVTV_K_PCG_FUSED);
+            HIP_TRY(launch_cg3d(P->g, P->stream, j == 0 ? 1 : 2, sigma, P->wmode, w, x, rb[j & 1], pb[j & 1],
+                                rb[(j + 1) & 1], pb[(j + 1) & 1], oty, ga, ca, gb, cb, P->st, P->partials, &nb));
+            P->tstop(hh);
+            hh = P->tstart(MVTV_K_REDUCE);
+            HIP_TRY(launch_finalize(P->stream, P->partials, nb, 4, 0, 5, nullptr, P->st));
+            P->tstop(hh);
+            return MVTV_OK;
+        }
+        int hh = P->tstart(MVTV_K_PCG_APPLY);
+        HIP_TRY(launch_apply_A(P->g, L, sigma, P->wmode, w, P->p, P->q, P->partials, P->st));
+        P->tstop(hh);
+        hh = P->tstart(MVTV_K_REDUCE);
+        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 0, 2, nullptr, P->st));
+        P->tstop(hh);
+        hh = P->tstart(MVTV_K_PCG_UPDATE);
+        HIP_TRY(launch_pcg_update(P->g, L, sigma, P->wmode, w, x, P->r, P->p, P->q, P->st, P->partials));
+        P->tstop(hh);
+        hh = P->tstart(MVTV_K_REDUCE);
+        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 2, 0, 3, nullptr, P->st));
+        P->tstop(hh);
+        hh = P->tstart(MVTV_K_PCG_DIRECTION);
+        HIP_TRY(launch_pcg_pupdate(P->g, L, sigma, P->wmode, w, P->r, P->p, P->st));
+        P->tstop(hh);
+        return MVTV_OK;
+    };
+    // Poll schedule: the previous solve's count predicts this one (warm starts change it slowly),
+    // so the first poll comes just before it and later polls every 2 iterations.
+    std::vector<size_t> mark;   // first timing entry of each enqueued iteration
+    int enq = 0;
+    int batch = P->pcg_hint > 0 ? std::max(2, P->pcg_hint - 2) : kPcgPoll;
+    for (;;) {
+        for (int b = 0; b < batch && enq < maxit; ++b, ++enq) {
+            mark.push_back(P->pending.size());
+            MVTV_TRY(enqueue(enq));
         }
         HIP_TRY(hipMemcpyAsync(P->host_st, P->st, sizeof(PcgState), hipMemcpyDeviceToHost, P->stream));
-        MVTV_TRY(P->sync());
-        if (P->host_st->done || enq + kPcgPoll >= maxit) break;
+        HIP_TRY(hipStreamSynchronize(P->stream));
+        const int done_iters = P->host_st->iter;
+        if (P->timing && done_iters < int(mark.size()))   // launches past convergence did no work
+            for (size_t e = mark[size_t(done_iters)]; e < P->pending.size(); ++e) P->pending[e].kid = -1;
+        P->harvest();
+        if (P->host_st->done || enq >= maxit) break;
+        batch = 2;
     }
     *iters = P->host_st->iter;
+    P->pcg_hint = *iters;
     *relres = P->host_st->bnorm2 > 0 ? std::sqrt(P->host_st->rnorm2 / P->host_st->bnorm2) : 0.0;
     return MVTV_OK;
 }

@@ -68,23 +68,36 @@ struct Cell {
     bool in;
 };
 
-template <int RX, int NREG, int IX>
+// INT: the workgroup's tile + 2 halo lies inside the mesh in dims 0 and 1, so no neighbour is
+// clamped and every cell is in the mesh (about 70 % of the workgroups at 512^3).
+template <int RX, int NREG, int IX, bool INT>
 __device__ __forceinline__ Cell cell_of(int cell, int ox, int oy, int iox, int ioy, int m0, int m1) {
     Cell s;
     const int ly = cell / RX, lx = cell - ly * RX;
     s.gx = ox + lx;
     s.gy = oy + ly;
-    s.in = cell < NREG && s.gx >= 0 && s.gx < m0 && s.gy >= 0 && s.gy < m1;
     s.c = (s.gy - ioy) * IX + (s.gx - iox);
-    s.xl = s.gx > 0 ? -1 : 0;
-    s.xr = s.gx + 1 < m0 ? 1 : 0;
-    s.yl = s.gy > 0 ? -IX : 0;
-    s.yr = s.gy + 1 < m1 ? IX : 0;
+    if constexpr (INT) {
+        s.in = cell < NREG;
+        s.xl = -1;
+        s.xr = 1;
+        s.yl = -IX;
+        s.yr = IX;
+    } else {
+        s.in = cell < NREG && s.gx >= 0 && s.gx < m0 && s.gy >= 0 && s.gy < m1;
+        s.xl = s.gx > 0 ? -1 : 0;
+        s.xr = s.gx + 1 < m0 ? 1 : 0;
+        s.yl = s.gy > 0 ? -IX : 0;
+        s.yr = s.gy + 1 < m1 ? IX : 0;
+    }
     return s;
 }
 
+template <bool INT>
 __device__ __forceinline__ int bpat(int gx, int gy, int gz, int m0, int m1, int m2) {
-    return int(gx > 0 && gx + 1 < m0) | (int(gy > 0 && gy + 1 < m1) << 1) | (int(gz > 0 && gz + 1 < m2) << 2);
+    const int zb = int(gz > 0 && gz + 1 < m2) << 2;
+    if constexpr (INT) return 3 | zb;
+    return int(gx > 0 && gx + 1 < m0) | (int(gy > 0 && gy + 1 < m1) << 1) | zb;
 }
 
 // In-plane sums of the dz = 0 layer (k0) and of the dz = +-1 layers (k1) around cell s.
@@ -101,25 +114,13 @@ __device__ __forceinline__ void plane_sums(const double* img, const Cell& s, con
 
 // MODE 0: prologue (r0 = b - A x0 with b = oty + ca ga + cb gb; reductions gamma0, delta0,
 // |r0|^2, |b|^2); MODE 1: first iteration (beta = 0, p_{-1} not read); MODE 2: iteration.
-template <int WM, int MODE>
-__global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
+template <int WM, int MODE, bool INT>
+__device__ __forceinline__ void cg3d_body(const Cg3dArgs& a, double* sP, double (*sR)[cg3d::NB], double* sU,
+                                          const double* sD, int X0, int Y0, int z0, int z1, double alpha,
+                                          double beta) {
     using namespace cg3d;
-    __shared__ double sP[NA];      // plane z of p_i (x_0 in the prologue), tile + 2
-    __shared__ double sR[2][NB];   // r_i of planes z-1, z (ping-pong), tile + 1
-    __shared__ double sU[NB];      // u_{i+1} of one plane, tile + 1
-    __shared__ double sD[8];       // 1 / diag (W = I) or sigma diag(D^T D) (W diagonal), by pattern
-    if (MODE != 0 && a.st->done) return;
-    const double alpha = MODE == 0 ? 0.0 : a.st->alpha;
-    const double beta = MODE == 2 ? a.st->beta : 0.0;
     int tid = threadIdx.x;   // re-hidden from the optimiser every plane (see the z loop)
-    if (tid < 8) sD[tid] = WM == W_DIAG ? a.acc[tid] : 1.0 / (1.0 + a.acc[tid]);
-
     const int m0 = a.m0, m1 = a.m1, m2 = a.m2;
-    const int nt = a.tiles_x * a.tiles_y;
-    const int tz = blockIdx.x / nt, trem = blockIdx.x - tz * nt;
-    const int ty = trem / a.tiles_x, tx = trem - ty * a.tiles_x;
-    const int X0 = tx * TX, Y0 = ty * TY;
-    const int z0 = tz * a.zchunk, z1 = min(m2, z0 + a.zchunk);
     const size_t pl = size_t(m0) * size_t(m1);
 
     // M^-1 v at a cell (W = I: table of reciprocals; W diagonal: one division)
@@ -137,7 +138,6 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
 
     const int zs = max(0, z0 - 2), ze = min(m2 - 1, z1 + 1);
     const int ulo = max(0, z0 - 1), uhi = min(m2 - 1, z1);   // planes of s and u formed here
-    __syncthreads();
 
     // s of plane e is complete: r_{i+1}, u_{i+1} on tile + 1, then accumulate w = A u.
     auto finish_plane = [&](int e, bool last) {
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
 #pragma unroll
         for (int k = 0; k < SB; ++k) {
             const int bc = tid + k * NT;
-            const Cell s = cell_of<BX, NB, AX>(bc, X0 - 1, Y0 - 1, X0 - 2, Y0 - 2, m0, m1);
+            const Cell s = cell_of<BX, NB, AX, INT>(bc, X0 - 1, Y0 - 1, X0 - 2, Y0 - 2, m0, m1);
             if (s.in) {
                 const size_t gi = eoff + size_t(s.gy) * m0 + s.gx;
                 const double wv = WM == W_DIAG ? a.wdiag[gi] : 1.0;
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
                 } else {
                     rn = fma(-alpha, se, sR[e & 1][bc]);
                 }
-                const double un = minv(rn, wv, bpat(s.gx, s.gy, e, m0, m1, m2));
+                const double un = minv(rn, wv, bpat<INT>(s.gx, s.gy, e, m0, m1, m2));
                 sU[bc] = un;
                 if (tile) {
                     a.r_out[gi] = rn;
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < SC; ++k) {
-            const Cell s = cell_of<TX, NC, BX>(tid + k * NT, X0, Y0, X0 - 1, Y0 - 1, m0, m1);
+            const Cell s = cell_of<TX, NC, BX, INT>(tid + k * NT, X0, Y0, X0 - 1, Y0 - 1, m0, m1);
             double k0v = 0.0, k1v = 0.0, ctr = 0.0;
             if (s.in) plane_sums(sU, s, a.K, k0v, k1v, ctr);
             cm1[k] += k1v;
@@ -205,6 +205,7 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
         lx = cell - ly * AX;
         gx = X0 - 2 + lx;
         gy = Y0 - 2 + ly;
+        if constexpr (INT) return cell < NA;
         return cell < NA && gx >= 0 && gx < m0 && gy >= 0 && gy < m1;
     };
     auto issue = [&](int z) {
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
                     sP[cell] = qx[k];
                 } else {
                     const double ri = qr[k];
-                    double pi = minv(ri, qw[k], bpat(gx, gy, z, m0, m1, m2));
+                    double pi = minv(ri, qw[k], bpat<INT>(gx, gy, z, m0, m1, m2));
                     if (MODE == 2) pi = fma(beta, qp[k], pi);
                     sP[cell] = pi;
                     if (lx >= 1 && lx <= BX && ly >= 1 && ly <= BY) sR[z & 1][(ly - 1) * BX + (lx - 1)] = ri;
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
         double bp1[SB];
 #pragma unroll
         for (int k = 0; k < SB; ++k) {
-            const Cell s = cell_of<BX, NB, AX>(tid + k * NT, X0 - 1, Y0 - 1, X0 - 2, Y0 - 2, m0, m1);
+            const Cell s = cell_of<BX, NB, AX, INT>(tid + k * NT, X0 - 1, Y0 - 1, X0 - 2, Y0 - 2, m0, m1);
             double k0v = 0.0, k1v = 0.0, ctr = 0.0;
             if (s.in) plane_sums(sP, s, a.K, k0v, k1v, ctr);
             bm1[k] += k1v;
@@ -292,6 +293,34 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
         }
     }
     block_reduce_store<4, 0, NT>(red, a.partials);
+}
+
+template <int WM, int MODE>
+__global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
+    using namespace cg3d;
+    __shared__ double sP[NA];      // plane z of p_i (x_0 in the prologue), tile + 2
+    __shared__ double sR[2][NB];   // r_i of planes z-1, z (ping-pong), tile + 1
+    __shared__ double sU[NB];      // u_{i+1} of one plane, tile + 1
+    __shared__ double sD[8];       // 1 / diag (W = I) or sigma diag(D^T D) (W diagonal), by pattern
+    if (MODE != 0 && a.st->done) return;
+    const double alpha = MODE == 0 ? 0.0 : a.st->alpha;
+    const double beta = MODE == 2 ? a.st->beta : 0.0;
+    if (threadIdx.x < 8) sD[threadIdx.x] = WM == W_DIAG ? a.acc[threadIdx.x] : 1.0 / (1.0 + a.acc[threadIdx.x]);
+    const int nt = a.tiles_x * a.tiles_y;
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and b+8 share one),
+    // so give each XCD a contiguous run of tiles; neighbouring tiles then share their halo
+    // lines in that XCD's L2. Placement affects speed only, never results.
+    int bid = blockIdx.x;
+    if ((gridDim.x & 7) == 0) bid = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);
+    const int tz = bid / nt, trem = bid - tz * nt;
+    const int ty = trem / a.tiles_x, tx = trem - ty * a.tiles_x;
+    const int X0 = tx * TX, Y0 = ty * TY;
+    const int z0 = tz * a.zchunk, z1 = min(a.m2, z0 + a.zchunk);
+    __syncthreads();
+    if (X0 >= 2 && X0 + AX - 2 <= a.m0 && Y0 >= 2 && Y0 + AY - 2 <= a.m1)
+        cg3d_body<WM, MODE, true>(a, sP, sR, sU, sD, X0, Y0, z0, z1, alpha, beta);
+    else
+        cg3d_body<WM, MODE, false>(a, sP, sR, sU, sD, X0, Y0, z0, z1, alpha, beta);
 }
 
 // ------------------------------------------------------------------------------------ launcher

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -q -m gpu ${TEST_ARGS} > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 900 python -m pytest ${TEST_ARGS:-tests} -q -m gpu > gpurun_out/gpu_tests.log 2>&1
 rc=$?
 tail -3 gpurun_out/gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests rc=$rc: stopping"; exit $rc; fi

@@ -41,7 +41,15 @@ def read_counter(d: str, counter: str):
                 if row.get("Counter_Name") != counter:
                     continue
                 per[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
+    # PCG launches enqueued after convergence return at once (done flag): drop them (< 2 % of the
+    # kernel's largest launch) so the per-launch figure describes real iterations
+    out, cnt = {}, {}
+    for k, v in per.items():
+        hi = max(v)
+        real = [x for x in v if x >= 0.02 * hi] or v
+        out[k] = sum(real) / len(real)
+        cnt[k] = len(real)
+    return out, cnt
 
 
 def main(out_dir: str, dest: str | None):
