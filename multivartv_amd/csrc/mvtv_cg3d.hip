@@ -16,31 +16,41 @@
 //
 // HBM traffic per iteration is 6N words (read x, r, p; write x, r, p) against 11N for the
 // three-kernel PCG. r and p ping-pong between two buffers: a launch reads neighbour halos of
-// r_i and p_{i-1} that their owning workgroups overwrite. A 512-thread workgroup owns a 64 x 16
-// column of the (dim 0, dim 1) plane over a chunk of dim-2 planes and marches through dim 2:
-// each plane is loaded once into LDS (with a 2-cell halo). D^T D's 27-point stencil is
-// reflection-symmetric per axis, so it has 8 distinct weights K(|dx|,|dy|,|dz|) and its
-// dz = -1 and dz = +1 layers are equal: a plane contributes one in-plane 9-point sum k0 to
-// output z and one sum k1 to outputs z-1 and z+1, accumulated in register queues (9 LDS reads
-// per cell per plane). Neighbours outside the mesh are clamped (1-D Neumann Laplacians,
-// x_{-1} := x_0), which is exactly the reference's D^T D. The Jacobi diagonal takes one of 8
-// values by boundary pattern (interior / face along each dimension), tabulated in LDS.
+// r_i and p_{i-1} that their owning workgroups overwrite.
+//
+// Geometry. A 512-thread workgroup owns a 60 x 20 column of the (dim 0, dim 1) plane over a
+// chunk of dim-2 planes and marches through dim 2. Each plane is staged in LDS as a 64 x 24
+// image (tile + 2-cell halo): ONE IMAGE ROW IS ONE WAVEFRONT ROW, and wave w owns image rows
+// 3w .. 3w+2 in every stage. So the thread that loads a cell is the thread that finishes it
+// (r_i never goes through LDS), rows are wave-uniform (row bounds and row addresses are scalar
+// work), and a thread's three rows share the five image rows their stencils read.
+//
+// D^T D's 27-point stencil is reflection-symmetric per axis, so it has 8 distinct weights
+// K(|dx|,|dy|,|dz|) and its dz = -1 and dz = +1 layers are equal: a plane contributes one
+// in-plane 9-point sum k0 to output z and one sum k1 to outputs z-1 and z+1, accumulated in
+// register queues. Boundaries: the reference's D^T D is a sum of Kronecker products of 1-D
+// Neumann Laplacians (clamped neighbours). In dims 0 and 1 the image holds the mesh's
+// half-sample MIRROR outside the mesh (cell -1 = cell 0, -2 = 1): the Neumann Laplacian
+// commutes with that extension, so the plain stencil on the mirrored image gives the clamped
+// result on the mesh AND the mirror of it on the ghost cells, which is exactly what the
+// second stencil (w = A u) needs. In dim 2 the z-march duplicates the k1 term at planes 0 and
+// m2-1. With W = I the identity is folded into the centre weight. The Jacobi diagonal takes
+// one of 8 values by boundary pattern (interior / face along each dimension), tabulated in LDS.
 #include <algorithm>
+#include <cstdint>
+#include <cstdlib>
 
 #include "mvtv_device.h"
 
 namespace mvtv {
 
 namespace cg3d {
-constexpr int NT = 512;                   // threads per workgroup
-constexpr int TX = 64, TY = 16;
-constexpr int AX = TX + 4, AY = TY + 4;   // tile + 2 halo
-constexpr int BX = TX + 2, BY = TY + 2;   // tile + 1 halo
-constexpr int NA = AX * AY, NB = BX * BY, NC = TX * TY;
-constexpr int SA = (NA + NT - 1) / NT;
-constexpr int SB = (NB + NT - 1) / NT;
-constexpr int SC = NC / NT;
-static_assert(NC % NT == 0, "tile must be a multiple of the block");
+constexpr int NT = 512, NW = NT / 64;    // threads, waves per workgroup
+constexpr int IW = 64;                   // image row = one wavefront
+constexpr int RPW = 3;                   // image rows per wave
+constexpr int IH = NW * RPW;             // 24 image rows
+constexpr int TX = IW - 4, TY = IH - 4;  // 60 x 20 output tile
+constexpr int IMG = (IH + 2) * IW + 2;   // + a guard row above and below, + 1 word each end
 }  // namespace cg3d
 
 struct Cg3dArgs {
@@ -55,257 +65,55 @@ struct Cg3dArgs {
     const double* gb;
     const PcgState* st;
     double* partials;
-    double K[8];     // sigma * D^T D weight at |dx| + 2 |dy| + 4 |dz|
+    double K[8];     // sigma * D^T D weight at |dx| + 2 |dy| + 4 |dz| (+1 at [0] when W = I)
     double acc[8];   // sigma * diag(D^T D) by boundary pattern (bit j: interior along dim j)
     double ca, cb;
     int m0, m1, m2, tiles_x, tiles_y, zchunk;
 };
 
-// One cell of a RX-wide region with origin (ox, oy), reading neighbours from an LDS image of
-// row length IX with origin (iox, ioy); neighbour offsets are 0 where the mesh clamps them.
-struct Cell {
-    int gx, gy, c, xl, xr, yl, yr;
-    bool in;
-};
+// Half-sample mirror into [0, m): -1 -> 0, -2 -> 1, m -> m-1, m+1 -> m-2; clamped beyond.
+__device__ __forceinline__ int mirror(int g, int m) {
+    g = g < 0 ? -1 - g : g;
+    g = g >= m ? 2 * m - 1 - g : g;
+    return min(max(g, 0), m - 1);
+}
 
-// INT: the workgroup's tile + 2 halo lies inside the mesh in dims 0 and 1, so no neighbour is
-// clamped and every cell is in the mesh (about 70 % of the workgroups at 512^3).
-template <int RX, int NREG, int IX, bool INT>
-__device__ __forceinline__ Cell cell_of(int cell, int ox, int oy, int iox, int ioy, int m0, int m1) {
-    Cell s;
-    const int ly = cell / RX, lx = cell - ly * RX;
-    s.gx = ox + lx;
-    s.gy = oy + ly;
-    s.c = (s.gy - ioy) * IX + (s.gx - iox);
-    if constexpr (INT) {
-        s.in = cell < NREG;
-        s.xl = -1;
-        s.xr = 1;
-        s.yl = -IX;
-        s.yr = IX;
-    } else {
-        s.in = cell < NREG && s.gx >= 0 && s.gx < m0 && s.gy >= 0 && s.gy < m1;
-        s.xl = s.gx > 0 ? -1 : 0;
-        s.xr = s.gx + 1 < m0 ? 1 : 0;
-        s.yl = s.gy > 0 ? -IX : 0;
-        s.yr = s.gy + 1 < m1 ? IX : 0;
+// The 3 output rows of a wave from the 5 image rows around them: in-plane sums k0 (dz = 0
+// layer) and k1 (dz = +-1 layer), and the centre value. img points at the wave's first row.
+__device__ __forceinline__ void wave_rows(const double* img, const double* K, double (&k0)[cg3d::RPW],
+                                          double (&k1)[cg3d::RPW], double (&ctr)[cg3d::RPW]) {
+    using namespace cg3d;
+    double c[RPW + 2], h[RPW + 2];
+#pragma unroll
+    for (int j = 0; j < RPW + 2; ++j) {
+        const double* q = img + (j - 1) * IW;
+        c[j] = q[0];
+        h[j] = q[-1] + q[1];
     }
-    return s;
-}
-
-template <bool INT>
-__device__ __forceinline__ int bpat(int gx, int gy, int gz, int m0, int m1, int m2) {
-    const int zb = int(gz > 0 && gz + 1 < m2) << 2;
-    if constexpr (INT) return 3 | zb;
-    return int(gx > 0 && gx + 1 < m0) | (int(gy > 0 && gy + 1 < m1) << 1) | zb;
-}
-
-// In-plane sums of the dz = 0 layer (k0) and of the dz = +-1 layers (k1) around cell s.
-__device__ __forceinline__ void plane_sums(const double* img, const Cell& s, const double* K, double& k0,
-                                           double& k1, double& centre) {
-    const int r0 = s.c + s.yl, r2 = s.c + s.yr;
-    const double c1 = img[s.c], h1 = img[s.c + s.xl] + img[s.c + s.xr];
-    const double cv = img[r0] + img[r2];
-    const double hv = img[r0 + s.xl] + img[r0 + s.xr] + img[r2 + s.xl] + img[r2 + s.xr];
-    centre = c1;
-    k0 = fma(K[0], c1, fma(K[1], h1, fma(K[2], cv, K[3] * hv)));
-    k1 = fma(K[4], c1, fma(K[5], h1, fma(K[6], cv, K[7] * hv)));
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+        const double cv = c[k] + c[k + 2], hv = h[k] + h[k + 2];
+        k0[k] = fma(K[0], c[k + 1], fma(K[1], h[k + 1], fma(K[2], cv, K[3] * hv)));
+        k1[k] = fma(K[4], c[k + 1], fma(K[5], h[k + 1], fma(K[6], cv, K[7] * hv)));
+        ctr[k] = c[k + 1];
+    }
 }
 
 // MODE 0: prologue (r0 = b - A x0 with b = oty + ca ga + cb gb; reductions gamma0, delta0,
 // |r0|^2, |b|^2); MODE 1: first iteration (beta = 0, p_{-1} not read); MODE 2: iteration.
-template <int WM, int MODE, bool INT>
-__device__ __forceinline__ void cg3d_body(const Cg3dArgs& a, double* sP, double (*sR)[cg3d::NB], double* sU,
-                                          const double* sD, int X0, int Y0, int z0, int z1, double alpha,
-                                          double beta) {
-    using namespace cg3d;
-    int tid = threadIdx.x;   // re-hidden from the optimiser every plane (see the z loop)
-    const int m0 = a.m0, m1 = a.m1, m2 = a.m2;
-    const size_t pl = size_t(m0) * size_t(m1);
-
-    // M^-1 v at a cell (W = I: table of reciprocals; W diagonal: one division)
-    auto minv = [&](double v, double wv, int pat) {
-        return WM == W_DIAG ? v / (wv + sD[pat]) : v * sD[pat];
-    };
-
-    double bm1[SB], b0[SB], pcm1[SB], pc0[SB];   // s accumulators and p centres, outputs z-1, z
-    double cm1[SC], c0[SC], ucm1[SC];            // w accumulators (outputs e-1, e), u centre at e-1
-#pragma unroll
-    for (int k = 0; k < SB; ++k) bm1[k] = b0[k] = pcm1[k] = pc0[k] = 0.0;
-#pragma unroll
-    for (int k = 0; k < SC; ++k) cm1[k] = c0[k] = ucm1[k] = 0.0;
-    double red[4] = {0.0, 0.0, 0.0, 0.0};   // gamma, delta, |r|^2, |b|^2
-
-    const int zs = max(0, z0 - 2), ze = min(m2 - 1, z1 + 1);
-    const int ulo = max(0, z0 - 1), uhi = min(m2 - 1, z1);   // planes of s and u formed here
-
-    // s of plane e is complete: r_{i+1}, u_{i+1} on tile + 1, then accumulate w = A u.
-    auto finish_plane = [&](int e, bool last) {
-        const size_t eoff = size_t(e) * pl;
-        const bool own = e >= z0 && e < z1;
-#pragma unroll
-        for (int k = 0; k < SB; ++k) {
-            const int bc = tid + k * NT;
-            const Cell s = cell_of<BX, NB, AX, INT>(bc, X0 - 1, Y0 - 1, X0 - 2, Y0 - 2, m0, m1);
-            if (s.in) {
-                const size_t gi = eoff + size_t(s.gy) * m0 + s.gx;
-                const double wv = WM == W_DIAG ? a.wdiag[gi] : 1.0;
-                const double se = fma(wv, last ? pc0[k] : pcm1[k], last ? b0[k] : bm1[k]);
-                const bool tile = own && s.gx >= X0 && s.gx < X0 + TX && s.gy >= Y0 && s.gy < Y0 + TY;
-                double rn;
-                if (MODE == 0) {
-                    const double b = fma(a.cb, a.gb[gi], fma(a.ca, a.ga[gi], a.oty[gi]));
-                    rn = b - se;
-                    if (tile) red[3] = fma(b, b, red[3]);
-                } else {
-                    rn = fma(-alpha, se, sR[e & 1][bc]);
-                }
-                const double un = minv(rn, wv, bpat<INT>(s.gx, s.gy, e, m0, m1, m2));
-                sU[bc] = un;
-                if (tile) {
-                    a.r_out[gi] = rn;
-                    red[0] = fma(rn, un, red[0]);
-                    red[2] = fma(rn, rn, red[2]);
-                }
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < SC; ++k) {
-            const Cell s = cell_of<TX, NC, BX, INT>(tid + k * NT, X0, Y0, X0 - 1, Y0 - 1, m0, m1);
-            double k0v = 0.0, k1v = 0.0, ctr = 0.0;
-            if (s.in) plane_sums(sU, s, a.K, k0v, k1v, ctr);
-            cm1[k] += k1v;
-            c0[k] += k0v + (e == 0 ? k1v : 0.0) + (e == m2 - 1 ? k1v : 0.0);
-            if (s.in) {
-                if (e - 1 >= z0 && e - 1 < z1) {   // w(e-1) is complete
-                    const double wv = WM == W_DIAG ? a.wdiag[size_t(e - 1) * pl + size_t(s.gy) * m0 + s.gx] : 1.0;
-                    red[1] = fma(fma(wv, ucm1[k], cm1[k]), ucm1[k], red[1]);
-                }
-                if (e == m2 - 1 && own) {          // last mesh plane: w(e) is complete too
-                    const double wv = WM == W_DIAG ? a.wdiag[eoff + size_t(s.gy) * m0 + s.gx] : 1.0;
-                    red[1] = fma(fma(wv, ctr, c0[k]), ctr, red[1]);
-                }
-            }
-            cm1[k] = c0[k];
-            c0[k] = k1v;
-            ucm1[k] = ctr;
-        }
-        __syncthreads();
-    };
-
-    // Stage A is split: issue() loads plane z's inputs into registers one plane ahead, so the HBM
-    // latency of plane z+1 overlaps the stencil work of plane z; commit() forms p_i into LDS.
-    double qr[SA], qp[SA], qx[SA], qw[SA];
-#pragma unroll
-    for (int k = 0; k < SA; ++k) qr[k] = qp[k] = qx[k] = qw[k] = 0.0;
-    auto a_cell = [&](int k, int& lx, int& ly, int& gx, int& gy) {
-        const int cell = tid + k * NT;
-        ly = cell / AX;
-        lx = cell - ly * AX;
-        gx = X0 - 2 + lx;
-        gy = Y0 - 2 + ly;
-        if constexpr (INT) return cell < NA;
-        return cell < NA && gx >= 0 && gx < m0 && gy >= 0 && gy < m1;
-    };
-    auto issue = [&](int z) {
-        const size_t zoff = size_t(z) * pl;
-        const bool ownz = z >= z0 && z < z1;
-#pragma unroll
-        for (int k = 0; k < SA; ++k) {
-            int lx, ly, gx, gy;
-            if (a_cell(k, lx, ly, gx, gy)) {
-                const size_t gi = zoff + size_t(gy) * m0 + gx;
-                if (MODE == 0) {
-                    qx[k] = a.x[gi];
-                } else {
-                    qr[k] = a.r_in[gi];
-                    if (MODE == 2) qp[k] = a.p_in[gi];
-                    if (WM == W_DIAG) qw[k] = a.wdiag[gi];
-                    if (ownz && lx >= 2 && lx < TX + 2 && ly >= 2 && ly < TY + 2) qx[k] = a.x[gi];
-                }
-            }
-        }
-    };
-    auto commit = [&](int z) {
-        const size_t zoff = size_t(z) * pl;
-        const bool ownz = z >= z0 && z < z1;
-#pragma unroll
-        for (int k = 0; k < SA; ++k) {
-            int lx, ly, gx, gy;
-            if (a_cell(k, lx, ly, gx, gy)) {
-                const int cell = tid + k * NT;
-                if (MODE == 0) {
-                    sP[cell] = qx[k];
-                } else {
-                    const double ri = qr[k];
-                    double pi = minv(ri, qw[k], bpat<INT>(gx, gy, z, m0, m1, m2));
-                    if (MODE == 2) pi = fma(beta, qp[k], pi);
-                    sP[cell] = pi;
-                    if (lx >= 1 && lx <= BX && ly >= 1 && ly <= BY) sR[z & 1][(ly - 1) * BX + (lx - 1)] = ri;
-                    if (ownz && lx >= 2 && lx < TX + 2 && ly >= 2 && ly < TY + 2) {
-                        const size_t gi = zoff + size_t(gy) * m0 + gx;
-                        a.p_out[gi] = pi;
-                        a.x[gi] = fma(alpha, pi, qx[k]);
-                    }
-                }
-            }
-        }
-    };
-
-    issue(zs);
-    for (int z = zs; z <= ze; ++z) {
-        // Make tid opaque per plane so the per-slot cell geometry is recomputed instead of hoisted
-        // out of the loop (hoisting it costs ~80 VGPRs and halves the workgroups per CU).
-        asm volatile("" : "+v"(tid));
-        // ---------------- stage A: plane z of p_i (x_0 in the prologue) on tile + 2, r_i on tile + 1
-        commit(z);
-        __syncthreads();
-        if (z + 1 <= ze) issue(z + 1);
-        // ---------------- stage B: plane z feeds s at outputs z-1 (k1), z (k0), z+1 (k1); clamped
-        // dim-2 neighbours: plane 0 is its own dz=-1 layer, plane m2-1 its own dz=+1 layer
-        double bp1[SB];
-#pragma unroll
-        for (int k = 0; k < SB; ++k) {
-            const Cell s = cell_of<BX, NB, AX, INT>(tid + k * NT, X0 - 1, Y0 - 1, X0 - 2, Y0 - 2, m0, m1);
-            double k0v = 0.0, k1v = 0.0, ctr = 0.0;
-            if (s.in) plane_sums(sP, s, a.K, k0v, k1v, ctr);
-            bm1[k] += k1v;
-            b0[k] += k0v + (z == 0 ? k1v : 0.0) + (z == m2 - 1 ? k1v : 0.0);
-            bp1[k] = k1v;
-            pc0[k] = ctr;
-        }
-        bool synced = false;
-        if (z - 1 >= ulo && z - 1 <= uhi) {
-            finish_plane(z - 1, false);
-            synced = true;
-        }
-        if (z == m2 - 1 && z >= ulo && z <= uhi) {
-            finish_plane(z, true);
-            synced = true;
-        }
-        if (!synced) __syncthreads();
-#pragma unroll
-        for (int k = 0; k < SB; ++k) {
-            bm1[k] = b0[k];
-            b0[k] = bp1[k];
-            pcm1[k] = pc0[k];
-        }
-    }
-    block_reduce_store<4, 0, NT>(red, a.partials);
-}
-
 template <int WM, int MODE>
 __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
     using namespace cg3d;
-    __shared__ double sP[NA];      // plane z of p_i (x_0 in the prologue), tile + 2
-    __shared__ double sR[2][NB];   // r_i of planes z-1, z (ping-pong), tile + 1
-    __shared__ double sU[NB];      // u_{i+1} of one plane, tile + 1
-    __shared__ double sD[8];       // 1 / diag (W = I) or sigma diag(D^T D) (W diagonal), by pattern
+    __shared__ double sP[IMG];   // plane z of p_i (x_0 in the prologue)
+    __shared__ double sU[IMG];   // u_{i+1} of one plane
+    __shared__ double sD[8];     // 1 / diag (W = I) or sigma diag(D^T D) (W diagonal), by pattern
     if (MODE != 0 && a.st->done) return;
     const double alpha = MODE == 0 ? 0.0 : a.st->alpha;
     const double beta = MODE == 2 ? a.st->beta : 0.0;
     if (threadIdx.x < 8) sD[threadIdx.x] = WM == W_DIAG ? a.acc[threadIdx.x] : 1.0 / (1.0 + a.acc[threadIdx.x]);
+
+    const int m0 = a.m0, m1 = a.m1, m2 = a.m2;
+    const size_t pl = size_t(m0) * size_t(m1);
     const int nt = a.tiles_x * a.tiles_y;
     // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and b+8 share one),
     // so give each XCD a contiguous run of tiles; neighbouring tiles then share their halo
@@ -315,12 +123,191 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
     const int tz = bid / nt, trem = bid - tz * nt;
     const int ty = trem / a.tiles_x, tx = trem - ty * a.tiles_x;
     const int X0 = tx * TX, Y0 = ty * TY;
-    const int z0 = tz * a.zchunk, z1 = min(a.m2, z0 + a.zchunk);
-    __syncthreads();
-    if (X0 >= 2 && X0 + AX - 2 <= a.m0 && Y0 >= 2 && Y0 + AY - 2 <= a.m1)
-        cg3d_body<WM, MODE, true>(a, sP, sR, sU, sD, X0, Y0, z0, z1, alpha, beta);
-    else
-        cg3d_body<WM, MODE, false>(a, sP, sR, sU, sD, X0, Y0, z0, z1, alpha, beta);
+    const int z0 = tz * a.zchunk, z1 = min(m2, z0 + a.zchunk);
+
+    // per-lane geometry (dim 0), fixed for the launch
+    const int lane = threadIdx.x & 63;
+    const int gx = X0 - 2 + lane;
+    const int gxm = mirror(gx, m0);
+    const uint32_t boff = uint32_t(gxm) * 8u;   // byte offset inside a mesh row
+    const bool own_x = lane >= 2 && lane < IW - 2 && gx < m0;
+    const int xb = int(gxm > 0 && gxm + 1 < m0);
+    // per-row geometry (dim 1): wave-uniform
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int row0 = wv * RPW;
+    size_t rowoff[RPW];
+    int ypat[RPW];
+    bool own_y[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) {
+        const int rho = row0 + k, gy = Y0 - 2 + rho, gym = mirror(gy, m1);
+        rowoff[k] = size_t(gym) * size_t(m0);
+        ypat[k] = int(gym > 0 && gym + 1 < m1) << 1;
+        own_y[k] = rho >= 2 && rho < IH - 2 && gy < m1;
+    }
+    const int li = 1 + (row0 + 1) * IW + lane;   // LDS index of (row0, lane)
+
+    // global element (plane z, slot k) at this lane
+    auto ld = [&](const double* base, size_t zoff, int k) {
+        return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base + zoff + rowoff[k]) + boff);
+    };
+    auto st = [&](double* base, size_t zoff, int k, double v) {
+        *reinterpret_cast<double*>(reinterpret_cast<char*>(base + zoff + rowoff[k]) + boff) = v;
+    };
+    auto zpat = [&](int z) { return int(z > 0 && z + 1 < m2) << 2; };
+    // M^-1 v at (slot k, pattern bits of the plane)
+    auto minv = [&](double v, double wvv, int k, int zp) {
+        const double d = sD[xb | ypat[k] | zp];
+        return WM == W_DIAG ? v / (wvv + d) : v * d;
+    };
+
+    double bm1[RPW], b0[RPW], pcm1[RPW], pc0[RPW];   // s accumulators and p centres, outputs z-1, z
+    double cm1[RPW], c0[RPW], ucm1[RPW];             // w accumulators (outputs e-1, e), u centre at e-1
+    double rm1[RPW], rz[RPW];                        // r_i at planes z-1, z (own loads, never in LDS)
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) bm1[k] = b0[k] = pcm1[k] = pc0[k] = cm1[k] = c0[k] = ucm1[k] = rm1[k] = rz[k] = 0.0;
+    double red[4] = {0.0, 0.0, 0.0, 0.0};   // gamma, delta, |r|^2, |b|^2
+
+    const int zs = max(0, z0 - 2), ze = min(m2 - 1, z1 + 1);
+    const int ulo = max(0, z0 - 1), uhi = min(m2 - 1, z1);   // planes of s and u formed here
+
+    // s of plane e is complete: r_{i+1}, u_{i+1} on tile + 1, then accumulate w = A u.
+    auto finish_plane = [&](int e, bool last) {
+        const size_t eoff = size_t(e) * pl;
+        const bool own = e >= z0 && e < z1;
+        const int zp = zpat(e);
+        double uc[RPW];
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            const double wvv = WM == W_DIAG ? ld(a.wdiag, eoff, k) : 1.0;
+            double se = last ? b0[k] : bm1[k];
+            if (WM == W_DIAG) se = fma(wvv, last ? pc0[k] : pcm1[k], se);
+            const bool tile = own && own_y[k] && own_x;
+            double rn;
+            if (MODE == 0) {
+                const double b = fma(a.cb, ld(a.gb, eoff, k), fma(a.ca, ld(a.ga, eoff, k), ld(a.oty, eoff, k)));
+                rn = b - se;
+                if (tile) red[3] = fma(b, b, red[3]);
+            } else {
+                rn = fma(-alpha, se, last ? rz[k] : rm1[k]);
+            }
+            const double un = minv(rn, wvv, k, zp);
+            sU[li + k * IW] = un;
+            uc[k] = un;
+            if (tile) {
+                st(a.r_out, eoff, k, rn);
+                red[0] = fma(rn, un, red[0]);
+                red[2] = fma(rn, rn, red[2]);
+            }
+        }
+        __syncthreads();
+        double k0v[RPW], k1v[RPW], ctr[RPW];
+        wave_rows(sU + li, a.K, k0v, k1v, ctr);
+        const bool prev_own = e - 1 >= z0 && e - 1 < z1;   // w(e-1) is complete
+        const bool end_own = e == m2 - 1 && own;             // last mesh plane: w(e) is complete too
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            cm1[k] += k1v[k];
+            c0[k] += k0v[k] + (e == 0 ? k1v[k] : 0.0) + (e == m2 - 1 ? k1v[k] : 0.0);
+            if (own_y[k] && own_x) {
+                if (prev_own) {
+                    double wq = cm1[k];
+                    if (WM == W_DIAG) wq = fma(ld(a.wdiag, eoff - pl, k), ucm1[k], wq);
+                    red[1] = fma(wq, ucm1[k], red[1]);
+                }
+                if (end_own) {
+                    double wq = c0[k];
+                    if (WM == W_DIAG) wq = fma(ld(a.wdiag, eoff, k), uc[k], wq);
+                    red[1] = fma(wq, uc[k], red[1]);
+                }
+            }
+            cm1[k] = c0[k];
+            c0[k] = k1v[k];
+            ucm1[k] = uc[k];
+        }
+        // no closing barrier: the next write of sU follows the next plane's post-commit barrier
+    };
+
+    // Stage A is split: issue() loads plane z's inputs into registers one plane ahead, so the HBM
+    // latency of plane z+1 overlaps the stencil work of plane z; commit() forms p_i into LDS.
+    double qr[RPW], qp[RPW], qx[RPW], qw[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; ++k) qr[k] = qp[k] = qx[k] = qw[k] = 0.0;
+    auto issue = [&](int z) {
+        const size_t zoff = size_t(z) * pl;
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            if (MODE == 0) {
+                qx[k] = ld(a.x, zoff, k);
+            } else {
+                qr[k] = ld(a.r_in, zoff, k);
+                if (MODE == 2) qp[k] = ld(a.p_in, zoff, k);
+                if (WM == W_DIAG) qw[k] = ld(a.wdiag, zoff, k);
+                // unconditional (every address is valid): a conditional load into the queue
+                // gets its stores merged with a dynamic index, which demotes qx to scratch
+                qx[k] = ld(a.x, zoff, k);
+            }
+        }
+    };
+    auto commit = [&](int z) {
+        const size_t zoff = size_t(z) * pl;
+        const bool ownz = z >= z0 && z < z1;
+        const int zp = zpat(z);
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            if (MODE == 0) {
+                sP[li + k * IW] = qx[k];
+            } else {
+                double pi = minv(qr[k], qw[k], k, zp);
+                if (MODE == 2) pi = fma(beta, qp[k], pi);
+                sP[li + k * IW] = pi;
+                rz[k] = qr[k];
+                if (ownz && own_y[k] && own_x) {
+                    st(a.p_out, zoff, k, pi);
+                    st(a.x, zoff, k, fma(alpha, pi, qx[k]));
+                }
+            }
+        }
+    };
+
+    __syncthreads();   // sD
+    issue(zs);
+    for (int z = zs; z <= ze; ++z) {
+        // ---------------- stage A: plane z of p_i (x_0 in the prologue) on tile + 2
+        commit(z);
+        __syncthreads();
+        if (z + 1 <= ze) issue(z + 1);
+        // ---------------- stage B: plane z feeds s at outputs z-1 (k1), z (k0), z+1 (k1); clamped
+        // dim-2 neighbours: plane 0 is its own dz=-1 layer, plane m2-1 its own dz=+1 layer
+        double k0v[RPW], k1v[RPW], ctr[RPW], bp1[RPW];
+        wave_rows(sP + li, a.K, k0v, k1v, ctr);
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            bm1[k] += k1v[k];
+            b0[k] += k0v[k] + (z == 0 ? k1v[k] : 0.0) + (z == m2 - 1 ? k1v[k] : 0.0);
+            bp1[k] = k1v[k];
+            pc0[k] = ctr[k];
+        }
+        bool synced = false;
+        if (z - 1 >= ulo && z - 1 <= uhi) {
+            finish_plane(z - 1, false);
+            synced = true;
+        }
+        if (z == m2 - 1 && z >= ulo && z <= uhi) {
+            if (synced) __syncthreads();   // sU is still being read by the previous plane's stage C
+            finish_plane(z, true);
+            synced = true;
+        }
+        if (!synced) __syncthreads();   // stage B's reads of sP before the next commit
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            bm1[k] = b0[k];
+            b0[k] = bp1[k];
+            pcm1[k] = pc0[k];
+            rm1[k] = rz[k];
+        }
+    }
+    block_reduce_store<4, 0, NT>(red, a.partials);
 }
 
 // ------------------------------------------------------------------------------------ launcher
@@ -336,7 +323,28 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
     a.tiles_x = (a.m0 + TX - 1) / TX;
     a.tiles_y = (a.m1 + TY - 1) / TY;
     const int tiles = a.tiles_x * a.tiles_y;
-    int nz = std::max(1, std::min(a.m2 / 16, (1024 + tiles - 1) / tiles));
+    // dim-2 chunks: each costs 3 extra plane steps (halo planes); workgroups run in rounds of
+    // `slots` (2 per CU), so pick the chunk count with the fewest plane steps per slot
+    static const int slots = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        return 2 * std::max(1, cus);
+    }();
+    static const int nz_env = [] {
+        const char* e = getenv("MVTV_CG3D_NZ");
+        return e ? atoi(e) : 0;
+    }();
+    int nz = 1;
+    long best = -1;
+    for (int c = 1; c <= a.m2 && c * tiles <= kMaxCgBlocks; ++c) {
+        const int zc = (a.m2 + c - 1) / c;
+        if ((a.m2 + zc - 1) / zc != c) continue;   // same chunking as a smaller count
+        const long cost = long((c * tiles + slots - 1) / slots) * (zc + 3);
+        if (best < 0 || cost < best) best = cost, nz = c;
+    }
+    if (nz_env > 0) nz = std::min(nz_env, a.m2);
     a.zchunk = (a.m2 + nz - 1) / nz;
     nz = (a.m2 + a.zchunk - 1) / a.zchunk;
     const int nblocks = tiles * nz;
@@ -360,6 +368,7 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
         a.K[t] = sigma * kk;
         a.acc[t] = sigma * dd;
     }
+    if (wmode != W_DIAG) a.K[0] += 1.0;   // W = I folded into the centre weight
     a.wdiag = wdiag;
     a.x = x;
     a.r_in = r_in;
