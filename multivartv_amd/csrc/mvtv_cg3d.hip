@@ -68,7 +68,7 @@ struct Cg3dArgs {
     double K[8];     // sigma * D^T D weight at |dx| + 2 |dy| + 4 |dz| (+1 at [0] when W = I)
     double acc[8];   // sigma * diag(D^T D) by boundary pattern (bit j: interior along dim j)
     double ca, cb;
-    int m0, m1, m2, tiles_x, tiles_y, zchunk;
+    int m0, m1, m2, tiles_x, tiles_y, zchunk, nblocks;
 };
 
 // Half-sample mirror into [0, m): -1 -> 0, -2 -> 1, m -> m-1, m+1 -> m-2; clamped beyond.
@@ -116,10 +116,15 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
     const size_t pl = size_t(m0) * size_t(m1);
     const int nt = a.tiles_x * a.tiles_y;
     // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and b+8 share one),
-    // so give each XCD a contiguous run of tiles; neighbouring tiles then share their halo
-    // lines in that XCD's L2. Placement affects speed only, never results.
-    int bid = blockIdx.x;
-    if ((gridDim.x & 7) == 0) bid = (bid & 7) * (gridDim.x >> 3) + (bid >> 3);
+    // so give each XCD a contiguous run of tiles (a compact patch of tile rows): a tile's halo
+    // lines are then its neighbours' own lines, fetched once into that XCD's L2. The grid is
+    // padded to a multiple of 8; padding workgroups contribute zero partials. Placement
+    // affects speed only, never results.
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    if (bid >= a.nblocks) {
+        if (threadIdx.x < 4) a.partials[blockIdx.x * 4 + threadIdx.x] = 0.0;
+        return;
+    }
     const int tz = bid / nt, trem = bid - tz * nt;
     const int ty = trem / a.tiles_x, tx = trem - ty * a.tiles_x;
     const int X0 = tx * TX, Y0 = ty * TY;
@@ -135,13 +140,15 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
     // per-row geometry (dim 1): wave-uniform
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int row0 = wv * RPW;
-    size_t rowoff[RPW];
+    size_t rowoff[RPW], xrowoff[RPW];
     int ypat[RPW];
     bool own_y[RPW];
 #pragma unroll
     for (int k = 0; k < RPW; ++k) {
         const int rho = row0 + k, gy = Y0 - 2 + rho, gym = mirror(gy, m1);
         rowoff[k] = size_t(gym) * size_t(m0);
+        // x is needed on tile rows only; halo rows load a tile row's lines instead (L2 hits)
+        xrowoff[k] = size_t(mirror(Y0 - 2 + min(max(rho, 2), IH - 3), m1)) * size_t(m0);
         ypat[k] = int(gym > 0 && gym + 1 < m1) << 1;
         own_y[k] = rho >= 2 && rho < IH - 2 && gy < m1;
     }
@@ -151,8 +158,10 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
     auto ld = [&](const double* base, size_t zoff, int k) {
         return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base + zoff + rowoff[k]) + boff);
     };
+    // stores are non-temporal: nothing written is read again in this launch, and keeping them
+    // out of L2 leaves it to the halo lines that neighbouring tiles read
     auto st = [&](double* base, size_t zoff, int k, double v) {
-        *reinterpret_cast<double*>(reinterpret_cast<char*>(base + zoff + rowoff[k]) + boff) = v;
+        __builtin_nontemporal_store(v, reinterpret_cast<double*>(reinterpret_cast<char*>(base + zoff + rowoff[k]) + boff));
     };
     auto zpat = [&](int z) { return int(z > 0 && z + 1 < m2) << 2; };
     // M^-1 v at (slot k, pattern bits of the plane)
@@ -245,7 +254,8 @@ __global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
                 if (WM == W_DIAG) qw[k] = ld(a.wdiag, zoff, k);
                 // unconditional (every address is valid): a conditional load into the queue
                 // gets its stores merged with a dynamic index, which demotes qx to scratch
-                qx[k] = ld(a.x, zoff, k);
+                qx[k] = *reinterpret_cast<const double*>(
+                    reinterpret_cast<const char*>(a.x + zoff + xrowoff[k]) + boff);
             }
         }
     };
@@ -338,7 +348,7 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
     }();
     int nz = 1;
     long best = -1;
-    for (int c = 1; c <= a.m2 && c * tiles <= kMaxCgBlocks; ++c) {
+    for (int c = 1; c <= a.m2 && c * tiles + 7 <= kMaxCgBlocks; ++c) {
         const int zc = (a.m2 + c - 1) / c;
         if ((a.m2 + zc - 1) / zc != c) continue;   // same chunking as a smaller count
         const long cost = long((c * tiles + slots - 1) / slots) * (zc + 3);
@@ -347,7 +357,8 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
     if (nz_env > 0) nz = std::min(nz_env, a.m2);
     a.zchunk = (a.m2 + nz - 1) / nz;
     nz = (a.m2 + a.zchunk - 1) / a.zchunk;
-    const int nblocks = tiles * nz;
+    a.nblocks = tiles * nz;
+    const int nblocks = (a.nblocks + 7) / 8 * 8;   // grid, padded for the XCD mapping
     if (nblocks > kMaxCgBlocks) return hipErrorInvalidValue;
     if (nblocks_out) *nblocks_out = nblocks;
     // K(o) = sum_S cS[S] prod_j f_j(o_j) with f = (j in S) ? (o == 0 ? 2 : -1) : (o == 0 ? 1 : 0):
