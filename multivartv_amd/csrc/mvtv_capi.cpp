@@ -110,12 +110,13 @@ struct mvtv_problem {
     int tstart(int kid) {
         if (!timing) return -1;
         Pending pd{get_event(), get_event(), kid};
-        (void)hipEventRecord(pd.a, stream);
+        g_timed = TimedLaunch{pd.a, pd.b};   // stamped by the next kernel dispatch (klaunch)
         pending.push_back(pd);
         return int(pending.size()) - 1;
     }
     void tstop(int h) {
-        if (h >= 0) (void)hipEventRecord(pending[h].b, stream);
+        if (h >= 0 && g_timed.start) pending[h].kid = -1;   // the launcher enqueued nothing
+        g_timed = TimedLaunch{};
     }
     void harvest() {  // call after a stream sync
         for (auto& pd : pending) {

@@ -394,7 +394,7 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
     a.st = st;
     a.partials = partials;
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(nblocks), dim3(NT), 0, s, a);
+        klaunch(kern, dim3(nblocks), dim3(NT), 0, s, a);
         return hipGetLastError();
     };
     if (wmode == W_DIAG) {

@@ -10,6 +10,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 namespace mvtv {
@@ -106,6 +107,26 @@ struct Launch {
     hipStream_t stream;
     int grid;
 };
+
+// Kernel timing (mvtv_capi.cpp instrumentation). When a start/stop pair is armed, the next launch
+// goes through hipExtLaunchKernelGGL, which stamps the events from the kernel's own dispatch packet
+// (the begin/end rocprofv3 reports). Separate hipEventRecord markers around a launch would add a
+// barrier packet plus a cache release/acquire each, inflating the measured duration.
+struct TimedLaunch {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local TimedLaunch g_timed;
+
+template <typename F, typename... Args>
+inline void klaunch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
+    if (g_timed.start) {
+        const TimedLaunch t = g_timed;
+        g_timed = TimedLaunch{};
+        hipExtLaunchKernelGGL(kernel, grid, block, shmem, s, t.start, t.stop, 0u, args...);
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, shmem, s, args...);
+    }
+}
 
 hipError_t launch_edge_update(const Geom& g, int order, int umode, const Launch& L, const double* theta,
                               double* edges, double t_old, double c_old, double t_new, const double* theta_old,

@@ -18,6 +18,8 @@
 
 namespace mvtv {
 
+thread_local TimedLaunch g_timed;
+
 // Jacobi diagonal of W + sigma * sum_S cS[S] (x)_{j in S} L_j at a node with multi-index c:
 // the 1-D Neumann Laplacian's diagonal is (c > 0) + (c < m - 1).
 template <int P, int WM>
@@ -521,7 +523,7 @@ hipError_t launch_edge_update(const Geom& g, int order, int umode, const Launch&
     return dispatch_p(g.p, [&](auto pc) {
         constexpr int P = decltype(pc)::value;
         auto go = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(L.grid), dim3(kThreads), 0, L.stream, g, theta, edges, t_old, c_old, t_new,
+            klaunch(kern, dim3(L.grid), dim3(kThreads), 0, L.stream, g, theta, edges, t_old, c_old, t_new,
                                theta_old, partials);
             return hipGetLastError();
         };
@@ -542,7 +544,7 @@ hipError_t launch_gather(const Geom& g, int order, int umode, const Launch& L, c
     return dispatch_p(g.p, [&](auto pc) {
         constexpr int P = decltype(pc)::value;
         auto go = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(L.grid), dim3(kThreads), 0, L.stream, g, edges, t, g_alpha, g_u, g_uprev,
+            klaunch(kern, dim3(L.grid), dim3(kThreads), 0, L.stream, g, edges, t, g_alpha, g_u, g_uprev,
                                c_prev, partials);
             return hipGetLastError();
         };
@@ -560,9 +562,9 @@ hipError_t launch_apply_D_padded(const Geom& g, int order, const Launch& L, cons
     return dispatch_p(g.p, [&](auto pc) {
         constexpr int P = decltype(pc)::value;
         if (order == 0)
-            hipLaunchKernelGGL((k_apply_D<P, 0>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, theta, edges);
+            klaunch((k_apply_D<P, 0>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, theta, edges);
         else
-            hipLaunchKernelGGL((k_apply_D<P, 1>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, theta, edges);
+            klaunch((k_apply_D<P, 1>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, theta, edges);
         return hipGetLastError();
     });
 }
@@ -571,9 +573,9 @@ hipError_t launch_edges_fill_valid(const Geom& g, int order, const Launch& L, do
     return dispatch_p(g.p, [&](auto pc) {
         constexpr int P = decltype(pc)::value;
         if (order == 0)
-            hipLaunchKernelGGL((k_edges_fill_valid<P, 0>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, edges, value);
+            klaunch((k_edges_fill_valid<P, 0>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, edges, value);
         else
-            hipLaunchKernelGGL((k_edges_fill_valid<P, 1>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, edges, value);
+            klaunch((k_edges_fill_valid<P, 1>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, edges, value);
         return hipGetLastError();
     });
 }
@@ -586,13 +588,13 @@ hipError_t launch_apply_A(const Geom& g, const Launch& L, double sigma, int wmod
         return dispatch_w(wmode, [&](auto wc) {
             constexpr int WM = decltype(wc)::value;
             if (partials && st)
-                hipLaunchKernelGGL((k_apply_A<P, WM, true, true>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sk,
+                klaunch((k_apply_A<P, WM, true, true>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sk,
                                    sigma, wdiag, x, q, partials, st);
             else if (partials)
-                hipLaunchKernelGGL((k_apply_A<P, WM, true, false>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sk,
+                klaunch((k_apply_A<P, WM, true, false>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sk,
                                    sigma, wdiag, x, q, partials, st);
             else
-                hipLaunchKernelGGL((k_apply_A<P, WM, false, false>), dim3(L.grid), dim3(kThreads), 0, L.stream, g,
+                klaunch((k_apply_A<P, WM, false, false>), dim3(L.grid), dim3(kThreads), 0, L.stream, g,
                                    sk, sigma, wdiag, x, q, partials, st);
             return hipGetLastError();
         });
@@ -607,7 +609,7 @@ hipError_t launch_pcg_init(const Geom& g, const Launch& L, double sigma, int wmo
         constexpr int P = decltype(pc)::value;
         return dispatch_w(wmode, [&](auto wc) {
             constexpr int WM = decltype(wc)::value;
-            hipLaunchKernelGGL((k_pcg_init<P, WM>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sk, sigma, wdiag,
+            klaunch((k_pcg_init<P, WM>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sk, sigma, wdiag,
                                oty, ga, ca, gb, cb, x, r, p, partials);
             return hipGetLastError();
         });
@@ -621,7 +623,7 @@ hipError_t launch_pcg_update(const Geom& g, const Launch& L, double sigma, int w
         constexpr int P = decltype(pc)::value;
         return dispatch_w(wmode, [&](auto wc) {
             constexpr int WM = decltype(wc)::value;
-            hipLaunchKernelGGL((k_pcg_update<P, WM>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sigma, wdiag, x,
+            klaunch((k_pcg_update<P, WM>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sigma, wdiag, x,
                                r, p, q, st, partials);
             return hipGetLastError();
         });
@@ -634,7 +636,7 @@ hipError_t launch_pcg_pupdate(const Geom& g, const Launch& L, double sigma, int 
         constexpr int P = decltype(pc)::value;
         return dispatch_w(wmode, [&](auto wc) {
             constexpr int WM = decltype(wc)::value;
-            hipLaunchKernelGGL((k_pcg_pupdate<P, WM>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sigma, wdiag, r,
+            klaunch((k_pcg_pupdate<P, WM>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sigma, wdiag, r,
                                p, st);
             return hipGetLastError();
         });
@@ -643,41 +645,41 @@ hipError_t launch_pcg_pupdate(const Geom& g, const Launch& L, double sigma, int 
 
 hipError_t launch_finalize(hipStream_t s, const double* partials, int nparts, int nr, int nmax, int op, double* out,
                            PcgState* st, double rtol2, int maxit) {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, s, partials, nparts, nr, nmax, op, out, st, rtol2, maxit);
+    klaunch(k_finalize, dim3(1), dim3(1024), 0, s, partials, nparts, nr, nmax, op, out, st, rtol2, maxit);
     return hipGetLastError();
 }
 
 hipError_t launch_maxabsdiff(const Geom& g, const Launch& L, const double* a, const double* b, double* partials) {
-    hipLaunchKernelGGL(k_maxabsdiff, dim3(L.grid), dim3(kThreads), 0, L.stream, g.N, a, b, partials);
+    klaunch(k_maxabsdiff, dim3(L.grid), dim3(kThreads), 0, L.stream, g.N, a, b, partials);
     return hipGetLastError();
 }
 
 hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n) {
-    hipLaunchKernelGGL(k_fill, dim3(elem_grid(n)), dim3(256), 0, s, x, v, n);
+    klaunch(k_fill, dim3(elem_grid(n)), dim3(256), 0, s, x, v, n);
     return hipGetLastError();
 }
 
 hipError_t launch_edges_import(const Geom& g, int order, hipStream_t s, int k, uint64_t e0, uint64_t cnt,
                                const double* compact, double* padded) {
-    hipLaunchKernelGGL(k_edges_import, dim3(elem_grid(cnt)), dim3(256), 0, s, red_dims(g, order, k),
+    klaunch(k_edges_import, dim3(elem_grid(cnt)), dim3(256), 0, s, red_dims(g, order, k),
                        uint64_t(k) * g.N, e0, cnt, compact, padded);
     return hipGetLastError();
 }
 
 hipError_t launch_edges_export(const Geom& g, int order, hipStream_t s, int k, uint64_t e0, uint64_t cnt,
                                const double* padded, double* compact, int umode, double t, double c) {
-    hipLaunchKernelGGL(k_edges_export, dim3(elem_grid(cnt)), dim3(256), 0, s, red_dims(g, order, k),
+    klaunch(k_edges_export, dim3(elem_grid(cnt)), dim3(256), 0, s, red_dims(g, order, k),
                        uint64_t(k) * g.N, e0, cnt, padded, compact, umode, t, c);
     return hipGetLastError();
 }
 
 hipError_t launch_edges_z_to_u(hipStream_t s, double* edges, uint64_t n, double t, double c) {
-    hipLaunchKernelGGL(k_edges_z_to_u, dim3(elem_grid(n)), dim3(256), 0, s, edges, n, t, c);
+    klaunch(k_edges_z_to_u, dim3(elem_grid(n)), dim3(256), 0, s, edges, n, t, c);
     return hipGetLastError();
 }
 
 hipError_t launch_gather_index(hipStream_t s, const double* theta, const int64_t* idx, int64_t n, double* out) {
-    hipLaunchKernelGGL(k_gather_index, dim3(elem_grid(uint64_t(n))), dim3(256), 0, s, theta, idx, n, out);
+    klaunch(k_gather_index, dim3(elem_grid(uint64_t(n))), dim3(256), 0, s, theta, idx, n, out);
     return hipGetLastError();
 }
 
