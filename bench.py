@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--dims", type=int, default=3)
     ap.add_argument("--lam", type=float, default=1.0)
     ap.add_argument("--pcg-rtol", type=float, default=1e-10)
+    ap.add_argument("--solver", choices=["auto", "pcg", "spectral"], default="auto",
+                    help="theta-solve: auto = spectral (exact DCT solve) where it applies, else Jacobi-PCG")
+    ap.add_argument("--pcg-steps", type=int, default=10,
+                    help="steps of the secondary Jacobi-PCG leg reported beside the main one (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-planes", type=int, default=0,
                     help="cpu_baseline sample: slowest-dim planes of the mesh (0 = auto)")
@@ -127,19 +131,43 @@ def main():
     del y
     log(f"[rank {D.rank}] setup {time.perf_counter() - t_setup:.1f}s: N={P.N} E={P.E} blocks={P.nb}")
 
-    opts = dict(fixed_iters=a.warmup, pcg_rtol=a.pcg_rtol)
+    solver = {"auto": mv.SOLVER_AUTO, "pcg": mv.SOLVER_PCG, "spectral": mv.SOLVER_SPECTRAL}[a.solver]
+    opts = dict(fixed_iters=a.warmup, pcg_rtol=a.pcg_rtol, theta_solver=solver)
     if a.warmup > 0:
         P.run(lam, **opts)
     D.barrier()
     P.timing(True)
     t0 = time.perf_counter()
-    st = P.run(lam, fixed_iters=a.steps, pcg_rtol=a.pcg_rtol)   # returns after the stream has drained
+    st = P.run(lam, fixed_iters=a.steps, pcg_rtol=a.pcg_rtol, theta_solver=solver)   # returns after the stream drained
     t1 = time.perf_counter()
     D.barrier()
     elapsed = t1 - t0
     tim = P.timings()
     P.timing(False)
+    used = "spectral" if st["theta_solver"] == mv.SOLVER_SPECTRAL else "pcg"
     kbar = st["pcg_iters"] / max(1, a.steps)
+    moved = sum(v["bytes_per_launch"] * v["launches"] for v in tim.values()) / max(1, a.steps)
+
+    # secondary leg: the north star's Jacobi-PCG theta-solve on the same state (reported, not the value)
+    pcg_leg = None
+    if used == "spectral" and a.pcg_steps > 0:
+        P.run(lam, fixed_iters=1, pcg_rtol=a.pcg_rtol, theta_solver=mv.SOLVER_PCG)   # warm the PCG poll schedule
+        D.barrier()
+        P.timing(True)
+        tp0 = time.perf_counter()
+        sp = P.run(lam, fixed_iters=a.pcg_steps, pcg_rtol=a.pcg_rtol, theta_solver=mv.SOLVER_PCG)
+        tp1 = time.perf_counter()
+        D.barrier()
+        tp = P.timings()
+        P.timing(False)
+        g_tp, = D.allreduce([tp1 - tp0], "max")
+        fk = tp["pcg_fused3d"] if tp["pcg_fused3d"]["launches"] else tp["pcg_apply_A"]
+        pk_ms = fk["ms"] / max(1, fk["launches"])
+        pcg_leg = {"value": round(D.world * a.pcg_steps / g_tp, 4), "steps": a.pcg_steps,
+                   "pcg_iters_mean": round(sp["pcg_iters"] / a.pcg_steps, 2),
+                   "kernel": "pcg_fused3d" if tp["pcg_fused3d"]["launches"] else "pcg_apply_A",
+                   "kernel_avg_ms": round(pk_ms, 4),
+                   "kernel_GBps": round(fk["bytes_per_launch"] / (pk_ms * 1e-3) / 1e9, 1) if fk["launches"] else None}
     g_elapsed, = D.allreduce([elapsed], "max")
     # global residual all-reduce over the independent fits
     r2, s2, n_unconv = D.allreduce([st["r_norm"] ** 2, st["s_norm"] ** 2, float(st["pcg_unconverged"])], "sum")
@@ -157,15 +185,15 @@ def main():
     d_avg_ms = tim[dom]["ms"] / tim[dom]["launches"]
     achieved = tim[dom]["bytes_per_launch"] / (d_avg_ms * 1e-3) / 1e9
     N, E = P.N, P.E
-    iter_bytes = 8.0 * (5 * E + 8 * N + 10 * kbar * N)          # SURVEY §8d algorithmic bytes per ADMM iteration
-    iter_gbps = iter_bytes * a.steps / elapsed / 1e9
+    iter_gbps = moved * a.steps / elapsed / 1e9                  # algorithmic bytes of every kernel launched
     pmc = load_pmc(dom)
 
     cpu = None
     if D.world == 1 and not a.no_cpu:
         planes = a.cpu_planes or max(4, m[-1] // 8)
         try:
-            cpu = cpu_baseline(m, lam, max(1, round(kbar)), planes)
+            k_cpu = pcg_leg["pcg_iters_mean"] if pcg_leg else kbar   # the oracle's theta-solve is PCG
+            cpu = cpu_baseline(m, lam, max(1, round(k_cpu)), planes)
         except Exception as e:  # the baseline is reported, never required
             log(f"cpu_baseline failed: {e}")
     P.close()
@@ -187,14 +215,17 @@ def main():
             "data": "synthetic: 3D towers + 0.5 N(0,1) (splitmix64/Box-Muller, seed 0x4D565456 + rank), O = I",
             "config": {"workload": f"{a.dims}D {a.size}^{a.dims} fp64 mesh-TV ADMM, variant B (rcpp admm_update), "
                                    f"lambda={lam}, fixed-iteration mode",
+                       "theta_solver": used,
                        "mesh": m, "nodes": N, "edges": E, "pcg_rtol": a.pcg_rtol, "pcg_iters_mean": round(kbar_all, 2),
                        "parallelism": "independent mesh fits, one per GPU" if D.world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": pmc, "bytes_per_launch": tim[dom]["bytes_per_launch"],
                          "avg_launch_ms": round(d_avg_ms, 4)},
-            "iteration_hbm": {"bytes_per_iter": iter_bytes, "GBps": round(iter_gbps, 1),
-                              "frac": round(iter_gbps / (HBM_PEAK_GBPS * 1), 4)},
+            "iteration_hbm": {"bytes_per_iter": moved, "GBps": round(iter_gbps, 1),
+                              "frac": round(iter_gbps / HBM_PEAK_GBPS, 4),
+                              "survey_bytes_per_iter": 8.0 * (5 * E + 8 * N + 10 * kbar * N)},
+            "pcg_leg": pcg_leg,
             "kernels": per,
             "residuals": {"r_norm": float(np.sqrt(r2)), "s_norm": float(np.sqrt(s2)),
                           "pcg_unconverged": int(n_unconv)},

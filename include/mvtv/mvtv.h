@@ -79,7 +79,17 @@ typedef struct mvtv_admm_opts {
     int32_t pcg_max_iter;   /* <= 0: 20000 */
     int32_t pcg_strict;     /* != 0: report MVTV_PCG_NOT_CONVERGED when a theta-solve stops at pcg_max_iter */
     int32_t verbose;        /* != 0: print "Lambda= .., Counter = .." like rcpp…/solvers.cpp:134 */
+    int32_t theta_solver;   /* mvtv_theta_solver: how spsolve(spcrosses, b) (rcpp…/solvers.cpp:113) is replaced */
 } mvtv_admm_opts;
+
+/* theta-solve of (W + sigma D^T D) theta = b. The reference factorises with SuperLU every
+ * iteration (rcpp…/solvers.cpp:113, cpp-code/solvers.cpp:116, code/solvers.py:72). */
+typedef enum mvtv_theta_solver {
+    MVTV_SOLVER_AUTO = 0,      /* SPECTRAL where it is exact, else PCG */
+    MVTV_SOLVER_PCG = 1,       /* Jacobi-PCG on the 3^p-point stencil, warm-started, pcg_rtol */
+    MVTV_SOLVER_SPECTRAL = 2   /* direct: cosine transforms + diagonal divide. Exact for W = I (mesh == data)
+                                  with every m_j a power of two <= 4096; MVTV_BAD_ARG otherwise */
+} mvtv_theta_solver;
 
 typedef struct mvtv_admm_stats {
     int32_t iters;          /* ADMM iterations executed */
@@ -92,6 +102,7 @@ typedef struct mvtv_admm_stats {
     int32_t pcg_iters_max;  /* max PCG iterations in one theta-solve */
     int32_t pcg_unconverged;/* theta-solves that hit pcg_max_iter */
     double seconds;         /* wall time of the call */
+    int32_t theta_solver;   /* the solver that ran (MVTV_SOLVER_PCG or MVTV_SOLVER_SPECTRAL) */
 } mvtv_admm_stats;
 
 typedef struct mvtv_problem mvtv_problem;
@@ -114,6 +125,8 @@ int32_t mvtv_problem_blocks(const mvtv_problem* prob);
 mvtv_status mvtv_problem_block_info(const mvtv_problem* prob, int32_t k, int32_t* code, int32_t* sprime, double* weight);
 /* new O^T y and W for the same mesh (CV folds re-run create_cache_objects, rcpp…/solvers.cpp:347-348) */
 mvtv_status mvtv_problem_set_data(mvtv_problem* prob, const double* oty, const double* wdiag);
+/* 1 if MVTV_SOLVER_SPECTRAL applies to this problem (W = I, power-of-two m_j <= 4096), else 0 */
+int32_t mvtv_problem_spectral_ok(const mvtv_problem* prob);
 
 /* ---- the hot path ------------------------------------------------------------------ */
 /* Drop-in for admm_update:
@@ -142,6 +155,8 @@ mvtv_status mvtv_apply_Dt(mvtv_problem* prob, const double* v, double* g_out);  
 mvtv_status mvtv_apply_A(mvtv_problem* prob, double sigma, const double* x, double* q_out); /* (W + sigma D^T D) x */
 mvtv_status mvtv_solve(mvtv_problem* prob, double sigma, const double* b, double* x_inout,
                        double rtol, int32_t max_iter, int32_t* iters, double* relres);
+/* direct theta-solve (I + sigma D^T D) x = b by cosine transforms (MVTV_SOLVER_SPECTRAL) */
+mvtv_status mvtv_solve_spectral(mvtv_problem* prob, double sigma, const double* b, double* x_out);
 
 /* ---- instrumentation (HIP events on the solver's stream) ---------------------------- */
 typedef enum mvtv_kernel_id {
@@ -154,7 +169,9 @@ typedef enum mvtv_kernel_id {
     MVTV_K_REDUCE = 6,        /* partial-sum finalisation / PCG scalars */
     MVTV_K_OTHER = 7,
     MVTV_K_PCG_FUSED = 8,     /* 3-D fused Chronopoulos-Gear iteration: p, A p, r, A M^-1 r, x in one pass */
-    MVTV_K_COUNT = 9
+    MVTV_K_DCT_FIRST = 9,     /* spectral solve, first pass: b formed on load, DCT along dim 0 */
+    MVTV_K_DCT = 10,          /* spectral solve, other passes (DCT / divide / inverse DCT along one dim) */
+    MVTV_K_COUNT = 11
 } mvtv_kernel_id;
 mvtv_status mvtv_timing_enable(mvtv_problem* prob, int32_t on);
 mvtv_status mvtv_timing_get(mvtv_problem* prob, int32_t kernel_id, double* total_ms, int64_t* launches,

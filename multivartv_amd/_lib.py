@@ -19,7 +19,8 @@ MVTV_HIP_ERROR, MVTV_NO_DEVICE, MVTV_OUT_OF_MEMORY, MVTV_PCG_NOT_CONVERGED = 4, 
 VARIANT_RCPP, VARIANT_CPP, VARIANT_PY = 0, 1, 2
 ORDER_CPP, ORDER_PY = 0, 1
 KERNELS = ["edge_update", "gather_Dt", "pcg_init", "pcg_apply_A", "pcg_update", "pcg_direction", "reduce", "other",
-           "pcg_fused3d"]
+           "pcg_fused3d", "dct_first", "dct"]
+SOLVER_AUTO, SOLVER_PCG, SOLVER_SPECTRAL = 0, 1, 2
 
 _dp = C.POINTER(C.c_double)
 
@@ -33,14 +34,14 @@ class AdmmOpts(C.Structure):
     _fields_ = [("variant", C.c_int32), ("tol", C.c_double), ("max_counter", C.c_int32),
                 ("fixed_iters", C.c_int32), ("sigma", C.c_double), ("ymean", C.c_double),
                 ("pcg_rtol", C.c_double), ("pcg_max_iter", C.c_int32), ("pcg_strict", C.c_int32),
-                ("verbose", C.c_int32)]
+                ("verbose", C.c_int32), ("theta_solver", C.c_int32)]
 
 
 class AdmmStats(C.Structure):
     _fields_ = [("iters", C.c_int32), ("status", C.c_int32), ("r_norm", C.c_double), ("s_norm", C.c_double),
                 ("eps_pri", C.c_double), ("eps_dual", C.c_double), ("rho", C.c_double),
                 ("dtheta_max", C.c_double), ("pcg_iters", C.c_int64), ("pcg_iters_max", C.c_int32),
-                ("pcg_unconverged", C.c_int32), ("seconds", C.c_double)]
+                ("pcg_unconverged", C.c_int32), ("seconds", C.c_double), ("theta_solver", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -76,6 +77,7 @@ SIGNATURES = {
     "mvtv_problem_blocks": (C.c_int32, [C.c_void_p]),
     "mvtv_problem_block_info": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), _dp]),
     "mvtv_problem_set_data": (C.c_int, [C.c_void_p, _dp, _dp]),
+    "mvtv_problem_spectral_ok": (C.c_int32, [C.c_void_p]),
     "mvtv_admm": (C.c_int, [C.c_void_p, C.POINTER(AdmmOpts), C.c_double, _dp, _dp, _dp, C.POINTER(AdmmStats)]),
     "mvtv_state_set": (C.c_int, [C.c_void_p, _dp, _dp, C.c_double]),
     "mvtv_state_get": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
@@ -85,6 +87,7 @@ SIGNATURES = {
     "mvtv_apply_Dt": (C.c_int, [C.c_void_p, _dp, _dp]),
     "mvtv_apply_A": (C.c_int, [C.c_void_p, C.c_double, _dp, _dp]),
     "mvtv_solve": (C.c_int, [C.c_void_p, C.c_double, _dp, _dp, C.c_double, C.c_int32, C.POINTER(C.c_int32), _dp]),
+    "mvtv_solve_spectral": (C.c_int, [C.c_void_p, C.c_double, _dp, _dp]),
     "mvtv_timing_enable": (C.c_int, [C.c_void_p, C.c_int32]),
     "mvtv_timing_get": (C.c_int, [C.c_void_p, C.c_int32, _dp, C.POINTER(C.c_int64), _dp]),
     "mvtv_kernel_name": (C.c_char_p, [C.c_int32]),
@@ -284,6 +287,15 @@ class Problem:
         _check(lib().mvtv_solve(self._h, float(sigma), _ptr(bb), _ptr(x), float(rtol), int(max_iter),
                                 C.byref(it), C.byref(rr)))
         return x, it.value, rr.value
+
+    def spectral_ok(self) -> bool:
+        return bool(lib().mvtv_problem_spectral_ok(self._h))
+
+    def solve_spectral(self, sigma, b):
+        bb = _f64(b, self.N)
+        x = np.empty(self.N)
+        _check(lib().mvtv_solve_spectral(self._h, float(sigma), _ptr(bb), _ptr(x)))
+        return x
 
     # ---- instrumentation --------------------------------------------------------------------
     def timing(self, on=True):

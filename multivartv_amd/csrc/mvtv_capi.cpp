@@ -77,6 +77,8 @@ struct mvtv_problem {
     size_t stage_n = 0;
     double* host_red = nullptr;   // pinned: reductions + PcgState mirror
     PcgState* host_st = nullptr;
+    SpecPlan spec;                // spectral theta-solve tables (allocated when the mesh allows it)
+    bool spec_mesh = false;       // every m_j a power of two <= 4096
 
     // resident ADMM state
     bool have_state = false;
@@ -166,6 +168,9 @@ void free_all(mvtv_problem* P) {
             *b = nullptr;
         }
     if (P->st) (void)hipFree(P->st);
+    for (double* t : {P->spec.tw, P->spec.twq, P->spec.lam})
+        if (t) (void)hipFree(t);
+    P->spec = SpecPlan{};
     if (P->host_red) (void)hipHostFree(P->host_red);
     for (auto& pd : P->pending) {
         (void)hipEventDestroy(pd.a);
@@ -299,6 +304,67 @@ mvtv_status pcg_solve(mvtv_problem* P, double sigma, const double* oty, const do
     *iters = P->host_st->iter;
     P->pcg_hint = *iters;
     *relres = P->host_st->bnorm2 > 0 ? std::sqrt(P->host_st->rnorm2 / P->host_st->bnorm2) : 0.0;
+    return MVTV_OK;
+}
+
+bool spectral_ok(const mvtv_problem* P) { return P->spec_mesh && P->wmode == W_IDENTITY; }
+
+// Device tables of the spectral solve. Twiddles and eigenvalues are evaluated in long double.
+mvtv_status spectral_plan(mvtv_problem* P) {
+    std::vector<double> tw, twq, lam;
+    SpecPlan& sp = P->spec;
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (int j = 0; j < P->g.p; ++j) {
+        const uint32_t m = P->g.m[j];
+        sp.tw_off[j] = uint32_t(tw.size());
+        sp.twq_off[j] = uint32_t(twq.size());
+        sp.lam_off[j] = uint32_t(lam.size());
+        for (uint32_t k = 0; k < m / 2; ++k) {
+            const long double a = -2.0L * pi * k / m;
+            tw.push_back(double(cosl(a)));
+            tw.push_back(double(sinl(a)));
+        }
+        for (uint32_t k = 0; k < m; ++k) {
+            const long double a = -pi * k / (2.0L * m);
+            twq.push_back(double(cosl(a)));
+            twq.push_back(double(sinl(a)));
+            const long double sn = sinl(pi * k / (2.0L * m));
+            lam.push_back(double(4.0L * sn * sn));
+        }
+    }
+    auto up = [&](double** dst, const std::vector<double>& v) -> mvtv_status {
+        MVTV_TRY(alloc(dst, v.size()));
+        HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice));
+        return MVTV_OK;
+    };
+    MVTV_TRY(up(&sp.tw, tw));
+    MVTV_TRY(up(&sp.twq, twq));
+    MVTV_TRY(up(&sp.lam, lam));
+    return MVTV_OK;
+}
+
+// Direct solve (I + sigma D^T D) x = oty + ca*ga + cb*gb: forward DCT along dims 0..p-2, the
+// last dim's forward/divide/inverse in one pass, inverse DCT along dims p-2..0. All in place on x.
+mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, const double* ga, double ca,
+                           const double* gb, double cb, double* x) {
+    const int p = P->g.p;
+    for (int d = 0; d < p; ++d) {
+        const bool first = d == 0;
+        const int mode = d == p - 1 ? 2 : 0;
+        const int h = P->tstart(first ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
+        if (first && ga)   // b = oty + ca*ga + cb*gb formed on load
+            HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, oty, ga, ca, gb ? gb : ga, gb ? cb : 0.0, x,
+                                    sigma, 1.0));
+        else
+            HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, first ? oty : x, nullptr, 0.0, nullptr, 0.0, x,
+                                    sigma, 1.0));
+        P->tstop(h);
+    }
+    for (int d = p - 2; d >= 0; --d) {
+        const int h = P->tstart(MVTV_K_DCT);
+        HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 1, d, x, nullptr, 0.0, nullptr, 0.0, x, sigma, 1.0));
+        P->tstop(h);
+    }
     return MVTV_OK;
 }
 
@@ -447,7 +513,13 @@ mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) 
         return s;
     }
     P->host_st = reinterpret_cast<PcgState*>(P->host_red + 16);
-    s = mvtv_problem_set_data(P, d->oty, d->wdiag);
+    P->spec_mesh = true;
+    for (int j = 0; j < p; ++j) {
+        const uint32_t mj = g.m[j];
+        if ((mj & (mj - 1)) != 0 || mj > 4096) P->spec_mesh = false;
+    }
+    if (P->spec_mesh) s = spectral_plan(P);
+    if (s == MVTV_OK) s = mvtv_problem_set_data(P, d->oty, d->wdiag);
     if (s != MVTV_OK) {
         free_all(P);
         delete P;
@@ -468,6 +540,7 @@ void mvtv_problem_destroy(mvtv_problem* P) {
 int64_t mvtv_problem_nodes(const mvtv_problem* P) { return P ? int64_t(P->g.N) : 0; }
 int64_t mvtv_problem_edges(const mvtv_problem* P) { return P ? P->E : 0; }
 int32_t mvtv_problem_blocks(const mvtv_problem* P) { return P ? P->g.nb : 0; }
+int32_t mvtv_problem_spectral_ok(const mvtv_problem* P) { return P && spectral_ok(P) ? 1 : 0; }
 
 mvtv_status mvtv_problem_block_info(const mvtv_problem* P, int32_t k, int32_t* code, int32_t* sprime, double* weight) {
     if (!P || k < 0 || k >= P->g.nb) return fail(MVTV_BAD_ARG, "block index");
@@ -543,6 +616,12 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     const int pcg_maxit = o.pcg_max_iter > 0 ? o.pcg_max_iter : 20000;
     const Launch L = P->L();
     const double N = double(P->g.N), E = double(P->E);
+    if (o.theta_solver < MVTV_SOLVER_AUTO || o.theta_solver > MVTV_SOLVER_SPECTRAL)
+        return fail(MVTV_BAD_ARG, "theta_solver");
+    if (o.theta_solver == MVTV_SOLVER_SPECTRAL && !spectral_ok(P))
+        return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and power-of-two m_j <= 4096");
+    const bool spectral = o.theta_solver == MVTV_SOLVER_SPECTRAL ||
+                          (o.theta_solver == MVTV_SOLVER_AUTO && spectral_ok(P));
 
     // ---- initial state: u explicit in the edge buffer, alpha_0 = D theta_0 ------------------
     double rho;
@@ -607,10 +686,14 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         // ---- theta-update: (W + sigma D^T D) theta = oty + rho D^T (alpha + u) ----------------
         int pit = 0;
         double relres = 0.0;
-        MVTV_TRY(pcg_solve(P, sigma, P->oty, P->ga, rho, gprev, rho * c_prev, P->theta, rtol, pcg_maxit, &pit, &relres));
+        if (spectral)
+            MVTV_TRY(spectral_solve(P, sigma, P->oty, P->ga, rho, gprev, rho * c_prev, P->theta));
+        else
+            MVTV_TRY(pcg_solve(P, sigma, P->oty, P->ga, rho, gprev, rho * c_prev, P->theta, rtol, pcg_maxit, &pit,
+                               &relres));
         S.pcg_iters += pit;
         S.pcg_iters_max = std::max(S.pcg_iters_max, pit);
-        if (pit >= pcg_maxit && !(relres <= rtol)) {
+        if (!spectral && pit >= pcg_maxit && !(relres <= rtol)) {
             S.pcg_unconverged += 1;
             if (o.pcg_strict) {
                 status = MVTV_PCG_NOT_CONVERGED;
@@ -703,6 +786,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     P->c_state = c_prev;
     P->rho = rho;
     S.iters = it;
+    S.theta_solver = spectral ? MVTV_SOLVER_SPECTRAL : MVTV_SOLVER_PCG;
     S.rho = rho;
     S.status = status;
     S.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -831,6 +915,24 @@ mvtv_status mvtv_solve(mvtv_problem* P, double sigma, const double* b, double* x
     return s;
 }
 
+mvtv_status mvtv_solve_spectral(mvtv_problem* P, double sigma, const double* b, double* x_out) {
+    if (!P || !b || !x_out) return fail(MVTV_BAD_ARG, "null argument");
+    if (!spectral_ok(P)) return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and power-of-two m_j <= 4096");
+    DeviceGuard dg(P->device);
+    double* dx = nullptr;
+    MVTV_TRY(alloc(&dx, P->g.N));
+    const size_t bytes = size_t(P->g.N) * sizeof(double);
+    mvtv_status s = MVTV_OK;
+    if (hipMemcpyAsync(dx, b, bytes, hipMemcpyHostToDevice, P->stream) != hipSuccess)
+        s = fail(MVTV_HIP_ERROR, "solve upload");
+    if (s == MVTV_OK) s = spectral_solve(P, sigma, dx, nullptr, 0.0, nullptr, 0.0, dx);
+    if (s == MVTV_OK && (hipMemcpyAsync(x_out, dx, bytes, hipMemcpyDeviceToHost, P->stream) != hipSuccess ||
+                         hipStreamSynchronize(P->stream) != hipSuccess))
+        s = fail(MVTV_HIP_ERROR, "solve download");
+    (void)hipFree(dx);
+    return s;
+}
+
 // ------------------------------------------------------------------------------ instrumentation
 mvtv_status mvtv_timing_enable(mvtv_problem* P, int32_t on) {
     if (!P) return fail(MVTV_BAD_ARG, "null problem");
@@ -861,6 +963,8 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
         case MVTV_K_PCG_UPDATE: b = 8.0 * ((6.0 + w) * N); break;       // x, r, p, q (+W) in, x, r out
         case MVTV_K_PCG_DIRECTION: b = 8.0 * ((3.0 + w) * N); break;    // r, p (+W) in, p out
         case MVTV_K_PCG_FUSED: b = 8.0 * ((6.0 + w) * N); break;        // x, r, p (+W) in, x, r, p out
+        case MVTV_K_DCT_FIRST: b = 8.0 * 4.0 * N; break;                 // oty, g_alpha, g_u in, x out
+        case MVTV_K_DCT: b = 8.0 * 2.0 * N; break;                       // x in, x out
         default: b = 0.0;
     }
     if (total_ms) *total_ms = P->ms[kid];
@@ -871,7 +975,8 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
 
 const char* mvtv_kernel_name(int32_t kid) {
     static const char* names[MVTV_K_COUNT] = {"edge_update", "gather_Dt", "pcg_init", "pcg_apply_A",
-                                               "pcg_update", "pcg_direction", "reduce", "other", "pcg_fused3d"};
+                                               "pcg_update", "pcg_direction", "reduce", "other", "pcg_fused3d",
+                                               "dct_first", "dct"};
     return (kid >= 0 && kid < MVTV_K_COUNT) ? names[kid] : "?";
 }
 

@@ -164,6 +164,18 @@ hipError_t launch_edges_z_to_u(hipStream_t s, double* edges, uint64_t n, double 
 // edges = value on every real edge, 0 on padding (variant u0 fills: B 0, A and C 1/lambda)
 hipError_t launch_edges_fill_valid(const Geom& g, int order, const Launch& L, double* edges, double value);
 hipError_t launch_apply_D_padded(const Geom& g, int order, const Launch& L, const double* theta, double* edges);
+// Spectral theta-solve tables (mvtv_spectral.hip), device-resident, offsets in doubles.
+struct SpecPlan {
+    double* tw = nullptr;     // per dim: m_j/2 complex FFT twiddles e^{-2 pi i k/m_j}
+    double* twq = nullptr;    // per dim: m_j complex twiddles e^{-i pi k/(2 m_j)}
+    double* lam = nullptr;    // per dim: m_j eigenvalues 4 sin^2(pi k/(2 m_j)) of the Neumann Laplacian
+    uint32_t tw_off[kMaxDims] = {0, 0, 0, 0}, twq_off[kMaxDims] = {0, 0, 0, 0}, lam_off[kMaxDims] = {0, 0, 0, 0};
+};
+// mode 0 forward DCT-II, 1 inverse (DCT-III, unnormalised), 2 forward + divide by mu * N + inverse;
+// ga != nullptr forms the input as in + ca*ga + cb*gb. In place (in == out) is allowed.
+hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
+                           const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
+                           double w0);
 hipError_t launch_gather_index(hipStream_t s, const double* theta, const int64_t* idx, int64_t n, double* out);
 
 }  // namespace mvtv

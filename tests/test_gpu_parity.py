@@ -84,13 +84,17 @@ def _rcpp_problem(meta, g):
     return mv.Problem(meta["m"], g["Oty"], wdiag=wdiag, deltas=meta["deltas"], order=mv.ORDER_CPP)
 
 
+SOLVERS = [mv.SOLVER_PCG, mv.SOLVER_AUTO]   # AUTO = spectral where exact (W = I, power-of-two mesh)
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
 @pytest.mark.parametrize("name", RCPP)
-def test_rcpp_trajectory(name):
+def test_rcpp_trajectory(name, solver):
     meta, g = load_golden(name)
     P = _rcpp_problem(meta, g)
     for k in (1, 5, 20):
         th, u, rho, st = P.admm(meta["lam"], g["theta0"], u=np.zeros(P.E), rho=meta["rho0"],
-                                fixed_iters=k, pcg_rtol=1e-13)
+                                fixed_iters=k, pcg_rtol=1e-13, theta_solver=solver)
         assert _rel(th, g[f"snap{k}"]) <= RTOL_THETA, k
         assert st["iters"] == k
     assert rho == float(g["fixed_rho"])
@@ -103,11 +107,13 @@ def test_rcpp_trajectory(name):
     P.close()
 
 
+@pytest.mark.parametrize("solver", SOLVERS)
 @pytest.mark.parametrize("name", RCPP)
-def test_rcpp_converged(name):
+def test_rcpp_converged(name, solver):
     meta, g = load_golden(name)
     P = _rcpp_problem(meta, g)
-    th, u, rho, st = P.admm(meta["lam"], g["theta0"], u=np.zeros(P.E), rho=meta["rho0"], pcg_rtol=1e-13)
+    th, u, rho, st = P.admm(meta["lam"], g["theta0"], u=np.zeros(P.E), rho=meta["rho0"], pcg_rtol=1e-13,
+                            theta_solver=solver)
     assert st["iters"] == meta["iters"]
     assert rho == meta["rho"]
     assert _rel(th, g["theta"]) <= RTOL_THETA
@@ -115,13 +121,16 @@ def test_rcpp_converged(name):
     P.close()
 
 
-def test_rcpp_warm_path_resident():
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_rcpp_warm_path_resident(solver):
     meta, g = load_golden("rcpp_path_2d_16")
     y = g["y"]
     P = mv.Problem(meta["m"], y, deltas=meta["deltas"], order=mv.ORDER_CPP)
+    assert P.spectral_ok()
     P.state_set(np.full(256, y.mean()), np.zeros(P.E), meta["lams"][0] / 5.0)
     for k, lam in enumerate(meta["lams"]):
-        st = P.run(lam, pcg_rtol=1e-13)
+        st = P.run(lam, pcg_rtol=1e-13, theta_solver=solver)
+        assert st["theta_solver"] == (mv.SOLVER_PCG if solver == mv.SOLVER_PCG else mv.SOLVER_SPECTRAL)
         th, u, rho = P.state_get()
         assert st["iters"] == int(g[f"iters{k}"])
         assert rho == float(g[f"rho{k}"])
@@ -130,11 +139,13 @@ def test_rcpp_warm_path_resident():
     P.close()
 
 
+@pytest.mark.parametrize("solver", SOLVERS)
 @pytest.mark.parametrize("name", ["cpp_2d_16", "cpp_3d_8_unit", "cpp_2d_12_frac"])
-def test_cpp_variant(name):
+def test_cpp_variant(name, solver):
     meta, g = load_golden(name)
     P = mv.Problem(meta["m"], g["y"], deltas=meta["deltas"], order=mv.ORDER_CPP, weighted=not meta["unit"])
-    th, u, rho, st = P.admm(meta["lam"], g["theta0"], variant=mv.VARIANT_CPP, ymean=meta["ymean"], pcg_rtol=1e-13)
+    th, u, rho, st = P.admm(meta["lam"], g["theta0"], variant=mv.VARIANT_CPP, ymean=meta["ymean"], pcg_rtol=1e-13,
+                            theta_solver=solver)
     assert st["iters"] == meta["iters"]
     assert rho == meta["rho"]
     assert _rel(th, g["theta"]) <= RTOL_THETA

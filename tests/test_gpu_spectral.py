@@ -1,0 +1,121 @@
+"""GPU parity of the spectral theta-solve (mvtv_spectral.hip) through the C ABI.
+
+The spectral solve is a direct method (cosine transforms + diagonal divide), so it is
+compared with SciPy's SuperLU factorisation of the same matrix I + sigma D^T D — the
+solver the reference calls every ADMM iteration (rcpp-code/MultivarTV/src/solvers.cpp:113)
+— at a rounding-level tolerance: max|x - x_ref| <= 1e-12 max|x_ref| (fp64).
+At the BASELINE sizes (256^3, 1024^2, 128^4 would not fit SuperLU) the check is the
+size-independent residual ||A x - b|| / ||b|| <= 1e-12 with A applied by the stencil kernel.
+"""
+import numpy as np
+import pytest
+
+from oracle import mvtv_oracle as O
+
+mv = pytest.importorskip("multivartv_amd")
+pytestmark = pytest.mark.gpu
+
+RTOL_DIRECT = 1e-12
+
+
+def _cond(P, sigma):
+    """cond(I + sigma D^T D) = max mu / min mu; mu = 1 + sigma sum_S cS[S] prod_{j in S} lam_j <= 1 + sigma sum cS 4^|S|."""
+    cs = 0.0
+    for _, sp, w in P.block_info():
+        cs += w * w * 4.0 ** bin(sp).count("1")
+    return 1.0 + sigma * cs
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / max(1e-300, np.max(np.abs(b))))
+
+
+CASES = [([2], None, "cpp", False), ([8], None, "cpp", False), ([1024], None, "py", False),
+         ([4096], None, "cpp", False), ([16, 8], [0.3, 0.7], "cpp", False), ([2, 64], [0.5, 0.5], "cpp", False),
+         ([32, 32], None, "py", False), ([8, 8, 8], [0.5, 0.25, 0.125], "cpp", False),
+         ([16, 16, 16], [0.2, 0.3, 0.4], "cpp", True), ([8, 8, 8], [0.5, 0.25, 0.125], "py", False),
+         ([4, 4, 4, 4], [0.5, 0.25, 0.125, 0.3], "cpp", False), ([4, 4, 4, 4], None, "py", False),
+         ([8, 8, 8, 8], [0.1, 0.2, 0.3, 0.4], "cpp", False)]
+
+
+def _problem(m, deltas, order, unit, seed=0):
+    rng = np.random.default_rng(seed)
+    N = int(np.prod(m))
+    o = mv.ORDER_CPP if order == "cpp" else mv.ORDER_PY
+    weighted = (deltas is not None) and not unit
+    P = mv.Problem(m, rng.standard_normal(N), deltas=deltas if deltas is not None else [1.0] * len(m), order=o,
+                   weighted=weighted)
+    D = O.build_D(m, O.block_table(len(m), deltas if weighted else None, order, unit_weights=unit))
+    return P, D
+
+
+@pytest.mark.parametrize("m,deltas,order,unit", CASES)
+@pytest.mark.parametrize("sigma", [0.05, 3.2, 400.0])
+def test_spectral_vs_superlu(m, deltas, order, unit, sigma):
+    P, D = _problem(m, deltas, order, unit)
+    assert P.spectral_ok()
+    N = int(np.prod(m))
+    b = np.random.default_rng(3).standard_normal(N)
+    ref = O._solver(np.ones(N), (D.T @ D).tocsc(), sigma).solve(b)
+    x = P.solve_spectral(sigma, b)
+    # both solvers are backward stable: forward error ~ eps * cond(A)
+    assert _rel(x, ref) <= max(RTOL_DIRECT, 2e-16 * _cond(P, sigma))
+    P.close()
+
+
+@pytest.mark.parametrize("m", [[256, 256, 256], [1024, 1024], [64, 64, 64, 64]])
+def test_spectral_residual_baseline_sizes(m):
+    """Config-sized meshes (3D 256^3, 2D 1024^2; 4D at 64^4): residual through the stencil operator."""
+    p = len(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    N = int(np.prod(m))
+    b = np.random.default_rng(5).standard_normal(N)
+    with mv.Problem(m, b, deltas=deltas, order=mv.ORDER_CPP) as P:
+        for sigma in (0.2, 51.2):
+            x = P.solve_spectral(sigma, b)
+            r = P.apply_A(sigma, x) - b
+            assert np.linalg.norm(r) / np.linalg.norm(b) <= RTOL_DIRECT, (p, sigma)
+
+
+def test_spectral_matches_pcg_large():
+    """256^3 theta-solve: spectral vs PCG at rtol 1e-13 agree to the PCG tolerance."""
+    m = [128, 128, 128]
+    N = int(np.prod(m))
+    b = np.random.default_rng(6).standard_normal(N)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    with mv.Problem(m, b, deltas=deltas, order=mv.ORDER_CPP) as P:
+        xs = P.solve_spectral(7.0, b)
+        xp, it, rr = P.solve(7.0, b, rtol=1e-13)
+        assert rr <= 1e-13
+        assert _rel(xs, xp) <= 1e-11
+
+
+def test_spectral_rejected_when_not_exact():
+    rng = np.random.default_rng(0)
+    with mv.Problem([12, 8], rng.standard_normal(96), deltas=[1, 1]) as P:       # 12 is not a power of two
+        assert not P.spectral_ok()
+        with pytest.raises(mv.MvtvError):
+            P.solve_spectral(1.0, np.zeros(96))
+        with pytest.raises(mv.MvtvError):
+            P.admm(1.0, np.zeros(96), u=np.zeros(P.E), rho=0.2, theta_solver=mv.SOLVER_SPECTRAL)
+        _, _, _, st = P.admm(1.0, np.zeros(96), u=np.zeros(P.E), rho=0.2, fixed_iters=2)
+        assert st["theta_solver"] == mv.SOLVER_PCG
+    with mv.Problem([8, 8], rng.standard_normal(64), wdiag=rng.uniform(0, 2, 64).round(), deltas=[1, 1]) as P:
+        assert not P.spectral_ok()                                               # W != I
+        _, _, _, st = P.admm(1.0, np.zeros(64), u=np.zeros(P.E), rho=0.2, fixed_iters=2)
+        assert st["theta_solver"] == mv.SOLVER_PCG
+
+
+def test_spectral_admm_towers_3d():
+    """ADMM on the bench's towers problem at 32^3: spectral and PCG runs take the same decisions."""
+    from multivartv_amd.synth import towers
+    m = [32, 32, 32]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        th0 = np.full(y.size, y.mean())
+        ts, us, rs, ss = P.admm(1.0, th0, u=np.zeros(P.E), rho=0.2, theta_solver=mv.SOLVER_SPECTRAL)
+        tp, up, rp, sp = P.admm(1.0, th0, u=np.zeros(P.E), rho=0.2, theta_solver=mv.SOLVER_PCG, pcg_rtol=1e-13)
+    assert ss["theta_solver"] == mv.SOLVER_SPECTRAL and sp["theta_solver"] == mv.SOLVER_PCG
+    assert ss["iters"] == sp["iters"] and rs == rp
+    assert _rel(ts, tp) <= 1e-8
