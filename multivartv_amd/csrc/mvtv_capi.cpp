@@ -319,7 +319,7 @@ mvtv_status spectral_plan(mvtv_problem* P) {
         sp.tw_off[j] = uint32_t(tw.size());
         sp.twq_off[j] = uint32_t(twq.size());
         sp.lam_off[j] = uint32_t(lam.size());
-        for (uint32_t k = 0; k < m / 2; ++k) {
+        for (uint32_t k = 0; k < m; ++k) {
             const long double a = -2.0L * pi * k / m;
             tw.push_back(double(cosl(a)));
             tw.push_back(double(sinl(a)));

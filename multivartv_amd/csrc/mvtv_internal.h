@@ -166,7 +166,7 @@ hipError_t launch_edges_fill_valid(const Geom& g, int order, const Launch& L, do
 hipError_t launch_apply_D_padded(const Geom& g, int order, const Launch& L, const double* theta, double* edges);
 // Spectral theta-solve tables (mvtv_spectral.hip), device-resident, offsets in doubles.
 struct SpecPlan {
-    double* tw = nullptr;     // per dim: m_j/2 complex FFT twiddles e^{-2 pi i k/m_j}
+    double* tw = nullptr;     // per dim: m_j complex FFT twiddles e^{-2 pi i k/m_j}
     double* twq = nullptr;    // per dim: m_j complex twiddles e^{-i pi k/(2 m_j)}
     double* lam = nullptr;    // per dim: m_j eigenvalues 4 sin^2(pi k/(2 m_j)) of the Neumann Laplacian
     uint32_t tw_off[kMaxDims] = {0, 0, 0, 0}, twq_off[kMaxDims] = {0, 0, 0, 0}, lam_off[kMaxDims] = {0, 0, 0, 0};

@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "mvtv_device.h"
 
@@ -67,6 +68,18 @@ struct SpecArgs {
 };
 
 enum SpecMode { SPEC_FWD = 0, SPEC_INV = 1, SPEC_MID = 2 };
+
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 ldnt2(const double* p) {
+    const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2*>(p));
+    return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ void stnt2(double* p, double2 v) {
+    dvec2 w;
+    w.x = v.x;
+    w.y = v.y;
+    __builtin_nontemporal_store(w, reinterpret_cast<dvec2*>(p));
+}
 
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -314,7 +327,367 @@ __global__ __launch_bounds__(spec::NT) void k_dct(SpecArgs a) {
     }
 }
 
+// =============================================================================================
+// Register-radix Stockham version (m >= 8): every thread holds 8 complex values of one complex
+// line (two real lines) and runs radix-8 butterflies in registers (one radix-2/4 stage first
+// when log2 m is not a multiple of 3); LDS only carries the exchange between stages. The first
+// forward stage reads the Makhoul-permuted input straight from HBM and the last inverse stage
+// stores the un-permuted output straight to HBM.
+//
+// Thread -> (complex line c, butterfly column j), j < m/8. For d > 0 lanes run over c first,
+// so the two real lines of a complex line are one 16-B access and the 2*NCL lines of a tile
+// make one contiguous row per mesh position; for d = 0 lanes run over j (lines are contiguous).
+namespace spec8 {
+template <int L>
+struct Shape {
+    static constexpr int M = 1 << L;
+    static constexpr int TPL = M / 8;                                     // threads per complex line
+    static constexpr int TQ = (8192 / M) < 16 ? (8192 / M) : 16;          // real lines per workgroup
+    static constexpr int NCL = TQ / 2;                                    // complex lines per workgroup
+    static constexpr int NT = NCL * TPL;
+    static constexpr int LP = M + M / 8 + 4;                              // padded line pitch (complex slots)
+    static constexpr int R0 = (L % 3 == 0) ? 8 : (L % 3 == 1 ? 2 : 4);    // radix of the first stage
+};
+__device__ __forceinline__ int pidx(int pos) { return pos + (pos >> 3); }   // one pad slot per 8
+}  // namespace spec8
+
+template <bool INV>
+__device__ __forceinline__ void fft4r(double2& z0, double2& z1, double2& z2, double2& z3) {
+    const double2 t0 = cadd(z0, z2), t1 = csub(z0, z2), t2 = cadd(z1, z3), t3 = crot<INV>(csub(z1, z3));
+    z0 = cadd(t0, t2);
+    z2 = csub(t0, t2);
+    z1 = cadd(t1, t3);
+    z3 = csub(t1, t3);
+}
+
+// natural-order radix-R DFT of z[0..R-1] in registers
+template <int R, bool INV>
+__device__ __forceinline__ void dft_r(double2* z) {
+    if constexpr (R == 2) {
+        const double2 a = z[0], b = z[1];
+        z[0] = cadd(a, b);
+        z[1] = csub(a, b);
+    } else if constexpr (R == 4) {
+        fft4r<INV>(z[0], z[1], z[2], z[3]);
+    } else {
+        double2 e0 = z[0], e1 = z[2], e2 = z[4], e3 = z[6];
+        double2 o0 = z[1], o1 = z[3], o2 = z[5], o3 = z[7];
+        fft4r<INV>(e0, e1, e2, e3);
+        fft4r<INV>(o0, o1, o2, o3);
+        constexpr double h = 0.70710678118654752440;
+        // w8^k o_k, w8 = e^{-+ i pi/4}
+        const double2 p1 = INV ? make_double2(h * (o1.x - o1.y), h * (o1.x + o1.y))
+                               : make_double2(h * (o1.x + o1.y), h * (o1.y - o1.x));
+        const double2 p2 = crot<INV>(o2);
+        const double2 p3 = INV ? make_double2(-h * (o3.x + o3.y), h * (o3.x - o3.y))
+                               : make_double2(h * (o3.y - o3.x), -h * (o3.x + o3.y));
+        z[0] = cadd(e0, o0);
+        z[4] = csub(e0, o0);
+        z[1] = cadd(e1, p1);
+        z[5] = csub(e1, p1);
+        z[2] = cadd(e2, p2);
+        z[6] = csub(e2, p2);
+        z[3] = cadd(e3, p3);
+        z[7] = csub(e3, p3);
+    }
+}
+
+// One Stockham stage of radix R on this thread's 8/R butterflies b_s = j + s*TPL. Register
+// z[s*R + r] holds input position b_s + r*M/R. Twiddles, then the DFT; output position of
+// z[s*R + r] is (b_s / NS) * NS * R + b_s % NS + r * NS.
+template <int L, int R, int NS, bool INV>
+__device__ __forceinline__ void stage_compute(double2* z, int j, const double2* __restrict__ tw) {
+    using S = spec8::Shape<L>;
+#pragma unroll
+    for (int s = 0; s < 8 / R; ++s) {
+        if constexpr (NS > 1) {
+            const int kk = (j + s * S::TPL) % NS;
+            constexpr int step = S::M / (NS * R);
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                double2 w = tw[kk * r * step];
+                if (INV) w = cconj(w);
+                z[s * R + r] = cmul(z[s * R + r], w);
+            }
+        }
+        dft_r<R, INV>(z + s * R);
+    }
+}
+template <int L, int R>
+__device__ __forceinline__ int stage_in_pos(int j, int i) {
+    using S = spec8::Shape<L>;
+    const int s = i / R, r = i % R;
+    return j + S::TPL * (s + r * (8 / R));
+}
+template <int L, int R, int NS>
+__device__ __forceinline__ int stage_out_pos(int j, int i) {
+    using S = spec8::Shape<L>;
+    const int s = i / R, r = i % R;
+    const int b = j + s * S::TPL;
+    return (b / NS) * NS * R + (b % NS) + r * NS;
+}
+
+// Stages after the first (the first is peeled: its input comes from HBM or the caller's LDS).
+// STAGE counts radix-8 stages done after R0. Writes the outputs of stage NS_IN's butterflies
+// to LDS, then (if more stages remain) reads the next stage's inputs.
+template <int L, int R, int NS, bool INV, bool LAST_TO_REGS>
+__device__ __forceinline__ void stages_from(double2* z, int j, double2* X, const double2* __restrict__ tw) {
+    using S = spec8::Shape<L>;
+    stage_compute<L, R, NS, INV>(z, j, tw);
+    constexpr int NS_NEXT = NS * R;
+    if constexpr (NS_NEXT == S::M && LAST_TO_REGS) {
+        return;   // caller stores z (output positions stage_out_pos<L, R, NS>)
+    } else {
+        __syncthreads();   // everyone has read this stage's inputs
+#pragma unroll
+        for (int i = 0; i < 8; ++i) X[spec8::pidx(stage_out_pos<L, R, NS>(j, i))] = z[i];
+        __syncthreads();
+        if constexpr (NS_NEXT < S::M) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) z[i] = X[spec8::pidx(stage_in_pos<L, 8>(j, i))];
+            stages_from<L, 8, NS_NEXT, INV, LAST_TO_REGS>(z, j, X, tw);
+        }
+    }
+}
+// radix of the last stage and its NS (for the register-resident output positions)
+template <int L>
+struct LastStage {
+    static constexpr int R = (L == 1 || L == 2) ? (1 << L) : 8;   // L >= 3 always ends with radix 8
+    static constexpr int NS = (1 << L) / R;
+};
+
+template <int L, int MODE, bool D0, bool FORMB>
+__global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
+    using S = spec8::Shape<L>;
+    constexpr int M = S::M, TPL = S::TPL, NCL = S::NCL;
+    __shared__ double2 buf[NCL * S::LP];
+    __shared__ double lc0[2 * NCL], lc1[2 * NCL];
+    const int t = threadIdx.x;
+    const int j = D0 ? (t % TPL) : (t / NCL);
+    const int c = D0 ? (t / TPL) : (t % NCL);
+    const uint32_t q0 = blockIdx.x * uint32_t(a.tq);
+    const int la = 2 * c, lb = 2 * c + 1;
+    const bool va = la < a.tq && q0 + la < a.nlines;
+    const bool vb = lb < a.tq && q0 + lb < a.nlines;
+    double2* X = buf + c * S::LP;
+    const double2* __restrict__ tw = a.tw;
+
+    for (int l = t; MODE == SPEC_MID && l < a.tq; l += S::NT) {
+        const uint32_t q = q0 + l;
+        double lamv[kMaxDims] = {0, 0, 0, 0};
+        uint32_t rest = q < a.nlines ? q : 0u;
+        for (int jj = 0; jj < a.p - 1; ++jj) {
+            const uint32_t qq = (jj < a.p - 2) ? a.fd[jj].div(rest) : 0u;
+            lamv[jj] = a.lam[a.lam_off[jj] + (rest - qq * a.m[jj])];
+            rest = qq;
+        }
+        double c0 = a.w0, c1 = 0.0;
+        for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
+            if (a.cS[Sm] == 0.0) continue;
+            double prod = a.sigma * a.cS[Sm];
+            for (int jj = 0; jj < a.p; ++jj)
+                if (jj != a.d && ((Sm >> jj) & 1)) prod *= lamv[jj];
+            if ((Sm >> a.d) & 1) c1 += prod;
+            else c0 += prod;
+        }
+        lc0[l] = c0;
+        lc1[l] = c1;
+    }
+
+    // element k of real line ql (local) -> global offset
+    auto gaddr = [&](int ql, uint32_t k) -> uint32_t {
+        const uint32_t q = q0 + uint32_t(ql);
+        if (D0) return (q << L) + k;
+        return (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (k << a.ls);
+    };
+    auto ld2 = [&](uint32_t k) -> double2 {   // (line la, line lb) at position k, b formed if FORMB
+        double2 v = make_double2(0.0, 0.0);
+        if (D0) {
+            if (va) {
+                const uint32_t g = gaddr(la, k);
+                v.x = __builtin_nontemporal_load(a.in + g);
+                if (FORMB) v.x += a.ca * __builtin_nontemporal_load(a.ga + g) + a.cb * __builtin_nontemporal_load(a.gb + g);
+            }
+            if (vb) {
+                const uint32_t g = gaddr(lb, k);
+                v.y = __builtin_nontemporal_load(a.in + g);
+                if (FORMB) v.y += a.ca * __builtin_nontemporal_load(a.ga + g) + a.cb * __builtin_nontemporal_load(a.gb + g);
+            }
+        } else if (va) {   // d > 0: lines la, lb are adjacent words (vb == va)
+            const uint32_t g = gaddr(la, k);
+            v = ldnt2(a.in + g);
+            if (FORMB) {
+                const double2 x1 = ldnt2(a.ga + g);
+                const double2 x2 = ldnt2(a.gb + g);
+                v.x += a.ca * x1.x + a.cb * x2.x;
+                v.y += a.ca * x1.y + a.cb * x2.y;
+            }
+        }
+        return v;
+    };
+    auto st2 = [&](uint32_t k, double2 v) {
+        if (D0) {
+            if (va) __builtin_nontemporal_store(v.x, a.out + gaddr(la, k));
+            if (vb) __builtin_nontemporal_store(v.y, a.out + gaddr(lb, k));
+        } else if (va) {
+            stnt2(a.out + gaddr(la, k), v);
+        }
+    };
+
+    double2 z[8];
+    if (MODE != SPEC_INV) {
+        // ---- forward FFT of the Makhoul sequence z[n] = x[2n] | x[2(M-1-n)+1] -----------------
+        constexpr int R0 = S::R0;
+        if (D0) {
+            // contiguous lines: 16-B loads of (x[2n], x[2n+1]) land at Makhoul positions n, M-1-n
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int n = j + s4 * TPL;
+                double2 xa = make_double2(0.0, 0.0), xb = make_double2(0.0, 0.0);
+                if (va) {
+                    const uint32_t g = gaddr(la, uint32_t(2 * n));
+                    xa = ldnt2(a.in + g);
+                    if (FORMB) {
+                        const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
+                        xa.x += a.ca * g1.x + a.cb * g2.x;
+                        xa.y += a.ca * g1.y + a.cb * g2.y;
+                    }
+                }
+                if (vb) {
+                    const uint32_t g = gaddr(lb, uint32_t(2 * n));
+                    xb = ldnt2(a.in + g);
+                    if (FORMB) {
+                        const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
+                        xb.x += a.ca * g1.x + a.cb * g2.x;
+                        xb.y += a.ca * g1.y + a.cb * g2.y;
+                    }
+                }
+                X[spec8::pidx(n)] = make_double2(xa.x, xb.x);
+                X[spec8::pidx(M - 1 - n)] = make_double2(xa.y, xb.y);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) z[i] = X[spec8::pidx(stage_in_pos<L, R0>(j, i))];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int n = stage_in_pos<L, R0>(j, i);
+                const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
+                z[i] = ld2(k);
+            }
+        }
+        stages_from<L, R0, 1, false, false>(z, j, X, tw);   // natural-order spectrum in LDS
+    }
+
+    // ---- spectrum <-> DCT coefficients for the pairs (k, M-k); k = 0 also takes M/2 -------------
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int k = j + s * TPL;
+        const int ka = k, kb = k ? M - k : M / 2;
+        const bool self = k == 0;
+        double2 Xk, Xmk;
+        if (MODE != SPEC_INV) {
+            const double2 Z1 = X[spec8::pidx(ka)], Z2 = X[spec8::pidx(kb)];
+            const double2 q1 = a.twq[ka], q2 = a.twq[kb];
+            if (self) {
+                Xk = make_double2(q1.x * Z1.x, q1.x * Z1.y);
+                Xmk = make_double2(q2.x * Z2.x, q2.x * Z2.y);
+            } else {
+                const double2 Ap = make_double2(0.5 * (Z1.x + Z2.x), 0.5 * (Z1.y - Z2.y));
+                const double2 Bp = make_double2(0.5 * (Z1.y + Z2.y), -0.5 * (Z1.x - Z2.x));
+                Xk = make_double2(q1.x * Ap.x - q1.y * Ap.y, q1.x * Bp.x - q1.y * Bp.y);
+                Xmk = make_double2(q2.x * Ap.x + q2.y * Ap.y, q2.x * Bp.x + q2.y * Bp.y);
+            }
+        } else {
+            Xk = ld2(uint32_t(ka));
+            Xmk = ld2(uint32_t(kb));
+        }
+        if (MODE == SPEC_FWD) {
+            st2(uint32_t(ka), Xk);
+            st2(uint32_t(kb), Xmk);
+            continue;
+        }
+        if (MODE == SPEC_MID) {
+            const double* lamd = a.lam + a.lam_off[a.d];
+            const double l1 = lamd[ka], l2 = lamd[kb];
+            Xk.x *= a.inv_n / (lc0[la] + lc1[la] * l1);
+            Xk.y *= a.inv_n / (lc0[lb] + lc1[lb] * l1);
+            Xmk.x *= a.inv_n / (lc0[la] + lc1[la] * l2);
+            Xmk.y *= a.inv_n / (lc0[lb] + lc1[lb] * l2);
+        }
+        const double2 q1 = cconj(a.twq[ka]), q2 = cconj(a.twq[kb]);
+        if (self) {
+            const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xmk.x));
+            const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xmk.y));
+            X[spec8::pidx(0)] = Xk;
+            X[spec8::pidx(M / 2)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+        } else {
+            const double2 va1 = cmul(q1, make_double2(Xk.x, -Xmk.x));
+            const double2 vb1 = cmul(q1, make_double2(Xk.y, -Xmk.y));
+            const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xk.x));
+            const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xk.y));
+            X[spec8::pidx(ka)] = make_double2(va1.x - vb1.y, va1.y + vb1.x);
+            X[spec8::pidx(kb)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+        }
+    }
+    if (MODE == SPEC_FWD) return;
+    __syncthreads();
+
+    // ---- inverse FFT, natural in; the last stage's outputs go straight to HBM, un-permuted ------
+    {
+        constexpr int R0 = S::R0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] = X[spec8::pidx(stage_in_pos<L, R0>(j, i))];
+        if (D0) {
+            // contiguous lines: the output goes through LDS so (x[2n], x[2n+1]) leave as one 16-B store
+            stages_from<L, R0, 1, true, false>(z, j, X, tw);
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int n = j + s4 * TPL;
+                const double2 v0 = X[spec8::pidx(n)], v1 = X[spec8::pidx(M - 1 - n)];
+                if (va) stnt2(a.out + gaddr(la, uint32_t(2 * n)), make_double2(v0.x, v1.x));
+                if (vb) stnt2(a.out + gaddr(lb, uint32_t(2 * n)), make_double2(v0.y, v1.y));
+            }
+        } else {
+            stages_from<L, R0, 1, true, true>(z, j, X, tw);
+            using LS = LastStage<L>;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int n = stage_out_pos<L, LS::R, LS::NS>(j, i);
+                const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
+                st2(k, z[i]);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------ launcher
+template <int L>
+static void launch_dct8(const SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
+    using S = spec8::Shape<L>;
+    const dim3 grid((a.nlines + uint32_t(a.tq) - 1) / uint32_t(a.tq)), block(S::NT);
+#define MVTV_DCT8(MODE, D0, FB) klaunch(k_dct8<L, MODE, D0, FB>, grid, block, 0, s, a)
+    if (mode == SPEC_FWD) {
+        if (d0) {
+            if (formb) MVTV_DCT8(SPEC_FWD, true, true);
+            else MVTV_DCT8(SPEC_FWD, true, false);
+        } else {
+            MVTV_DCT8(SPEC_FWD, false, false);
+        }
+    } else if (mode == SPEC_INV) {
+        if (d0) MVTV_DCT8(SPEC_INV, true, false);
+        else MVTV_DCT8(SPEC_INV, false, false);
+    } else {
+        if (d0) {
+            if (formb) MVTV_DCT8(SPEC_MID, true, true);
+            else MVTV_DCT8(SPEC_MID, true, false);
+        } else {
+            MVTV_DCT8(SPEC_MID, false, false);
+        }
+    }
+#undef MVTV_DCT8
+}
+
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
                            double w0) {
@@ -346,11 +719,31 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     a.p = g.p;
     a.L = 0;
     while ((1u << a.L) < m) ++a.L;
+    if ((1u << a.L) != m || m > 4096) return hipErrorInvalidValue;
+    const bool formb = ga != nullptr;
+    if (a.L >= 3 && !std::getenv("MVTV_DCT_LDS")) {
+        static constexpr int tq8[13] = {0, 0, 0, 16, 16, 16, 16, 16, 16, 16, 8, 4, 2};
+        int tq = tq8[a.L];
+        if (d > 0) tq = std::min<int>(tq, int(g.stride[d]));
+        a.tq = tq;
+        switch (a.L) {
+            case 3: launch_dct8<3>(a, s, mode, d == 0, formb); break;
+            case 4: launch_dct8<4>(a, s, mode, d == 0, formb); break;
+            case 5: launch_dct8<5>(a, s, mode, d == 0, formb); break;
+            case 6: launch_dct8<6>(a, s, mode, d == 0, formb); break;
+            case 7: launch_dct8<7>(a, s, mode, d == 0, formb); break;
+            case 8: launch_dct8<8>(a, s, mode, d == 0, formb); break;
+            case 9: launch_dct8<9>(a, s, mode, d == 0, formb); break;
+            case 10: launch_dct8<10>(a, s, mode, d == 0, formb); break;
+            case 11: launch_dct8<11>(a, s, mode, d == 0, formb); break;
+            case 12: launch_dct8<12>(a, s, mode, d == 0, formb); break;
+        }
+        return hipGetLastError();
+    }
     int tq = std::max(2, std::min(16, int(spec::LDS_WORDS / m)));
     if (d > 0) tq = std::min<int>(tq, int(g.stride[d]));
-    if (tq < 2 || (1u << a.L) != m || m > 4096) return hipErrorInvalidValue;
+    if (tq < 2) return hipErrorInvalidValue;
     a.tq = tq;
-    const bool formb = ga != nullptr;
     const dim3 grid((a.nlines + uint32_t(tq) - 1) / uint32_t(tq)), block(spec::NT);
 #define MVTV_DCT_LAUNCH(MODE, D0, FB) klaunch(k_dct<MODE, D0, FB>, grid, block, 0, s, a)
     if (mode == SPEC_FWD) {
