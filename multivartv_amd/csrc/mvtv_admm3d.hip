@@ -1,0 +1,292 @@
+// mvtv_admm3d.hip — z-marching edge kernels for 3-D meshes (the BASELINE 512^3 path).
+//
+// Same arithmetic as k_edge_update / k_gather in mvtv_kernels.hip (the reference's
+// alpha = soft(D theta - u), u += alpha - D theta and D^T alpha, D^T u;
+// rcpp-code/MultivarTV/src/solvers.cpp:112-121), but each thread owns one (x, y) column of
+// the mesh and walks dim 2, so the dim-2 neighbours every difference needs come from
+// registers instead of a second trip to HBM:
+//   k_edge3d:   D theta at anchor (x,y,e) reads theta at (x+a, y+b, e+c); the c = 1 plane
+//               loaded at step e is the c = 0 plane of step e+1.
+//   k_gather3d: D^T v at (x,y,e) is a sum over the backward corners (x-a, y-b, e-c); the
+//               in-plane part Q_k(e) of every block whose difference set contains dim 2 is
+//               carried to step e+1, which subtracts it (the c = 1 corners).
+// The (x+1, y+1) / (x-1, y-1) in-plane neighbours are other lanes' and other waves' own
+// cells of the same step, so they are L1/L2 hits. A workgroup is a 64 x 4 column tile over a
+// chunk of dim-2 planes; tiles are dealt to XCDs in contiguous runs so a tile's neighbour rows
+// sit in the same L2.
+#include <algorithm>
+#include <cstdlib>
+
+#include "mvtv_device.h"
+
+namespace mvtv {
+
+namespace e3d {
+constexpr int TX = 64, TY = 4, NT = TX * TY;
+}
+
+struct Edge3dArgs {
+    Geom g;
+    const double* theta;
+    double* edges;
+    const double* theta_old;
+    double* g_alpha;
+    double* g_u;
+    const double* g_uprev;
+    double* partials;
+    double t_old, c_old, t_new;   // edge3d
+    double t, c_prev;             // gather3d
+    int tiles_x, tiles_y, zchunk, nblocks;
+};
+
+// tile of this workgroup (XCD-aware: XCD b%8 gets a contiguous run of tiles)
+struct Tile3 {
+    int x, y, z0, z1;
+    bool valid;
+};
+__device__ __forceinline__ Tile3 tile3(const Edge3dArgs& a) {
+    Tile3 t{};
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    t.valid = bid < a.nblocks;
+    if (!t.valid) return t;
+    const int nt = a.tiles_x * a.tiles_y;
+    const int tz = bid / nt, rem = bid - tz * nt;
+    const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
+    t.x = tx * e3d::TX + int(threadIdx.x & 63);
+    t.y = ty * e3d::TY + int(threadIdx.x >> 6);
+    t.z0 = tz * a.zchunk;
+    t.z1 = min(int(a.g.m[2]), t.z0 + a.zchunk);
+    return t;
+}
+
+// --------------------------------------------------------------------- edge update
+// z_new = D theta - u_old; alpha = soft(z_new, t_new); r = alpha - D theta.
+// Reductions: |r|^2, |D theta|^2, |alpha|^2 and (DTH) max |theta - theta_old|.
+template <int ORD, int UM, bool DTH>
+__global__ __launch_bounds__(e3d::NT) void k_edge3d(const Edge3dArgs a) {
+    constexpr int P = 3, NC = 8;
+    const Geom& g = a.g;
+    double red[ER_N] = {0.0, 0.0, 0.0, 0.0};
+    const Tile3 T = tile3(a);
+    if (T.valid && T.x < int(g.m[0]) && T.y < int(g.m[1])) {
+        const uint32_t m0 = g.m[0], pl = g.m[0] * g.m[1];
+        const uint32_t xo[2] = {uint32_t(T.x), uint32_t(min(T.x + 1, int(g.m[0]) - 1))};
+        const uint32_t yo[2] = {uint32_t(T.y) * m0, uint32_t(min(T.y + 1, int(g.m[1]) - 1)) * m0};
+        double th0[4], th1[4];
+        auto load_plane = [&](double (&th)[4], int e) {
+            const uint32_t zo = uint32_t(e) * pl;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) th[q] = a.theta[zo + yo[q >> 1] + xo[q & 1]];
+        };
+        load_plane(th0, T.z0);
+        for (int e = T.z0; e < T.z1; ++e) {
+            load_plane(th1, min(e + 1, int(g.m[2]) - 1));
+            const uint32_t i = uint32_t(e) * pl + yo[0] + xo[0];
+            double v[NC];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                v[q] = th0[q];       // corner T = q in dims 0, 1; dim 2 not set
+                v[q | 4] = th1[q];   // dim 2 set
+            }
+            if constexpr (DTH) red[ER_DTH] = fmax(red[ER_DTH], fabs(v[0] - a.theta_old[i]));
+            // forward-difference butterfly: v[S] = sum_{T subset S} (-1)^|T| theta(i + e_T)
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+#pragma unroll
+                for (int q = 0; q < NC; ++q)
+                    if (!((q >> j) & 1)) v[q | (1 << j)] = v[q] - v[q | (1 << j)];
+            static_for<0, 7>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                if (k < g.nb) {
+                    const double d = g.w[k] * v[S];
+                    double* ep = a.edges + uint64_t(k) * g.N + i;
+                    const double stored = __builtin_nontemporal_load(ep);
+                    const double uo = (UM == U_EXPLICIT) ? stored : -a.c_old * clampd(stored, a.t_old);
+                    const double z = d - uo;
+                    const double al = z - clampd(z, a.t_new);
+                    const double r = al - d;
+                    __builtin_nontemporal_store(z, ep);
+                    red[ER_R2] = fma(r, r, red[ER_R2]);
+                    red[ER_D2] = fma(d, d, red[ER_D2]);
+                    red[ER_A2] = fma(al, al, red[ER_A2]);
+                }
+            });
+#pragma unroll
+            for (int q = 0; q < 4; ++q) th0[q] = th1[q];
+        }
+    }
+    if (!T.valid)
+        for (int k = 0; k < ER_N; ++k) red[k] = 0.0;
+    block_reduce_store<ER_N, 1, e3d::NT>(red, a.partials);
+}
+
+// --------------------------------------------------------------------- D^T gather
+// g_alpha = D^T alpha, g_u = D^T u (u unscaled: -clamp(z, t)); explicit mode: g_u = D^T v.
+// Reductions: |g_u|^2, |g_u - c_prev g_uprev|^2 (B's dual residual), |g_alpha + c_prev g_uprev|^2 (A's).
+template <int ORD, int UM, bool PREV>
+__global__ __launch_bounds__(e3d::NT) void k_gather3d(const Edge3dArgs a) {
+    constexpr int P = 3;
+    const Geom& g = a.g;
+    double red[GR_N] = {0.0, 0.0, 0.0};
+    const Tile3 T = tile3(a);
+    if (T.valid && T.x < int(g.m[0]) && T.y < int(g.m[1])) {
+        const uint32_t m0 = g.m[0], pl = g.m[0] * g.m[1];
+        const bool okx = T.x > 0, oky = T.y > 0;
+        const uint32_t base_xy = uint32_t(T.y) * m0 + uint32_t(T.x);
+        // in-plane backward corner q (bit 0: x-1, bit 1: y-1) offset, and whether it exists
+        const uint32_t qoff[4] = {0u, okx ? 1u : 0u, oky ? m0 : 0u, (okx ? 1u : 0u) + (oky ? m0 : 0u)};
+        const bool qok[4] = {true, okx, oky, okx && oky};
+        double qa_prev[7], qu_prev[7];   // Q_k(e-1) of blocks whose S' contains dim 2
+#pragma unroll
+        for (int k = 0; k < 7; ++k) qa_prev[k] = qu_prev[k] = 0.0;
+
+        // in-plane sums Q_k(e) for alpha and u of block k at plane e
+        auto plane_q = [&](auto kc, int e, double& qa, double& qu) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+            constexpr int SI = S & 3;   // in-plane part of the difference set
+            const double* eb = a.edges + uint64_t(k) * g.N + uint32_t(e) * pl + base_xy;
+            qa = 0.0;
+            qu = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if ((q & ~SI) != 0) continue;   // corner q subset of S
+                const double vv = *(eb - qoff[q]);
+                const double v = qok[q] ? vv : 0.0;
+                const bool neg = __builtin_popcount(q) & 1;
+                if constexpr (UM == U_FROM_Z) {
+                    const double cl = clampd(v, a.t);
+                    const double al = v - cl;
+                    qa = neg ? qa - al : qa + al;
+                    qu = neg ? qu + cl : qu - cl;   // u = -clamp
+                } else {
+                    qu = neg ? qu - v : qu + v;
+                }
+            }
+        };
+        if (T.z0 > 0) {   // carried sums of plane z0 - 1
+            static_for<0, 7>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                if (k < g.nb && (S & 4)) plane_q(kc, T.z0 - 1, qa_prev[k], qu_prev[k]);
+            });
+        }
+        for (int e = T.z0; e < T.z1; ++e) {
+            double ga = 0.0, gu = 0.0;
+            static_for<0, 7>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                if (k < g.nb) {
+                    double qa, qu;
+                    plane_q(kc, e, qa, qu);
+                    double ca = qa, cu = qu;
+                    if constexpr ((S & 4) != 0) {
+                        ca -= qa_prev[k];   // zero at e = 0 (no plane -1)
+                        cu -= qu_prev[k];
+                        qa_prev[k] = qa;
+                        qu_prev[k] = qu;
+                    }
+                    ga = fma(g.w[k], ca, ga);
+                    gu = fma(g.w[k], cu, gu);
+                }
+            });
+            const uint32_t i = uint32_t(e) * pl + base_xy;
+            if constexpr (UM == U_FROM_Z) __builtin_nontemporal_store(ga, a.g_alpha + i);
+            __builtin_nontemporal_store(gu, a.g_u + i);
+            red[GR_GU2] = fma(gu, gu, red[GR_GU2]);
+            if constexpr (PREV) {
+                const double gp = a.c_prev * __builtin_nontemporal_load(a.g_uprev + i);
+                const double db = gu - gp, da = ga + gp;
+                red[GR_S2B] = fma(db, db, red[GR_S2B]);
+                red[GR_S2A] = fma(da, da, red[GR_S2A]);
+            }
+        }
+    }
+    if (!T.valid)
+        for (int k = 0; k < GR_N; ++k) red[k] = 0.0;
+    block_reduce_store<GR_N, 0, e3d::NT>(red, a.partials);
+}
+
+// ------------------------------------------------------------------------------------ launchers
+namespace {
+Edge3dArgs e3d_args(const Geom& g) {
+    Edge3dArgs a{};
+    a.g = g;
+    a.tiles_x = int((g.m[0] + e3d::TX - 1) / e3d::TX);
+    a.tiles_y = int((g.m[1] + e3d::TY - 1) / e3d::TY);
+    const int tiles = a.tiles_x * a.tiles_y;
+    // dim-2 chunks: enough workgroups to fill 256 CUs several times over, long enough marches
+    // that the carried plane (gather) and the extra theta plane (edge) are amortised
+    static const int want = [] {
+        const char* e = std::getenv("MVTV_E3D_WG");
+        return e ? std::atoi(e) : 4096;
+    }();
+    int nz = std::max(1, std::min(int(g.m[2]), want / std::max(1, tiles)));
+    while (nz > 1 && ((nz * tiles + 7) / 8 * 8) > kMaxCgBlocks) --nz;
+    a.zchunk = (int(g.m[2]) + nz - 1) / nz;
+    nz = (int(g.m[2]) + a.zchunk - 1) / a.zchunk;
+    a.nblocks = tiles * nz;
+    return a;
+}
+}  // namespace
+
+bool edge3d_ok(const Geom& g) {
+    if (g.p != 3 || std::getenv("MVTV_E3D_OFF")) return false;
+    const Edge3dArgs a = e3d_args(g);
+    return (a.nblocks + 7) / 8 * 8 <= kMaxCgBlocks;
+}
+
+hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
+                         double t_old, double c_old, double t_new, const double* theta_old, double* partials,
+                         int* nparts) {
+    Edge3dArgs a = e3d_args(g);
+    a.theta = theta;
+    a.edges = edges;
+    a.theta_old = theta_old;
+    a.partials = partials;
+    a.t_old = t_old;
+    a.c_old = c_old;
+    a.t_new = t_new;
+    const int grid = (a.nblocks + 7) / 8 * 8;
+    *nparts = grid;
+    auto go = [&](auto kern) {
+        klaunch(kern, dim3(grid), dim3(e3d::NT), 0, s, a);
+        return hipGetLastError();
+    };
+    const bool dth = theta_old != nullptr;
+    if (order == 0) {
+        if (umode == U_EXPLICIT) return dth ? go(k_edge3d<0, U_EXPLICIT, true>) : go(k_edge3d<0, U_EXPLICIT, false>);
+        return dth ? go(k_edge3d<0, U_FROM_Z, true>) : go(k_edge3d<0, U_FROM_Z, false>);
+    }
+    if (umode == U_EXPLICIT) return dth ? go(k_edge3d<1, U_EXPLICIT, true>) : go(k_edge3d<1, U_EXPLICIT, false>);
+    return dth ? go(k_edge3d<1, U_FROM_Z, true>) : go(k_edge3d<1, U_FROM_Z, false>);
+}
+
+hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
+                           double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
+                           int* nparts) {
+    Edge3dArgs a = e3d_args(g);
+    a.edges = const_cast<double*>(edges);   // read only in k_gather3d
+    a.g_alpha = g_alpha;
+    a.g_u = g_u;
+    a.g_uprev = g_uprev;
+    a.partials = partials;
+    a.t = t;
+    a.c_prev = c_prev;
+    const int grid = (a.nblocks + 7) / 8 * 8;
+    *nparts = grid;
+    auto go = [&](auto kern) {
+        klaunch(kern, dim3(grid), dim3(e3d::NT), 0, s, a);
+        return hipGetLastError();
+    };
+    const bool prev = g_uprev != nullptr;
+    if (order == 0) {
+        if (umode == U_EXPLICIT) return prev ? go(k_gather3d<0, U_EXPLICIT, true>) : go(k_gather3d<0, U_EXPLICIT, false>);
+        return prev ? go(k_gather3d<0, U_FROM_Z, true>) : go(k_gather3d<0, U_FROM_Z, false>);
+    }
+    if (umode == U_EXPLICIT) return prev ? go(k_gather3d<1, U_EXPLICIT, true>) : go(k_gather3d<1, U_EXPLICIT, false>);
+    return prev ? go(k_gather3d<1, U_FROM_Z, true>) : go(k_gather3d<1, U_FROM_Z, false>);
+}
+
+}  // namespace mvtv

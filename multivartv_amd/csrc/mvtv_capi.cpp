@@ -79,6 +79,7 @@ struct mvtv_problem {
     PcgState* host_st = nullptr;
     SpecPlan spec;                // spectral theta-solve tables (allocated when the mesh allows it)
     bool spec_mesh = false;       // every m_j a power of two <= 4096
+    bool e3d = false;             // z-marching 3-D edge kernels
 
     // resident ADMM state
     bool have_state = false;
@@ -519,6 +520,7 @@ mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) 
         if ((mj & (mj - 1)) != 0 || mj > 4096) P->spec_mesh = false;
     }
     if (P->spec_mesh) s = spectral_plan(P);
+    P->e3d = edge3d_ok(g);
     if (s == MVTV_OK) s = mvtv_problem_set_data(P, d->oty, d->wdiag);
     if (s != MVTV_OK) {
         free_all(P);
@@ -643,7 +645,12 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     double* gnew = P->gu;
     // g_uprev = D^T u0, g_alpha = D^T D theta0  ->  b_1 = oty + rho D^T (alpha0 + u0)
     int h = P->tstart(MVTV_K_GATHER);
-    HIP_TRY(launch_gather(P->g, P->order, U_EXPLICIT, L, P->edges, 0.0, nullptr, gprev, nullptr, 1.0, P->partials));
+    int np = L.grid;
+    if (P->e3d)
+        HIP_TRY(launch_gather3d(P->g, P->order, U_EXPLICIT, P->stream, P->edges, 0.0, nullptr, gprev, nullptr, 1.0,
+                                P->partials, &np));
+    else
+        HIP_TRY(launch_gather(P->g, P->order, U_EXPLICIT, L, P->edges, 0.0, nullptr, gprev, nullptr, 1.0, P->partials));
     P->tstop(h);
     h = P->tstart(MVTV_K_OTHER);
     HIP_TRY(launch_apply_A(P->g, L, 1.0, W_NONE, nullptr, P->theta, P->ga, nullptr, nullptr));
@@ -704,20 +711,30 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         // ---- z-update (soft threshold) and dual update over all edges -----------------------
         const double t_new = rho != 0.0 ? lambda / rho : INFINITY;
         h = P->tstart(MVTV_K_EDGE_UPDATE);
-        HIP_TRY(launch_edge_update(P->g, P->order, mode, L, P->theta, P->edges, t_z, c_prev, t_new,
-                                   track_theta ? P->thold : nullptr, P->partials));
+        np = L.grid;
+        if (P->e3d)
+            HIP_TRY(launch_edge3d(P->g, P->order, mode, P->stream, P->theta, P->edges, t_z, c_prev, t_new,
+                                  track_theta ? P->thold : nullptr, P->partials, &np));
+        else
+            HIP_TRY(launch_edge_update(P->g, P->order, mode, L, P->theta, P->edges, t_z, c_prev, t_new,
+                                       track_theta ? P->thold : nullptr, P->partials));
         P->tstop(h);
         h = P->tstart(MVTV_K_REDUCE);
-        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, ER_N, 1, 0, P->red, P->st));
+        HIP_TRY(launch_finalize(P->stream, P->partials, np, ER_N, 1, 0, P->red, P->st));
         P->tstop(h);
         mode = U_FROM_Z;
         t_z = t_new;
         // ---- D^T alpha, D^T u and the dual residual norms ---------------------------------------
         h = P->tstart(MVTV_K_GATHER);
-        HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, L, P->edges, t_z, P->ga, gnew, gprev, c_prev, P->partials));
+        np = L.grid;
+        if (P->e3d)
+            HIP_TRY(launch_gather3d(P->g, P->order, U_FROM_Z, P->stream, P->edges, t_z, P->ga, gnew, gprev, c_prev,
+                                    P->partials, &np));
+        else
+            HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, L, P->edges, t_z, P->ga, gnew, gprev, c_prev, P->partials));
         P->tstop(h);
         h = P->tstart(MVTV_K_REDUCE);
-        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, GR_N, 0, 0, P->red + ER_N, P->st));
+        HIP_TRY(launch_finalize(P->stream, P->partials, np, GR_N, 0, 0, P->red + ER_N, P->st));
         P->tstop(h);
         HIP_TRY(hipMemcpyAsync(P->host_red, P->red, (ER_N + GR_N) * sizeof(double), hipMemcpyDeviceToHost, P->stream));
         MVTV_TRY(P->sync());

@@ -176,6 +176,15 @@ struct SpecPlan {
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
                            double w0);
+// z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /
+// launch_gather, *nparts workgroup rows
+bool edge3d_ok(const Geom& g);
+hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
+                         double t_old, double c_old, double t_new, const double* theta_old, double* partials,
+                         int* nparts);
+hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
+                           double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
+                           int* nparts);
 hipError_t launch_gather_index(hipStream_t s, const double* theta, const int64_t* idx, int64_t n, double* out);
 
 }  // namespace mvtv
