@@ -737,7 +737,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         HIP_TRY(launch_finalize(P->stream, P->partials, np, GR_N, 0, 0, P->red + ER_N, P->st));
         P->tstop(h);
         HIP_TRY(hipMemcpyAsync(P->host_red, P->red, (ER_N + GR_N) * sizeof(double), hipMemcpyDeviceToHost, P->stream));
-        MVTV_TRY(P->sync());
+        HIP_TRY(hipStreamSynchronize(P->stream));   // timing events are harvested after the loop
         const double* R = P->host_red;
         const double r_norm = std::sqrt(R[ER_R2]);
         it += 1;
@@ -795,6 +795,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
             break;
         }
     }
+    P->harvest();   // the stream is idle here (last iteration synchronised)
     if (o.verbose) std::printf("Lambda= %g, Counter = %d\n", lambda, counter);
     // keep the resident state consistent: g_uprev buffer is P->guprev
     if (gprev != P->guprev) std::swap(P->guprev, P->gu);

@@ -345,10 +345,14 @@ struct Shape {
     static constexpr int TQ = (8192 / M) < 16 ? (8192 / M) : 16;          // real lines per workgroup
     static constexpr int NCL = TQ / 2;                                    // complex lines per workgroup
     static constexpr int NT = NCL * TPL;
-    static constexpr int LP = M + M / 8 + 4;                              // padded line pitch (complex slots)
+    // line pitch (complex slots): a multiple of 8 plus 8 mod 16, and slot = pidx(pos) ^ (c & 7), so
+    // c-fastest lanes (d > 0) hit distinct banks for the 16-B reads (16-lane groups) and writes
+    // (8-lane groups); j-fastest lanes (d = 0) are spread by pidx
+    static constexpr int LP = (M + M / 8 + 15) / 16 * 16 + 8;
     static constexpr int R0 = (L % 3 == 0) ? 8 : (L % 3 == 1 ? 2 : 4);    // radix of the first stage
 };
 __device__ __forceinline__ int pidx(int pos) { return pos + (pos >> 3); }   // one pad slot per 8
+__device__ __forceinline__ int slot(int pos, int cx) { return pidx(pos) ^ cx; }
 }  // namespace spec8
 
 template <bool INV>
@@ -431,7 +435,7 @@ __device__ __forceinline__ int stage_out_pos(int j, int i) {
 // STAGE counts radix-8 stages done after R0. Writes the outputs of stage NS_IN's butterflies
 // to LDS, then (if more stages remain) reads the next stage's inputs.
 template <int L, int R, int NS, bool INV, bool LAST_TO_REGS>
-__device__ __forceinline__ void stages_from(double2* z, int j, double2* X, const double2* __restrict__ tw) {
+__device__ __forceinline__ void stages_from(double2* z, int j, double2* X, int cx, const double2* __restrict__ tw) {
     using S = spec8::Shape<L>;
     stage_compute<L, R, NS, INV>(z, j, tw);
     constexpr int NS_NEXT = NS * R;
@@ -440,12 +444,12 @@ __device__ __forceinline__ void stages_from(double2* z, int j, double2* X, const
     } else {
         __syncthreads();   // everyone has read this stage's inputs
 #pragma unroll
-        for (int i = 0; i < 8; ++i) X[spec8::pidx(stage_out_pos<L, R, NS>(j, i))] = z[i];
+        for (int i = 0; i < 8; ++i) X[spec8::slot(stage_out_pos<L, R, NS>(j, i), cx)] = z[i];
         __syncthreads();
         if constexpr (NS_NEXT < S::M) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) z[i] = X[spec8::pidx(stage_in_pos<L, 8>(j, i))];
-            stages_from<L, 8, NS_NEXT, INV, LAST_TO_REGS>(z, j, X, tw);
+            for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, 8>(j, i), cx)];
+            stages_from<L, 8, NS_NEXT, INV, LAST_TO_REGS>(z, j, X, cx, tw);
         }
     }
 }
@@ -470,6 +474,7 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
     const bool va = la < a.tq && q0 + la < a.nlines;
     const bool vb = lb < a.tq && q0 + lb < a.nlines;
     double2* X = buf + c * S::LP;
+    const int cx = c & 7;
     const double2* __restrict__ tw = a.tw;
 
     for (int l = t; MODE == SPEC_MID && l < a.tq; l += S::NT) {
@@ -562,12 +567,12 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
                         xb.y += a.ca * g1.y + a.cb * g2.y;
                     }
                 }
-                X[spec8::pidx(n)] = make_double2(xa.x, xb.x);
-                X[spec8::pidx(M - 1 - n)] = make_double2(xa.y, xb.y);
+                X[spec8::slot(n, cx)] = make_double2(xa.x, xb.x);
+                X[spec8::slot(M - 1 - n, cx)] = make_double2(xa.y, xb.y);
             }
             __syncthreads();
 #pragma unroll
-            for (int i = 0; i < 8; ++i) z[i] = X[spec8::pidx(stage_in_pos<L, R0>(j, i))];
+            for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, R0>(j, i), cx)];
         } else {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -576,7 +581,7 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
                 z[i] = ld2(k);
             }
         }
-        stages_from<L, R0, 1, false, false>(z, j, X, tw);   // natural-order spectrum in LDS
+        stages_from<L, R0, 1, false, false>(z, j, X, cx, tw);   // natural-order spectrum in LDS
     }
 
     // ---- spectrum <-> DCT coefficients for the pairs (k, M-k); k = 0 also takes M/2 -------------
@@ -587,7 +592,7 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
         const bool self = k == 0;
         double2 Xk, Xmk;
         if (MODE != SPEC_INV) {
-            const double2 Z1 = X[spec8::pidx(ka)], Z2 = X[spec8::pidx(kb)];
+            const double2 Z1 = X[spec8::slot(ka, cx)], Z2 = X[spec8::slot(kb, cx)];
             const double2 q1 = a.twq[ka], q2 = a.twq[kb];
             if (self) {
                 Xk = make_double2(q1.x * Z1.x, q1.x * Z1.y);
@@ -619,15 +624,15 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
         if (self) {
             const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xmk.x));
             const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xmk.y));
-            X[spec8::pidx(0)] = Xk;
-            X[spec8::pidx(M / 2)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+            X[spec8::slot(0, cx)] = Xk;
+            X[spec8::slot(M / 2, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
         } else {
             const double2 va1 = cmul(q1, make_double2(Xk.x, -Xmk.x));
             const double2 vb1 = cmul(q1, make_double2(Xk.y, -Xmk.y));
             const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xk.x));
             const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xk.y));
-            X[spec8::pidx(ka)] = make_double2(va1.x - vb1.y, va1.y + vb1.x);
-            X[spec8::pidx(kb)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+            X[spec8::slot(ka, cx)] = make_double2(va1.x - vb1.y, va1.y + vb1.x);
+            X[spec8::slot(kb, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
         }
     }
     if (MODE == SPEC_FWD) return;
@@ -637,19 +642,19 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
     {
         constexpr int R0 = S::R0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) z[i] = X[spec8::pidx(stage_in_pos<L, R0>(j, i))];
+        for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, R0>(j, i), cx)];
         if (D0) {
             // contiguous lines: the output goes through LDS so (x[2n], x[2n+1]) leave as one 16-B store
-            stages_from<L, R0, 1, true, false>(z, j, X, tw);
+            stages_from<L, R0, 1, true, false>(z, j, X, cx, tw);
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
                 const int n = j + s4 * TPL;
-                const double2 v0 = X[spec8::pidx(n)], v1 = X[spec8::pidx(M - 1 - n)];
+                const double2 v0 = X[spec8::slot(n, cx)], v1 = X[spec8::slot(M - 1 - n, cx)];
                 if (va) stnt2(a.out + gaddr(la, uint32_t(2 * n)), make_double2(v0.x, v1.x));
                 if (vb) stnt2(a.out + gaddr(lb, uint32_t(2 * n)), make_double2(v0.y, v1.y));
             }
         } else {
-            stages_from<L, R0, 1, true, true>(z, j, X, tw);
+            stages_from<L, R0, 1, true, true>(z, j, X, cx, tw);
             using LS = LastStage<L>;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
