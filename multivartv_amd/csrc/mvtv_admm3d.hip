@@ -36,6 +36,7 @@ struct Edge3dArgs {
     double* partials;
     double t_old, c_old, t_new;   // edge3d
     double t, c_prev;             // gather3d
+    const AdmmCtl* ctl;           // device scalars (asynchronous loop) or nullptr
     int tiles_x, tiles_y, zchunk, nblocks;
 };
 
@@ -66,6 +67,13 @@ template <int ORD, int UM, bool DTH>
 __global__ __launch_bounds__(e3d::NT) void k_edge3d(const Edge3dArgs a) {
     constexpr int P = 3, NC = 8;
     const Geom& g = a.g;
+    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        t_old = a.ctl->t_z;
+        c_old = a.ctl->c_prev;
+        t_new = a.ctl->t_next;
+    }
     double red[ER_N] = {0.0, 0.0, 0.0, 0.0};
     const Tile3 T = tile3(a);
     if (T.valid && T.x < int(g.m[0]) && T.y < int(g.m[1])) {
@@ -102,9 +110,9 @@ __global__ __launch_bounds__(e3d::NT) void k_edge3d(const Edge3dArgs a) {
                     const double d = g.w[k] * v[S];
                     double* ep = a.edges + uint64_t(k) * g.N + i;
                     const double stored = __builtin_nontemporal_load(ep);
-                    const double uo = (UM == U_EXPLICIT) ? stored : -a.c_old * clampd(stored, a.t_old);
+                    const double uo = (UM == U_EXPLICIT) ? stored : -c_old * clampd(stored, t_old);
                     const double z = d - uo;
-                    const double al = z - clampd(z, a.t_new);
+                    const double al = z - clampd(z, t_new);
                     const double r = al - d;
                     __builtin_nontemporal_store(z, ep);
                     red[ER_R2] = fma(r, r, red[ER_R2]);
@@ -128,6 +136,12 @@ template <int ORD, int UM, bool PREV>
 __global__ __launch_bounds__(e3d::NT) void k_gather3d(const Edge3dArgs a) {
     constexpr int P = 3;
     const Geom& g = a.g;
+    double tt = a.t, c_prev = a.c_prev;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        tt = a.ctl->t_next;
+        c_prev = a.ctl->c_prev;
+    }
     double red[GR_N] = {0.0, 0.0, 0.0};
     const Tile3 T = tile3(a);
     if (T.valid && T.x < int(g.m[0]) && T.y < int(g.m[1])) {
@@ -156,7 +170,7 @@ __global__ __launch_bounds__(e3d::NT) void k_gather3d(const Edge3dArgs a) {
                 const double v = qok[q] ? vv : 0.0;
                 const bool neg = __builtin_popcount(q) & 1;
                 if constexpr (UM == U_FROM_Z) {
-                    const double cl = clampd(v, a.t);
+                    const double cl = clampd(v, tt);
                     const double al = v - cl;
                     qa = neg ? qa - al : qa + al;
                     qu = neg ? qu + cl : qu - cl;   // u = -clamp
@@ -196,7 +210,7 @@ __global__ __launch_bounds__(e3d::NT) void k_gather3d(const Edge3dArgs a) {
             __builtin_nontemporal_store(gu, a.g_u + i);
             red[GR_GU2] = fma(gu, gu, red[GR_GU2]);
             if constexpr (PREV) {
-                const double gp = a.c_prev * __builtin_nontemporal_load(a.g_uprev + i);
+                const double gp = c_prev * __builtin_nontemporal_load(a.g_uprev + i);
                 const double db = gu - gp, da = ga + gp;
                 red[GR_S2B] = fma(db, db, red[GR_S2B]);
                 red[GR_S2A] = fma(da, da, red[GR_S2A]);
@@ -239,8 +253,9 @@ bool edge3d_ok(const Geom& g) {
 
 hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
                          double t_old, double c_old, double t_new, const double* theta_old, double* partials,
-                         int* nparts) {
+                         int* nparts, const AdmmCtl* ctl) {
     Edge3dArgs a = e3d_args(g);
+    a.ctl = ctl;
     a.theta = theta;
     a.edges = edges;
     a.theta_old = theta_old;
@@ -265,8 +280,9 @@ hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, con
 
 hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                            double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
-                           int* nparts) {
+                           int* nparts, const AdmmCtl* ctl) {
     Edge3dArgs a = e3d_args(g);
+    a.ctl = ctl;
     a.edges = const_cast<double*>(edges);   // read only in k_gather3d
     a.g_alpha = g_alpha;
     a.g_u = g_u;

@@ -80,6 +80,9 @@ struct mvtv_problem {
     SpecPlan spec;                // spectral theta-solve tables (allocated when the mesh allows it)
     bool spec_mesh = false;       // every m_j a power of two <= 4096
     bool e3d = false;             // z-marching 3-D edge kernels
+    AdmmCtl* ctl = nullptr;       // device control block of the asynchronous ADMM loop
+    AdmmCtl* host_ctl = nullptr;  // pinned mirror
+    int admm_hint = 0;            // ADMM iterations of the last converged run (enqueue-ahead depth)
 
     // resident ADMM state
     bool have_state = false;
@@ -169,6 +172,8 @@ void free_all(mvtv_problem* P) {
             *b = nullptr;
         }
     if (P->st) (void)hipFree(P->st);
+    if (P->ctl) (void)hipFree(P->ctl);
+    if (P->host_ctl) (void)hipHostFree(P->host_ctl);
     for (double* t : {P->spec.tw, P->spec.twq, P->spec.lam})
         if (t) (void)hipFree(t);
     P->spec = SpecPlan{};
@@ -347,7 +352,7 @@ mvtv_status spectral_plan(mvtv_problem* P) {
 // Direct solve (I + sigma D^T D) x = oty + ca*ga + cb*gb: forward DCT along dims 0..p-2, the
 // last dim's forward/divide/inverse in one pass, inverse DCT along dims p-2..0. All in place on x.
 mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, const double* ga, double ca,
-                           const double* gb, double cb, double* x) {
+                           const double* gb, double cb, double* x, const AdmmCtl* ctl = nullptr) {
     const int p = P->g.p;
     for (int d = 0; d < p; ++d) {
         const bool first = d == 0;
@@ -355,15 +360,15 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
         const int h = P->tstart(first ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
         if (first && ga)   // b = oty + ca*ga + cb*gb formed on load
             HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, oty, ga, ca, gb ? gb : ga, gb ? cb : 0.0, x,
-                                    sigma, 1.0));
+                                    sigma, 1.0, ctl));
         else
             HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, first ? oty : x, nullptr, 0.0, nullptr, 0.0, x,
-                                    sigma, 1.0));
+                                    sigma, 1.0, ctl));
         P->tstop(h);
     }
     for (int d = p - 2; d >= 0; --d) {
         const int h = P->tstart(MVTV_K_DCT);
-        HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 1, d, x, nullptr, 0.0, nullptr, 0.0, x, sigma, 1.0));
+        HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 1, d, x, nullptr, 0.0, nullptr, 0.0, x, sigma, 1.0, ctl));
         P->tstop(h);
     }
     return MVTV_OK;
@@ -508,6 +513,9 @@ mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) 
         s = fail(MVTV_OUT_OF_MEMORY, "hipMalloc(PcgState)");
     if (s == MVTV_OK && hipHostMalloc(reinterpret_cast<void**>(&P->host_red), 16 * sizeof(double) + sizeof(PcgState)) != hipSuccess)
         s = fail(MVTV_OUT_OF_MEMORY, "hipHostMalloc");
+    if (s == MVTV_OK && (hipMalloc(reinterpret_cast<void**>(&P->ctl), sizeof(AdmmCtl)) != hipSuccess ||
+                         hipHostMalloc(reinterpret_cast<void**>(&P->host_ctl), sizeof(AdmmCtl)) != hipSuccess))
+        s = fail(MVTV_OUT_OF_MEMORY, "control block");
     if (s != MVTV_OK) {
         free_all(P);
         delete P;
@@ -631,32 +639,39 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     else if (variant == MVTV_VARIANT_CPP) rho = double(int(lambda));     // int rho = lambda (:108)
     else rho = lambda;                                                   // rho = tune (py :55)
     double sigma = std::isnan(o.sigma) ? (variant == MVTV_VARIANT_RCPP ? rho : lambda) : o.sigma;
-    if (P->edge_mode == U_FROM_Z) {
-        HIP_TRY(launch_edges_z_to_u(P->stream, P->edges, uint64_t(P->g.nb) * P->g.N, P->t_z, P->c_state));
-        P->edge_mode = U_EXPLICIT;
-        P->c_state = 1.0;
-    }
-    if (P->u_default) {
-        const double u0 = variant == MVTV_VARIANT_RCPP ? 0.0 : 1.0 / lambda;   // A :101, C :62
-        HIP_TRY(launch_edges_fill_valid(P->g, P->order, L, P->edges, u0));
-        P->u_default = false;
-    }
     double* gprev = P->guprev;
     double* gnew = P->gu;
-    // g_uprev = D^T u0, g_alpha = D^T D theta0  ->  b_1 = oty + rho D^T (alpha0 + u0)
-    int h = P->tstart(MVTV_K_GATHER);
-    int np = L.grid;
-    if (P->e3d)
-        HIP_TRY(launch_gather3d(P->g, P->order, U_EXPLICIT, P->stream, P->edges, 0.0, nullptr, gprev, nullptr, 1.0,
-                                P->partials, &np));
-    else
-        HIP_TRY(launch_gather(P->g, P->order, U_EXPLICIT, L, P->edges, 0.0, nullptr, gprev, nullptr, 1.0, P->partials));
-    P->tstop(h);
+    double c_prev = 1.0, t_z = 0.0;
+    int mode = U_EXPLICIT;
+    int h = -1;
+    if (P->edge_mode == U_FROM_Z) {
+        // resume from the resident state of the previous call: u0 = -c clamp(z, t_z) is read straight
+        // from z by the first edge update, and P->guprev already holds D^T clamp-part of it (scale c)
+        mode = U_FROM_Z;
+        t_z = P->t_z;
+        c_prev = P->c_state;
+    } else {
+        if (P->u_default) {
+            const double u0 = variant == MVTV_VARIANT_RCPP ? 0.0 : 1.0 / lambda;   // A :101, C :62
+            HIP_TRY(launch_edges_fill_valid(P->g, P->order, L, P->edges, u0));
+            P->u_default = false;
+        }
+        // g_uprev = D^T u0
+        h = P->tstart(MVTV_K_GATHER);
+        int np0 = L.grid;
+        if (P->e3d)
+            HIP_TRY(launch_gather3d(P->g, P->order, U_EXPLICIT, P->stream, P->edges, 0.0, nullptr, gprev, nullptr, 1.0,
+                                    P->partials, &np0));
+        else
+            HIP_TRY(launch_gather(P->g, P->order, U_EXPLICIT, L, P->edges, 0.0, nullptr, gprev, nullptr, 1.0,
+                                  P->partials));
+        P->tstop(h);
+    }
+    // g_alpha = D^T D theta0 (alpha0 = D theta0, rcpp…/solvers.cpp:101)  ->  b_1 = oty + rho D^T (alpha0 + u0)
     h = P->tstart(MVTV_K_OTHER);
     HIP_TRY(launch_apply_A(P->g, L, 1.0, W_NONE, nullptr, P->theta, P->ga, nullptr, nullptr));
     P->tstop(h);
-    double c_prev = 1.0, t_z = 0.0;
-    int mode = U_EXPLICIT;
+    int np = L.grid;
 
     const bool track_theta = variant != MVTV_VARIANT_RCPP;
     double dtheta = 0.0;
@@ -668,6 +683,116 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         HIP_TRY(hipMemcpyAsync(P->host_red, P->red, sizeof(double), hipMemcpyDeviceToHost, P->stream));
         MVTV_TRY(P->sync());
         dtheta = P->host_red[0];
+    }
+
+    // ---- asynchronous loop (spectral theta-solve): the decisions of every iteration are taken on
+    // the device by k_admm_control, the host enqueues iterations ahead and polls the done flag -------
+    const bool first_runs = o.fixed_iters > 0 ? o.fixed_iters > 0
+                                              : (variant == MVTV_VARIANT_RCPP ? true
+                                                                              : (dtheta > tol && !(variant == MVTV_VARIANT_PY &&
+                                                                                                   max_counter <= 0)));
+    if (spectral && first_runs && !std::getenv("MVTV_ADMM_SYNC")) {
+        AdmmCtl& c = *P->host_ctl;
+        std::memset(&c, 0, sizeof(c));
+        c.variant = variant;
+        c.fixed_iters = o.fixed_iters > 0 ? o.fixed_iters : 0;
+        c.max_counter = max_counter;
+        c.lambda = lambda;
+        c.tol = tol;
+        c.sqrtN = std::sqrt(N);
+        c.sqrtE = std::sqrt(E);
+        c.rho = rho;
+        c.sigma = sigma;
+        c.c_prev = c_prev;
+        c.t_z = t_z;
+        c.t_next = rho != 0.0 ? lambda / rho : INFINITY;
+        c.counter = 1;
+        c.dtheta = dtheta;
+        c.dual_norm = c.primal_norm = 1.0;
+        c.eps_dual = c.eps_pri = tol;
+        HIP_TRY(hipMemcpyAsync(P->ctl, &c, sizeof(AdmmCtl), hipMemcpyHostToDevice, P->stream));
+        double* gbuf[2] = {P->guprev, P->gu};
+        auto enqueue = [&](int j) -> mvtv_status {
+            double* gp = gbuf[j & 1];
+            double* gn = gbuf[(j + 1) & 1];
+            const int um = j == 0 ? mode : U_FROM_Z;
+            if (track_theta)
+                HIP_TRY(hipMemcpyAsync(P->thold, P->theta, size_t(P->g.N) * sizeof(double), hipMemcpyDeviceToDevice,
+                                       P->stream));
+            MVTV_TRY(spectral_solve(P, sigma, P->oty, P->ga, rho, gp, rho, P->theta, P->ctl));
+            int hh = P->tstart(MVTV_K_EDGE_UPDATE);
+            int npe = L.grid;
+            if (P->e3d)
+                HIP_TRY(launch_edge3d(P->g, P->order, um, P->stream, P->theta, P->edges, 0.0, 1.0, 0.0,
+                                      track_theta ? P->thold : nullptr, P->partials, &npe, P->ctl));
+            else
+                HIP_TRY(launch_edge_update(P->g, P->order, um, L, P->theta, P->edges, 0.0, 1.0, 0.0,
+                                           track_theta ? P->thold : nullptr, P->partials, P->ctl));
+            P->tstop(hh);
+            hh = P->tstart(MVTV_K_REDUCE);
+            HIP_TRY(launch_finalize(P->stream, P->partials, npe, ER_N, 1, 0, P->red, P->st, 0.0, 0, P->ctl));
+            P->tstop(hh);
+            hh = P->tstart(MVTV_K_GATHER);
+            int npg = L.grid;
+            if (P->e3d)
+                HIP_TRY(launch_gather3d(P->g, P->order, U_FROM_Z, P->stream, P->edges, 0.0, P->ga, gn, gp, 1.0,
+                                        P->partials, &npg, P->ctl));
+            else
+                HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, L, P->edges, 0.0, P->ga, gn, gp, 1.0, P->partials,
+                                      P->ctl));
+            P->tstop(hh);
+            hh = P->tstart(MVTV_K_REDUCE);
+            HIP_TRY(launch_finalize(P->stream, P->partials, npg, GR_N, 0, 0, P->red + ER_N, P->st, 0.0, 0, P->ctl));
+            HIP_TRY(launch_admm_control(P->stream, P->ctl, P->red));
+            P->tstop(hh);
+            return MVTV_OK;
+        };
+        const int limit = o.fixed_iters > 0 ? o.fixed_iters
+                                            : (variant == MVTV_VARIANT_PY ? max_counter : max_counter + 1);
+        int target = o.fixed_iters > 0 ? o.fixed_iters : (P->admm_hint > 0 ? P->admm_hint : 16);
+        std::vector<size_t> mark;   // first timing entry of each enqueued iteration
+        int enq = 0;
+        for (;;) {
+            while (enq < target && enq < limit) {
+                mark.push_back(P->pending.size());
+                MVTV_TRY(enqueue(enq++));
+            }
+            HIP_TRY(hipMemcpyAsync(P->host_ctl, P->ctl, sizeof(AdmmCtl), hipMemcpyDeviceToHost, P->stream));
+            HIP_TRY(hipStreamSynchronize(P->stream));
+            if (c.done || enq >= limit) break;
+            target = enq + std::max(4, enq / 4);
+        }
+        const int it_done = c.it;
+        if (P->timing && it_done < int(mark.size()))   // iterations enqueued past the stop did no work
+            for (size_t e = mark[size_t(it_done)]; e < P->pending.size(); ++e) P->pending[e].kid = -1;
+        P->harvest();
+        if (o.fixed_iters <= 0 && c.status == 0) P->admm_hint = it_done + 1;
+        if (it_done & 1) std::swap(P->guprev, P->gu);   // P->guprev holds D^T u of the current state
+        if (it_done > 0) P->edge_mode = U_FROM_Z;
+        if (it_done > 0) P->t_z = c.t_z;
+        P->c_state = c.c_prev;
+        P->rho = c.rho;
+        mvtv_admm_stats S{};
+        S.iters = it_done;
+        S.rho = c.rho;
+        S.r_norm = c.r_norm;
+        S.s_norm = c.s_norm;
+        if (variant == MVTV_VARIANT_RCPP) {
+            S.eps_pri = c.eps_pri;
+            S.eps_dual = c.eps_dual;
+        }
+        S.dtheta_max = c.dtheta;
+        S.theta_solver = MVTV_SOLVER_SPECTRAL;
+        mvtv_status status = c.status ? MVTV_MAXITER : MVTV_OK;
+        if (status == MVTV_MAXITER) {
+            if (variant == MVTV_VARIANT_CPP) fail(status, "Failed to converge!");
+            else if (variant == MVTV_VARIANT_RCPP && o.verbose) std::printf("ADMM reached max_counter at lambda = %g\n", lambda);
+        }
+        if (o.verbose) std::printf("Lambda= %g, Counter = %d\n", lambda, c.counter);
+        S.status = status;
+        S.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (stats) *stats = S;
+        return status;
     }
 
     mvtv_admm_stats S{};

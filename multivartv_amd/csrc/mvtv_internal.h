@@ -94,6 +94,17 @@ struct PcgState {
     int32_t pad;
 };
 
+// Device-resident ADMM control (asynchronous loop, mvtv_capi.cpp): the scalars the kernels of one
+// iteration consume, written by k_admm_control at the end of each iteration. Every kernel of the
+// loop returns at once when `done` is set, so the host can enqueue iterations ahead of the decision.
+struct AdmmCtl {
+    int32_t done, status, it, counter;
+    int32_t variant, fixed_iters, max_counter, pad;
+    double lambda, tol, sqrtN, sqrtE;
+    double rho, sigma, c_prev, t_z, t_next;   // t_z: threshold z was formed with; t_next = lambda / rho
+    double r_norm, s_norm, eps_pri, eps_dual, dtheta, dual_norm, primal_norm;
+};
+
 enum UMode { U_EXPLICIT = 0, U_FROM_Z = 1 };
 enum WMode { W_NONE = 0, W_IDENTITY = 1, W_DIAG = 2 };
 
@@ -128,11 +139,14 @@ inline void klaunch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t
     }
 }
 
+// ctl != nullptr: scalars come from the device control block (t_old = t_z, c_old = c_prev,
+// t_new = t_next; gather t = t_next) and the launch is a no-op once ctl->done is set
 hipError_t launch_edge_update(const Geom& g, int order, int umode, const Launch& L, const double* theta,
                               double* edges, double t_old, double c_old, double t_new, const double* theta_old,
-                              double* partials);
+                              double* partials, const AdmmCtl* ctl = nullptr);
 hipError_t launch_gather(const Geom& g, int order, int umode, const Launch& L, const double* edges, double t,
-                         double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials);
+                         double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
+                         const AdmmCtl* ctl = nullptr);
 hipError_t launch_apply_A(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
                           const double* x, double* q, double* partials, const PcgState* st);
 hipError_t launch_pcg_init(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
@@ -146,7 +160,10 @@ hipError_t launch_pcg_pupdate(const Geom& g, const Launch& L, double sigma, int 
 // op: 0 plain (sums, ER_DTH-style max in the last nmax slots), 1 pcg-init, 2 pcg-after-Ap, 3 pcg-after-update,
 // 4 cg3d prologue, 5 cg3d iteration
 hipError_t launch_finalize(hipStream_t s, const double* partials, int nparts, int nr, int nmax, int op, double* out,
-                           PcgState* st, double rtol2 = 0.0, int maxit = 0);
+                           PcgState* st, double rtol2 = 0.0, int maxit = 0, const AdmmCtl* ctl = nullptr);
+// end of an asynchronous ADMM iteration: red = [|r|^2, |D theta|^2, |alpha|^2, max dtheta, |g_u|^2,
+// |s_B|^2, |s_A|^2]; adapt_step, stopping test and the next iteration's scalars (mvtv_capi.cpp mirror)
+hipError_t launch_admm_control(hipStream_t s, AdmmCtl* ctl, const double* red);
 // fused 3-D Chronopoulos-Gear PCG (mvtv_cg3d.hip): mode 0 prologue, 1 first iteration, 2 iteration;
 // partials get 4 values per workgroup (gamma, delta, |r|^2, |b|^2), *nblocks_out workgroups
 hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int wmode, const double* wdiag,
@@ -175,16 +192,16 @@ struct SpecPlan {
 // ga != nullptr forms the input as in + ca*ga + cb*gb. In place (in == out) is allowed.
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
-                           double w0);
+                           double w0, const AdmmCtl* ctl = nullptr);
 // z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /
 // launch_gather, *nparts workgroup rows
 bool edge3d_ok(const Geom& g);
 hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
                          double t_old, double c_old, double t_new, const double* theta_old, double* partials,
-                         int* nparts);
+                         int* nparts, const AdmmCtl* ctl = nullptr);
 hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                            double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
-                           int* nparts);
+                           int* nparts, const AdmmCtl* ctl = nullptr);
 hipError_t launch_gather_index(hipStream_t s, const double* theta, const int64_t* idx, int64_t n, double* out);
 
 }  // namespace mvtv

@@ -76,8 +76,14 @@ __global__ __launch_bounds__(kThreads) void k_edge_update(Geom g, const double* 
                                                           double* __restrict__ edges, double t_old,
                                                           double c_old, double t_new,
                                                           const double* __restrict__ theta_old,
-                                                          double* __restrict__ partials) {
+                                                          double* __restrict__ partials, const AdmmCtl* ctl) {
     constexpr int NC = 1 << P;
+    if (ctl) {
+        if (ctl->done) return;
+        t_old = ctl->t_z;
+        c_old = ctl->c_prev;
+        t_new = ctl->t_next;
+    }
     double red[ER_N] = {0.0, 0.0, 0.0, 0.0};
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < g.N; i += gridDim.x * kThreads) {
         uint32_t c[kMaxDims];
@@ -127,8 +133,13 @@ template <int P, int ORD, int UM, bool PREV>
 __global__ __launch_bounds__(kThreads) void k_gather(Geom g, const double* __restrict__ edges, double t,
                                                      double* __restrict__ g_alpha, double* __restrict__ g_u,
                                                      const double* __restrict__ g_uprev, double c_prev,
-                                                     double* __restrict__ partials) {
+                                                     double* __restrict__ partials, const AdmmCtl* ctl) {
     constexpr int NC = 1 << P;
+    if (ctl) {
+        if (ctl->done) return;
+        t = ctl->t_next;
+        c_prev = ctl->c_prev;
+    }
     double red[GR_N] = {0.0, 0.0, 0.0};
     for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < g.N; i += gridDim.x * kThreads) {
         uint32_t c[kMaxDims];
@@ -329,8 +340,9 @@ __global__ __launch_bounds__(kThreads) void k_pcg_pupdate(Geom g, double sigma, 
 // Sums the per-block partials in a fixed order (deterministic), then applies the PCG scalar step.
 __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ partials, int nparts, int nr,
                                                    int nmax, int op, double* __restrict__ out, PcgState* st,
-                                                   double rtol2, int maxit) {
+                                                   double rtol2, int maxit, const AdmmCtl* ctl) {
     if ((op == 2 || op == 3 || op == 5) && st->done) return;
+    if (ctl && ctl->done) return;
     __shared__ double sm[1024];
     __shared__ double res[kMaxRed];
     for (int k = 0; k < nr; ++k) {
@@ -519,12 +531,12 @@ int elem_grid(uint64_t n) {
 
 hipError_t launch_edge_update(const Geom& g, int order, int umode, const Launch& L, const double* theta,
                               double* edges, double t_old, double c_old, double t_new, const double* theta_old,
-                              double* partials) {
+                              double* partials, const AdmmCtl* ctl) {
     return dispatch_p(g.p, [&](auto pc) {
         constexpr int P = decltype(pc)::value;
         auto go = [&](auto kern) {
             klaunch(kern, dim3(L.grid), dim3(kThreads), 0, L.stream, g, theta, edges, t_old, c_old, t_new,
-                               theta_old, partials);
+                               theta_old, partials, ctl);
             return hipGetLastError();
         };
         const bool dth = theta_old != nullptr;
@@ -540,12 +552,13 @@ hipError_t launch_edge_update(const Geom& g, int order, int umode, const Launch&
 }
 
 hipError_t launch_gather(const Geom& g, int order, int umode, const Launch& L, const double* edges, double t,
-                         double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials) {
+                         double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
+                         const AdmmCtl* ctl) {
     return dispatch_p(g.p, [&](auto pc) {
         constexpr int P = decltype(pc)::value;
         auto go = [&](auto kern) {
             klaunch(kern, dim3(L.grid), dim3(kThreads), 0, L.stream, g, edges, t, g_alpha, g_u, g_uprev,
-                               c_prev, partials);
+                               c_prev, partials, ctl);
             return hipGetLastError();
         };
         const bool prev = g_uprev != nullptr;
@@ -644,8 +657,90 @@ hipError_t launch_pcg_pupdate(const Geom& g, const Launch& L, double sigma, int 
 }
 
 hipError_t launch_finalize(hipStream_t s, const double* partials, int nparts, int nr, int nmax, int op, double* out,
-                           PcgState* st, double rtol2, int maxit) {
-    klaunch(k_finalize, dim3(1), dim3(1024), 0, s, partials, nparts, nr, nmax, op, out, st, rtol2, maxit);
+                           PcgState* st, double rtol2, int maxit, const AdmmCtl* ctl) {
+    klaunch(k_finalize, dim3(1), dim3(1024), 0, s, partials, nparts, nr, nmax, op, out, st, rtol2, maxit, ctl);
+    return hipGetLastError();
+}
+
+// One thread: the host loop body of mvtv_admm_run after the reductions, verbatim (same operations
+// in the same order, so decisions match the synchronous loop), then the next iteration's top test.
+__global__ void k_admm_control(AdmmCtl* __restrict__ c, const double* __restrict__ R) {
+    if (c->done) return;
+    const double* G = R + ER_N;
+    const double r_norm = sqrt(R[ER_R2]);
+    const double rho = c->rho;
+    c->t_z = c->t_next;
+    c->it += 1;
+    c->counter += 1;
+    double c_next = 1.0, rho_next = rho;
+    int status = 0;
+    const bool fixed = c->fixed_iters > 0;
+    if (c->variant == 0) {   // B: rcpp-code/MultivarTV/src/solvers.cpp:117-125
+        c->dual_norm = fabs(rho) * sqrt(G[GR_S2B]);
+        c->primal_norm = r_norm;
+        c->eps_dual = c->tol * (c->sqrtN + sqrt(G[GR_GU2]));
+        c->eps_pri = c->tol * (c->sqrtE + fmax(sqrt(R[ER_D2]), sqrt(R[ER_A2])));
+        const double tau = 2.0;
+        if (c->primal_norm > 10 * c->dual_norm) {
+            rho_next = tau * rho;
+            c_next = 1.0 / tau;
+        } else if (c->dual_norm > 10 * c->primal_norm) {
+            rho_next = 1.0 / tau * rho;
+            c_next = tau;
+        }
+        c->s_norm = c->dual_norm;
+    } else if (c->variant == 1) {   // A: cpp-code/solvers.cpp:118-126
+        const double s_norm = fabs(rho) * sqrt(G[GR_S2A]);
+        c->dtheta = R[ER_DTH];
+        c->s_norm = s_norm;
+        if (!fixed && c->counter > c->max_counter) {
+            status = 1;
+            rho_next = rho;
+        } else {
+            if (r_norm > 20 * s_norm) {
+                rho_next = 20 * rho;
+                c_next = 0.05;
+            } else if (s_norm > 20 * r_norm) {
+                rho_next = 0.1 * rho;
+                c_next = 10.0;
+            }
+            rho_next = double(int(rho_next));
+        }
+    } else {
+        c->dtheta = R[ER_DTH];
+    }
+    c->r_norm = r_norm;
+    c->c_prev = c_next;
+    c->rho = rho_next;
+    if (c->variant == 0) c->sigma = rho_next;
+    c->t_next = rho_next != 0.0 ? c->lambda / rho_next : INFINITY;
+    if (status) {
+        c->status = 1;
+        c->done = 1;
+        return;
+    }
+    if (c->variant == 0 && !fixed && c->counter > c->max_counter) {
+        c->status = 1;
+        c->done = 1;
+        return;
+    }
+    // loop-top test of the next iteration
+    if (fixed) {
+        if (c->it >= c->fixed_iters) c->done = 1;
+    } else if (c->variant == 0) {
+        if (!(c->dual_norm > c->eps_dual || c->primal_norm > c->eps_pri)) c->done = 1;
+    } else {
+        if (!(c->dtheta > c->tol)) {
+            c->done = 1;
+        } else if (c->variant == 2 && c->it >= c->max_counter) {
+            c->status = 1;
+            c->done = 1;
+        }
+    }
+}
+
+hipError_t launch_admm_control(hipStream_t s, AdmmCtl* ctl, const double* red) {
+    klaunch(k_admm_control, dim3(1), dim3(1), 0, s, ctl, red);
     return hipGetLastError();
 }
 

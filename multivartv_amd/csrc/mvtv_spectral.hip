@@ -65,6 +65,7 @@ struct SpecArgs {
     uint32_t nlines;         // N / m
     int32_t d, p, L, tq;     // line dimension, dims, log2 m, lines per workgroup
     int32_t ls;              // log2 stride
+    const AdmmCtl* ctl;      // asynchronous ADMM loop: sigma, ca = rho, cb = rho c_prev from the device
 };
 
 enum SpecMode { SPEC_FWD = 0, SPEC_INV = 1, SPEC_MID = 2 };
@@ -182,7 +183,14 @@ __device__ __forceinline__ uint32_t line_addr(const SpecArgs& a, uint32_t q0, ui
 }
 
 template <int MODE, bool D0, bool FORMB>
-__global__ __launch_bounds__(spec::NT) void k_dct(SpecArgs a) {
+__global__ __launch_bounds__(spec::NT) void k_dct(const SpecArgs a) {
+    double sigma = a.sigma, ca = a.ca, cb = a.cb;   // locals: see k_dct8
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+        ca = a.ctl->rho;
+        cb = a.ctl->rho * a.ctl->c_prev;
+    }
     __shared__ double2 buf[spec::LDS_WORDS / 2 + 8 * spec::PAD];
     __shared__ double lc0[16], lc1[16];     // MID: per-line eigenvalue coefficients
     const int L = a.L;
@@ -207,7 +215,7 @@ __global__ __launch_bounds__(spec::NT) void k_dct(SpecArgs a) {
         const int dbit = 1 << a.d;
         for (int S = 1; S < (1 << a.p); ++S) {
             if (a.cS[S] == 0.0) continue;
-            double prod = a.sigma * a.cS[S];
+            double prod = sigma * a.cS[S];
             for (int j = 0; j < a.p; ++j)
                 if (j != a.d && ((S >> j) & 1)) prod *= lamv[j];
             if (S & dbit) c1 += prod;
@@ -233,7 +241,7 @@ __global__ __launch_bounds__(spec::NT) void k_dct(SpecArgs a) {
         if (q0 + ql < a.nlines) {
             const uint32_t gi = line_addr<D0>(a, q0, ql, k);
             v = __builtin_nontemporal_load(a.in + gi);
-            if (FORMB) v += a.ca * __builtin_nontemporal_load(a.ga + gi) + a.cb * __builtin_nontemporal_load(a.gb + gi);
+            if (FORMB) v += ca * __builtin_nontemporal_load(a.ga + gi) + cb * __builtin_nontemporal_load(a.gb + gi);
         }
         const uint32_t pos = (MODE == SPEC_INV) ? k : perm_pos(k, m, L);
         bw[2 * ((ql >> 1) * LP + pos) + (ql & 1)] = v;
@@ -461,8 +469,16 @@ struct LastStage {
 };
 
 template <int L, int MODE, bool D0, bool FORMB>
-__global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
+__global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(const SpecArgs a) {
     using S = spec8::Shape<L>;
+    // scalars into locals: writing into the by-value argument struct would demote it to scratch
+    double sigma = a.sigma, ca = a.ca, cb = a.cb;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+        ca = a.ctl->rho;
+        cb = a.ctl->rho * a.ctl->c_prev;
+    }
     constexpr int M = S::M, TPL = S::TPL, NCL = S::NCL;
     __shared__ double2 buf[NCL * S::LP];
     __shared__ double lc0[2 * NCL], lc1[2 * NCL];
@@ -489,7 +505,7 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
         double c0 = a.w0, c1 = 0.0;
         for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
             if (a.cS[Sm] == 0.0) continue;
-            double prod = a.sigma * a.cS[Sm];
+            double prod = sigma * a.cS[Sm];
             for (int jj = 0; jj < a.p; ++jj)
                 if (jj != a.d && ((Sm >> jj) & 1)) prod *= lamv[jj];
             if ((Sm >> a.d) & 1) c1 += prod;
@@ -511,12 +527,12 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
             if (va) {
                 const uint32_t g = gaddr(la, k);
                 v.x = __builtin_nontemporal_load(a.in + g);
-                if (FORMB) v.x += a.ca * __builtin_nontemporal_load(a.ga + g) + a.cb * __builtin_nontemporal_load(a.gb + g);
+                if (FORMB) v.x += ca * __builtin_nontemporal_load(a.ga + g) + cb * __builtin_nontemporal_load(a.gb + g);
             }
             if (vb) {
                 const uint32_t g = gaddr(lb, k);
                 v.y = __builtin_nontemporal_load(a.in + g);
-                if (FORMB) v.y += a.ca * __builtin_nontemporal_load(a.ga + g) + a.cb * __builtin_nontemporal_load(a.gb + g);
+                if (FORMB) v.y += ca * __builtin_nontemporal_load(a.ga + g) + cb * __builtin_nontemporal_load(a.gb + g);
             }
         } else if (va) {   // d > 0: lines la, lb are adjacent words (vb == va)
             const uint32_t g = gaddr(la, k);
@@ -524,8 +540,8 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
             if (FORMB) {
                 const double2 x1 = ldnt2(a.ga + g);
                 const double2 x2 = ldnt2(a.gb + g);
-                v.x += a.ca * x1.x + a.cb * x2.x;
-                v.y += a.ca * x1.y + a.cb * x2.y;
+                v.x += ca * x1.x + cb * x2.x;
+                v.y += ca * x1.y + cb * x2.y;
             }
         }
         return v;
@@ -554,8 +570,8 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
                     xa = ldnt2(a.in + g);
                     if (FORMB) {
                         const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
-                        xa.x += a.ca * g1.x + a.cb * g2.x;
-                        xa.y += a.ca * g1.y + a.cb * g2.y;
+                        xa.x += ca * g1.x + cb * g2.x;
+                        xa.y += ca * g1.y + cb * g2.y;
                     }
                 }
                 if (vb) {
@@ -563,8 +579,8 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(SpecArgs a) {
                     xb = ldnt2(a.in + g);
                     if (FORMB) {
                         const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
-                        xb.x += a.ca * g1.x + a.cb * g2.x;
-                        xb.y += a.ca * g1.y + a.cb * g2.y;
+                        xb.x += ca * g1.x + cb * g2.x;
+                        xb.y += ca * g1.y + cb * g2.y;
                     }
                 }
                 X[spec8::slot(n, cx)] = make_double2(xa.x, xb.x);
@@ -695,8 +711,9 @@ static void launch_dct8(const SpecArgs& a, hipStream_t s, int mode, bool d0, boo
 
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
-                           double w0) {
+                           double w0, const AdmmCtl* ctl) {
     SpecArgs a{};
+    a.ctl = ctl;
     a.in = in;
     a.ga = ga;
     a.gb = gb;

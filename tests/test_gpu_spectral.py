@@ -119,3 +119,29 @@ def test_spectral_admm_towers_3d():
     assert ss["theta_solver"] == mv.SOLVER_SPECTRAL and sp["theta_solver"] == mv.SOLVER_PCG
     assert ss["iters"] == sp["iters"] and rs == rp
     assert _rel(ts, tp) <= 1e-8
+
+
+@pytest.mark.parametrize("variant", [mv.VARIANT_RCPP, mv.VARIANT_CPP, mv.VARIANT_PY])
+def test_async_loop_matches_host_loop(variant, monkeypatch):
+    """The device-side ADMM control (k_admm_control, no per-iteration host sync) takes the same
+    decisions as the host loop: same iteration count, rho, and theta to the last bit in practice."""
+    from multivartv_amd.synth import towers
+    m = [16, 16, 16]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    lam = 1.0 if variant == mv.VARIANT_RCPP else 2.0
+    out = {}
+    for mode in ("async", "sync"):
+        if mode == "sync":
+            monkeypatch.setenv("MVTV_ADMM_SYNC", "1")
+        else:
+            monkeypatch.delenv("MVTV_ADMM_SYNC", raising=False)
+        with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+            th0 = np.full(y.size, y.mean())
+            out[mode] = P.admm(lam, th0, u=np.zeros(P.E) if variant == mv.VARIANT_RCPP else None, rho=lam / 5,
+                               variant=variant, ymean=float(y.mean()), return_u=True)
+    (ta, ua, ra, sa), (ts, us, rs, ss) = out["async"], out["sync"]
+    assert sa["theta_solver"] == mv.SOLVER_SPECTRAL
+    assert sa["iters"] == ss["iters"] and ra == rs and sa["status"] == ss["status"]
+    assert _rel(ta, ts) <= 1e-12
+    assert np.max(np.abs(ua - us)) <= 1e-12 * max(1.0, np.max(np.abs(us)))
