@@ -16,13 +16,14 @@
 // sit in the same L2.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "mvtv_device.h"
 
 namespace mvtv {
 
 namespace e3d {
-constexpr int TX = 64, TY = 4, NT = TX * TY;
+constexpr int TX = 64;
 }
 
 struct Edge3dArgs {
@@ -38,6 +39,7 @@ struct Edge3dArgs {
     double t, c_prev;             // gather3d
     const AdmmCtl* ctl;           // device scalars (asynchronous loop) or nullptr
     int tiles_x, tiles_y, zchunk, nblocks;
+    int ty;                       // rows per tile (= waves per workgroup)
 };
 
 // tile of this workgroup (XCD-aware: XCD b%8 gets a contiguous run of tiles)
@@ -54,7 +56,7 @@ __device__ __forceinline__ Tile3 tile3(const Edge3dArgs& a) {
     const int tz = bid / nt, rem = bid - tz * nt;
     const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
     t.x = tx * e3d::TX + int(threadIdx.x & 63);
-    t.y = ty * e3d::TY + int(threadIdx.x >> 6);
+    t.y = ty * a.ty + int(threadIdx.x >> 6);
     t.z0 = tz * a.zchunk;
     t.z1 = min(int(a.g.m[2]), t.z0 + a.zchunk);
     return t;
@@ -63,8 +65,10 @@ __device__ __forceinline__ Tile3 tile3(const Edge3dArgs& a) {
 // --------------------------------------------------------------------- edge update
 // z_new = D theta - u_old; alpha = soft(z_new, t_new); r = alpha - D theta.
 // Reductions: |r|^2, |D theta|^2, |alpha|^2 and (DTH) max |theta - theta_old|.
-template <int ORD, int UM, bool DTH>
-__global__ __launch_bounds__(e3d::NT) void k_edge3d(const Edge3dArgs a) {
+// NB (blocks of D: 7, or 6 for Python's weighted create_D) is a template parameter so the block
+// loop has no branches and every block's loads of a step issue together.
+template <int ORD, int UM, bool DTH, int NT, int NB>
+__global__ __launch_bounds__(NT) void k_edge3d(const Edge3dArgs a) {
     constexpr int P = 3, NC = 8;
     const Geom& g = a.g;
     double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new;
@@ -103,10 +107,10 @@ __global__ __launch_bounds__(e3d::NT) void k_edge3d(const Edge3dArgs a) {
 #pragma unroll
                 for (int q = 0; q < NC; ++q)
                     if (!((q >> j) & 1)) v[q | (1 << j)] = v[q] - v[q | (1 << j)];
-            static_for<0, 7>([&](auto kc) {
+            static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                if (k < g.nb) {
+                {
                     const double d = g.w[k] * v[S];
                     double* ep = a.edges + uint64_t(k) * g.N + i;
                     const double stored = __builtin_nontemporal_load(ep);
@@ -126,14 +130,14 @@ __global__ __launch_bounds__(e3d::NT) void k_edge3d(const Edge3dArgs a) {
     }
     if (!T.valid)
         for (int k = 0; k < ER_N; ++k) red[k] = 0.0;
-    block_reduce_store<ER_N, 1, e3d::NT>(red, a.partials);
+    block_reduce_store<ER_N, 1, NT>(red, a.partials);
 }
 
 // --------------------------------------------------------------------- D^T gather
 // g_alpha = D^T alpha, g_u = D^T u (u unscaled: -clamp(z, t)); explicit mode: g_u = D^T v.
 // Reductions: |g_u|^2, |g_u - c_prev g_uprev|^2 (B's dual residual), |g_alpha + c_prev g_uprev|^2 (A's).
-template <int ORD, int UM, bool PREV>
-__global__ __launch_bounds__(e3d::NT) void k_gather3d(const Edge3dArgs a) {
+template <int ORD, int UM, bool PREV, int NT, int NB>
+__global__ __launch_bounds__(NT) void k_gather3d(const Edge3dArgs a) {
     constexpr int P = 3;
     const Geom& g = a.g;
     double tt = a.t, c_prev = a.c_prev;
@@ -180,18 +184,18 @@ __global__ __launch_bounds__(e3d::NT) void k_gather3d(const Edge3dArgs a) {
             }
         };
         if (T.z0 > 0) {   // carried sums of plane z0 - 1
-            static_for<0, 7>([&](auto kc) {
+            static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                if (k < g.nb && (S & 4)) plane_q(kc, T.z0 - 1, qa_prev[k], qu_prev[k]);
+                if constexpr ((S & 4) != 0) plane_q(kc, T.z0 - 1, qa_prev[k], qu_prev[k]);
             });
         }
         for (int e = T.z0; e < T.z1; ++e) {
             double ga = 0.0, gu = 0.0;
-            static_for<0, 7>([&](auto kc) {
+            static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                if (k < g.nb) {
+                {
                     double qa, qu;
                     plane_q(kc, e, qa, qu);
                     double ca = qa, cu = qu;
@@ -219,22 +223,31 @@ __global__ __launch_bounds__(e3d::NT) void k_gather3d(const Edge3dArgs a) {
     }
     if (!T.valid)
         for (int k = 0; k < GR_N; ++k) red[k] = 0.0;
-    block_reduce_store<GR_N, 0, e3d::NT>(red, a.partials);
+    block_reduce_store<GR_N, 0, NT>(red, a.partials);
 }
 
 // ------------------------------------------------------------------------------------ launchers
 namespace {
+int e3d_rows() {
+    static const int ty = [] {
+        const char* e = std::getenv("MVTV_E3D_TY");
+        const int v = e ? std::atoi(e) : 4;
+        return v == 8 ? 8 : 4;
+    }();
+    return ty;
+}
 Edge3dArgs e3d_args(const Geom& g) {
     Edge3dArgs a{};
     a.g = g;
+    a.ty = e3d_rows();
     a.tiles_x = int((g.m[0] + e3d::TX - 1) / e3d::TX);
-    a.tiles_y = int((g.m[1] + e3d::TY - 1) / e3d::TY);
+    a.tiles_y = int((g.m[1] + a.ty - 1) / a.ty);
     const int tiles = a.tiles_x * a.tiles_y;
     // dim-2 chunks: enough workgroups to fill 256 CUs several times over, long enough marches
     // that the carried plane (gather) and the extra theta plane (edge) are amortised
     static const int want = [] {
         const char* e = std::getenv("MVTV_E3D_WG");
-        return e ? std::atoi(e) : 4096;
+        return e ? std::atoi(e) : 8192;
     }();
     int nz = std::max(1, std::min(int(g.m[2]), want / std::max(1, tiles)));
     while (nz > 1 && ((nz * tiles + 7) / 8 * 8) > kMaxCgBlocks) --nz;
@@ -265,17 +278,29 @@ hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, con
     a.t_new = t_new;
     const int grid = (a.nblocks + 7) / 8 * 8;
     *nparts = grid;
-    auto go = [&](auto kern) {
-        klaunch(kern, dim3(grid), dim3(e3d::NT), 0, s, a);
-        return hipGetLastError();
-    };
     const bool dth = theta_old != nullptr;
-    if (order == 0) {
-        if (umode == U_EXPLICIT) return dth ? go(k_edge3d<0, U_EXPLICIT, true>) : go(k_edge3d<0, U_EXPLICIT, false>);
-        return dth ? go(k_edge3d<0, U_FROM_Z, true>) : go(k_edge3d<0, U_FROM_Z, false>);
-    }
-    if (umode == U_EXPLICIT) return dth ? go(k_edge3d<1, U_EXPLICIT, true>) : go(k_edge3d<1, U_EXPLICIT, false>);
-    return dth ? go(k_edge3d<1, U_FROM_Z, true>) : go(k_edge3d<1, U_FROM_Z, false>);
+    auto pick = [&](auto ntc) {
+        constexpr int NT = decltype(ntc)::value;
+        auto go = [&](auto kern) {
+            klaunch(kern, dim3(grid), dim3(NT), 0, s, a);
+            return hipGetLastError();
+        };
+        if (order == 0) {
+            if (umode == U_EXPLICIT)
+                return dth ? go(k_edge3d<0, U_EXPLICIT, true, NT, 7>) : go(k_edge3d<0, U_EXPLICIT, false, NT, 7>);
+            return dth ? go(k_edge3d<0, U_FROM_Z, true, NT, 7>) : go(k_edge3d<0, U_FROM_Z, false, NT, 7>);
+        }
+        if (g.nb == 6) {
+            if (umode == U_EXPLICIT)
+                return dth ? go(k_edge3d<1, U_EXPLICIT, true, NT, 6>) : go(k_edge3d<1, U_EXPLICIT, false, NT, 6>);
+            return dth ? go(k_edge3d<1, U_FROM_Z, true, NT, 6>) : go(k_edge3d<1, U_FROM_Z, false, NT, 6>);
+        }
+        if (umode == U_EXPLICIT)
+            return dth ? go(k_edge3d<1, U_EXPLICIT, true, NT, 7>) : go(k_edge3d<1, U_EXPLICIT, false, NT, 7>);
+        return dth ? go(k_edge3d<1, U_FROM_Z, true, NT, 7>) : go(k_edge3d<1, U_FROM_Z, false, NT, 7>);
+    };
+    if (a.ty == 8) return pick(std::integral_constant<int, 512>{});
+    return pick(std::integral_constant<int, 256>{});
 }
 
 hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
@@ -292,17 +317,29 @@ hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, c
     a.c_prev = c_prev;
     const int grid = (a.nblocks + 7) / 8 * 8;
     *nparts = grid;
-    auto go = [&](auto kern) {
-        klaunch(kern, dim3(grid), dim3(e3d::NT), 0, s, a);
-        return hipGetLastError();
-    };
     const bool prev = g_uprev != nullptr;
-    if (order == 0) {
-        if (umode == U_EXPLICIT) return prev ? go(k_gather3d<0, U_EXPLICIT, true>) : go(k_gather3d<0, U_EXPLICIT, false>);
-        return prev ? go(k_gather3d<0, U_FROM_Z, true>) : go(k_gather3d<0, U_FROM_Z, false>);
-    }
-    if (umode == U_EXPLICIT) return prev ? go(k_gather3d<1, U_EXPLICIT, true>) : go(k_gather3d<1, U_EXPLICIT, false>);
-    return prev ? go(k_gather3d<1, U_FROM_Z, true>) : go(k_gather3d<1, U_FROM_Z, false>);
+    auto pick = [&](auto ntc) {
+        constexpr int NT = decltype(ntc)::value;
+        auto go = [&](auto kern) {
+            klaunch(kern, dim3(grid), dim3(NT), 0, s, a);
+            return hipGetLastError();
+        };
+        if (order == 0) {
+            if (umode == U_EXPLICIT)
+                return prev ? go(k_gather3d<0, U_EXPLICIT, true, NT, 7>) : go(k_gather3d<0, U_EXPLICIT, false, NT, 7>);
+            return prev ? go(k_gather3d<0, U_FROM_Z, true, NT, 7>) : go(k_gather3d<0, U_FROM_Z, false, NT, 7>);
+        }
+        if (g.nb == 6) {
+            if (umode == U_EXPLICIT)
+                return prev ? go(k_gather3d<1, U_EXPLICIT, true, NT, 6>) : go(k_gather3d<1, U_EXPLICIT, false, NT, 6>);
+            return prev ? go(k_gather3d<1, U_FROM_Z, true, NT, 6>) : go(k_gather3d<1, U_FROM_Z, false, NT, 6>);
+        }
+        if (umode == U_EXPLICIT)
+            return prev ? go(k_gather3d<1, U_EXPLICIT, true, NT, 7>) : go(k_gather3d<1, U_EXPLICIT, false, NT, 7>);
+        return prev ? go(k_gather3d<1, U_FROM_Z, true, NT, 7>) : go(k_gather3d<1, U_FROM_Z, false, NT, 7>);
+    };
+    if (a.ty == 8) return pick(std::integral_constant<int, 512>{});
+    return pick(std::integral_constant<int, 256>{});
 }
 
 }  // namespace mvtv
