@@ -359,6 +359,13 @@ struct Shape {
     static constexpr int LP = (M + M / 8 + 15) / 16 * 16 + 8;
     static constexpr int R0 = (L % 3 == 0) ? 8 : (L % 3 == 1 ? 2 : 4);    // radix of the first stage
 };
+// kernel-level shape with an optional smaller tile (TQW real lines per workgroup)
+template <int L, int TQW>
+struct ShapeK : Shape<L> {
+    static constexpr int TQ = TQW > 0 ? TQW : Shape<L>::TQ;
+    static constexpr int NCL = TQ / 2;
+    static constexpr int NT = NCL * Shape<L>::TPL;
+};
 __device__ __forceinline__ int pidx(int pos) { return pos + (pos >> 3); }   // one pad slot per 8
 __device__ __forceinline__ int slot(int pos, int cx) { return pidx(pos) ^ cx; }
 }  // namespace spec8
@@ -468,9 +475,9 @@ struct LastStage {
     static constexpr int NS = (1 << L) / R;
 };
 
-template <int L, int MODE, bool D0, bool FORMB>
-__global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(const SpecArgs a) {
-    using S = spec8::Shape<L>;
+template <int L, int MODE, bool D0, bool FORMB, int TQW = 0>
+__global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const SpecArgs a) {
+    using S = spec8::ShapeK<L, TQW>;
     // scalars into locals: writing into the by-value argument struct would demote it to scratch
     double sigma = a.sigma, ca = a.ca, cb = a.cb;
     if (a.ctl) {
@@ -684,8 +691,10 @@ __global__ __launch_bounds__(spec8::Shape<L>::NT) void k_dct8(const SpecArgs a) 
 
 // ------------------------------------------------------------------------------ launcher
 template <int L>
-static void launch_dct8(const SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
+static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
     using S = spec8::Shape<L>;
+    // tile size: 16 lines (128-B rows for d > 0) measured best; 8 lines (64-B rows) cost +50 % per
+    // pass and 32 lines (one 150-KB workgroup per CU) +6 % at 512^3
     const dim3 grid((a.nlines + uint32_t(a.tq) - 1) / uint32_t(a.tq)), block(S::NT);
 #define MVTV_DCT8(MODE, D0, FB) klaunch(k_dct8<L, MODE, D0, FB>, grid, block, 0, s, a)
     if (mode == SPEC_FWD) {
