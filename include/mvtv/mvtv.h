@@ -155,6 +155,10 @@ mvtv_status mvtv_apply_Dt(mvtv_problem* prob, const double* v, double* g_out);  
 mvtv_status mvtv_apply_A(mvtv_problem* prob, double sigma, const double* x, double* q_out); /* (W + sigma D^T D) x */
 mvtv_status mvtv_solve(mvtv_problem* prob, double sigma, const double* b, double* x_inout,
                        double rtol, int32_t max_iter, int32_t* iters, double* relres);
+/* lam_max_pinv (rcpp…/utils.cpp:306-355, called by create_lambdas rcpp…/solvers.cpp:186-200):
+ * 5 ||D x||_inf with x from the reference's CG on D^T D x = O^T y (relative stop 1e-4, at most
+ * min(N, 2000) iterations), its recurrences reproduced step by step on the GPU. */
+mvtv_status mvtv_lambda_max(mvtv_problem* prob, double* out, int32_t* iters);
 /* direct theta-solve (I + sigma D^T D) x = b by cosine transforms (MVTV_SOLVER_SPECTRAL) */
 mvtv_status mvtv_solve_spectral(mvtv_problem* prob, double sigma, const double* b, double* x_out);
 

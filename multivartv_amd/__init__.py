@@ -7,4 +7,6 @@ the reference's Python interface (code/solvers.py, code/utils.py) over that ABI.
 from ._lib import (ORDER_CPP, ORDER_PY, SOLVER_AUTO, SOLVER_PCG, SOLVER_SPECTRAL, VARIANT_CPP,  # noqa: F401
                    VARIANT_PY, VARIANT_RCPP, DimMismatchError, MaxIterError, MvtvError, Problem, device_count, lib)
 
+from . import cv  # noqa: E402,F401  (CV / lambda-path driver, rcpp…/solvers.cpp:186-376)
+
 __version__ = "0.1.0"

@@ -88,6 +88,7 @@ SIGNATURES = {
     "mvtv_apply_A": (C.c_int, [C.c_void_p, C.c_double, _dp, _dp]),
     "mvtv_solve": (C.c_int, [C.c_void_p, C.c_double, _dp, _dp, C.c_double, C.c_int32, C.POINTER(C.c_int32), _dp]),
     "mvtv_solve_spectral": (C.c_int, [C.c_void_p, C.c_double, _dp, _dp]),
+    "mvtv_lambda_max": (C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int32)]),
     "mvtv_timing_enable": (C.c_int, [C.c_void_p, C.c_int32]),
     "mvtv_timing_get": (C.c_int, [C.c_void_p, C.c_int32, _dp, C.POINTER(C.c_int64), _dp]),
     "mvtv_kernel_name": (C.c_char_p, [C.c_int32]),
@@ -287,6 +288,12 @@ class Problem:
         _check(lib().mvtv_solve(self._h, float(sigma), _ptr(bb), _ptr(x), float(rtol), int(max_iter),
                                 C.byref(it), C.byref(rr)))
         return x, it.value, rr.value
+
+    def lambda_max(self):
+        """lam_max_pinv of the released package on the GPU: (lambda_max, CG iterations)."""
+        v, it = C.c_double(), C.c_int32()
+        _check(lib().mvtv_lambda_max(self._h, C.byref(v), C.byref(it)))
+        return v.value, it.value
 
     def spectral_ok(self) -> bool:
         return bool(lib().mvtv_problem_spectral_ok(self._h))

@@ -1058,6 +1058,63 @@ mvtv_status mvtv_solve(mvtv_problem* P, double sigma, const double* b, double* x
     return s;
 }
 
+mvtv_status mvtv_lambda_max(mvtv_problem* P, double* out, int32_t* iters) {
+    if (!P || !out) return fail(MVTV_BAD_ARG, "null argument");
+    DeviceGuard dg(P->device);
+    const Launch L = P->L();
+    const size_t bytes = size_t(P->g.N) * sizeof(double);
+    // scratch: x, d, r, p, t (the PCG buffers; the ADMM state theta / edges is untouched)
+    if (!P->p2) MVTV_TRY(alloc(&P->p2, P->g.N));
+    if (!P->thold) MVTV_TRY(alloc(&P->thold, P->g.N));
+    double *x = P->thold, *d = P->r, *r = P->q, *p = P->p, *t = P->p2;
+    auto dot = [&](double* v, double* res) -> mvtv_status {
+        HIP_TRY(launch_cg_vec(P->g, L, 0, 0.0, v, nullptr, nullptr, nullptr, P->partials));
+        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 0, 0, P->red, P->st));
+        HIP_TRY(hipMemcpyAsync(P->host_red, P->red, sizeof(double), hipMemcpyDeviceToHost, P->stream));
+        HIP_TRY(hipStreamSynchronize(P->stream));
+        *res = P->host_red[0];
+        return MVTV_OK;
+    };
+    auto AtA = [&](const double* v, double* outv) -> mvtv_status {   // crossD * v (W = 0, sigma = 1)
+        HIP_TRY(launch_apply_A(P->g, L, 1.0, W_NONE, nullptr, v, outv, nullptr, nullptr));
+        return MVTV_OK;
+    };
+    // cg(ata, Oty) of rcpp…/utils.cpp:306-341, line by line
+    HIP_TRY(hipMemsetAsync(x, 0, bytes, P->stream));
+    HIP_TRY(hipMemcpyAsync(d, P->oty, bytes, hipMemcpyDeviceToDevice, P->stream));   // d = b - A x, x = 0
+    MVTV_TRY(AtA(d, r));                                                             // r = A^T d
+    HIP_TRY(hipMemcpyAsync(p, r, bytes, hipMemcpyDeviceToDevice, P->stream));
+    double rr = 0.0;
+    MVTV_TRY(dot(r, &rr));
+    const double rsold0 = std::sqrt(rr);
+    double rsold = std::pow(rsold0, 2), rsnew = rsold + 1.0;
+    MVTV_TRY(AtA(p, t));
+    int iter = 0;
+    const int MAXIT = P->g.N < 2000 ? int(P->g.N) : 2000;
+    while (std::sqrt(rsnew) >= 0.0001 * rsold0) {
+        double tt = 0.0;
+        MVTV_TRY(dot(t, &tt));
+        const double alpha = rsold / std::pow(std::sqrt(tt), 2);
+        HIP_TRY(launch_cg_vec(P->g, L, 1, alpha, x, d, p, t, nullptr));
+        MVTV_TRY(AtA(d, r));
+        MVTV_TRY(dot(r, &rr));
+        rsnew = std::pow(std::sqrt(rr), 2);
+        iter += 1;
+        if (iter == MAXIT) break;
+        HIP_TRY(launch_cg_vec(P->g, L, 2, rsnew / rsold, p, nullptr, r, nullptr, nullptr));   // p = r + beta p
+        MVTV_TRY(AtA(p, t));
+        rsold = rsnew;
+    }
+    // 5 * ||D x||_inf (lam_max_pinv, :351-355)
+    HIP_TRY(launch_dmaxabs(P->g, P->order, L, x, P->partials));
+    HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 1, 0, P->red, P->st));
+    HIP_TRY(hipMemcpyAsync(P->host_red, P->red, sizeof(double), hipMemcpyDeviceToHost, P->stream));
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    *out = 5.0 * P->host_red[0];
+    if (iters) *iters = iter;
+    return MVTV_OK;
+}
+
 mvtv_status mvtv_solve_spectral(mvtv_problem* P, double sigma, const double* b, double* x_out) {
     if (!P || !b || !x_out) return fail(MVTV_BAD_ARG, "null argument");
     if (!spectral_ok(P)) return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and power-of-two m_j <= 4096");

@@ -172,6 +172,11 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
                        const double* gb, double cb, const PcgState* st, double* partials, int* nblocks_out);
 hipError_t launch_maxabsdiff(const Geom& g, const Launch& L, const double* a, const double* b, double* partials);
 hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n);
+// CG vector steps of lam_max_pinv (op 0 |x|^2 into partials, 1 x += c p & y -= c t, 2 x = p + c x)
+hipError_t launch_cg_vec(const Geom& g, const Launch& L, int op, double coef, double* x, double* y, const double* p,
+                         const double* t, double* partials);
+// per-workgroup max |D x| (one max-partial per workgroup, L.grid rows)
+hipError_t launch_dmaxabs(const Geom& g, int order, const Launch& L, const double* x, double* partials);
 // compact <-> padded edge layouts for one block segment [e0, e0+cnt) of block k
 hipError_t launch_edges_import(const Geom& g, int order, hipStream_t s, int k, uint64_t e0, uint64_t cnt,
                                const double* compact, double* padded);

@@ -419,6 +419,58 @@ __global__ void k_fill(double* __restrict__ x, double v, uint64_t n) {
         x[i] = v;
 }
 
+// --------------------------------------------------------------------- lam_max_pinv support
+// CG on (D^T D) with the reference's recurrences (rcpp-code/MultivarTV/src/utils.cpp:306-355):
+// op 0: sum x*x;  op 1: x += alpha p, d -= alpha t;  op 2: p = r + beta p
+__global__ __launch_bounds__(kThreads) void k_cg_vec(int op, uint32_t n, double coef, double* __restrict__ x,
+                                                     double* __restrict__ y, const double* __restrict__ p,
+                                                     const double* __restrict__ t, double* __restrict__ partials) {
+    double red[1] = {0.0};
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        if (op == 0) {
+            red[0] = fma(x[i], x[i], red[0]);
+        } else if (op == 1) {
+            x[i] = fma(coef, p[i], x[i]);
+            y[i] = fma(-coef, t[i], y[i]);
+        } else {
+            x[i] = fma(coef, x[i], p[i]);   // x = p (the new r) + beta x
+        }
+    }
+    if (op == 0) block_reduce_store<1, 0>(red, partials);
+}
+
+// max over all blocks and anchors of |(D x)_e| (padding anchors give exactly 0)
+template <int P, int ORD>
+__global__ __launch_bounds__(kThreads) void k_dmaxabs(Geom g, const double* __restrict__ x,
+                                                      double* __restrict__ partials) {
+    constexpr int NC = 1 << P;
+    double red[1] = {0.0};
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < g.N; i += gridDim.x * kThreads) {
+        uint32_t c[kMaxDims];
+        decode<P>(g, i, c);
+        double a[NC];
+#pragma unroll
+        for (int T = 0; T < NC; ++T) {
+            uint32_t idx = i;
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+                if ((T >> j) & 1) idx += (c[j] + 1 < g.m[j]) ? g.stride[j] : 0u;
+            a[T] = x[idx];
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int T = 0; T < NC; ++T)
+                if (!((T >> j) & 1)) a[T | (1 << j)] = a[T] - a[T | (1 << j)];
+        static_for<0, NC - 1>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+            if (k < g.nb) red[0] = fmax(red[0], fabs(g.w[k] * a[S]));
+        });
+    }
+    block_reduce_store<1, 1>(red, partials);
+}
+
 struct RedDims {
     uint64_t rd[kMaxDims];
     uint64_t stride[kMaxDims];
@@ -747,6 +799,21 @@ hipError_t launch_admm_control(hipStream_t s, AdmmCtl* ctl, const double* red) {
 hipError_t launch_maxabsdiff(const Geom& g, const Launch& L, const double* a, const double* b, double* partials) {
     klaunch(k_maxabsdiff, dim3(L.grid), dim3(kThreads), 0, L.stream, g.N, a, b, partials);
     return hipGetLastError();
+}
+
+hipError_t launch_cg_vec(const Geom& g, const Launch& L, int op, double coef, double* x, double* y, const double* p,
+                         const double* t, double* partials) {
+    klaunch(k_cg_vec, dim3(L.grid), dim3(kThreads), 0, L.stream, op, g.N, coef, x, y, p, t, partials);
+    return hipGetLastError();
+}
+
+hipError_t launch_dmaxabs(const Geom& g, int order, const Launch& L, const double* x, double* partials) {
+    return dispatch_p(g.p, [&](auto pc) {
+        constexpr int P = decltype(pc)::value;
+        if (order == 0) klaunch(k_dmaxabs<P, 0>, dim3(L.grid), dim3(kThreads), 0, L.stream, g, x, partials);
+        else klaunch(k_dmaxabs<P, 1>, dim3(L.grid), dim3(kThreads), 0, L.stream, g, x, partials);
+        return hipGetLastError();
+    });
 }
 
 hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n) {
