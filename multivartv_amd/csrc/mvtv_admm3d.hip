@@ -40,6 +40,7 @@ struct Edge3dArgs {
     const AdmmCtl* ctl;           // device scalars (asynchronous loop) or nullptr
     int tiles_x, tiles_y, zchunk, nblocks;
     int ty;                       // rows per tile (= waves per workgroup)
+    int zlo, zhi;                 // planes processed (g.ibeg / plane .. g.iend / plane)
 };
 
 // tile of this workgroup (XCD-aware: XCD b%8 gets a contiguous run of tiles)
@@ -57,8 +58,8 @@ __device__ __forceinline__ Tile3 tile3(const Edge3dArgs& a) {
     const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
     t.x = tx * e3d::TX + int(threadIdx.x & 63);
     t.y = ty * a.ty + int(threadIdx.x >> 6);
-    t.z0 = tz * a.zchunk;
-    t.z1 = min(int(a.g.m[2]), t.z0 + a.zchunk);
+    t.z0 = a.zlo + tz * a.zchunk;
+    t.z1 = min(a.zhi, t.z0 + a.zchunk);
     return t;
 }
 
@@ -240,6 +241,8 @@ Edge3dArgs e3d_args(const Geom& g) {
     Edge3dArgs a{};
     a.g = g;
     a.ty = e3d_rows();
+    a.zlo = int(g.ibeg / (g.m[0] * g.m[1]));
+    a.zhi = int(g.iend / (g.m[0] * g.m[1]));
     a.tiles_x = int((g.m[0] + e3d::TX - 1) / e3d::TX);
     a.tiles_y = int((g.m[1] + a.ty - 1) / a.ty);
     const int tiles = a.tiles_x * a.tiles_y;
@@ -249,10 +252,11 @@ Edge3dArgs e3d_args(const Geom& g) {
         const char* e = std::getenv("MVTV_E3D_WG");
         return e ? std::atoi(e) : 8192;
     }();
-    int nz = std::max(1, std::min(int(g.m[2]), want / std::max(1, tiles)));
+    const int nzp = std::max(1, a.zhi - a.zlo);
+    int nz = std::max(1, std::min(nzp, want / std::max(1, tiles)));
     while (nz > 1 && ((nz * tiles + 7) / 8 * 8) > kMaxCgBlocks) --nz;
-    a.zchunk = (int(g.m[2]) + nz - 1) / nz;
-    nz = (int(g.m[2]) + a.zchunk - 1) / a.zchunk;
+    a.zchunk = (nzp + nz - 1) / nz;
+    nz = (nzp + a.zchunk - 1) / a.zchunk;
     a.nblocks = tiles * nz;
     return a;
 }

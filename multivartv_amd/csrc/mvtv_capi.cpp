@@ -84,6 +84,14 @@ struct mvtv_problem {
     AdmmCtl* host_ctl = nullptr;  // pinned mirror
     int admm_hint = 0;            // ADMM iterations of the last converged run (enqueue-ahead depth)
 
+    // slab decomposition (mvtv_problem_create_slab): this problem holds planes [zb, ze) of dim p-1
+    // of a mesh with m_global planes, plus ghost planes below / above
+    bool slab = false;
+    int64_t m_global = 0, zb = 0, ze = 0;
+    int g_lo = 0, g_hi = 0;
+    double* scratch = nullptr;
+    size_t scratch_n = 0;
+
     // resident ADMM state
     bool have_state = false;
     bool u_default = true;
@@ -165,7 +173,7 @@ mvtv_status alloc(double** ptr, size_t n) {
 
 void free_all(mvtv_problem* P) {
     double** bufs[] = {&P->oty, &P->wdiag, &P->theta, &P->edges, &P->ga, &P->gu, &P->guprev, &P->r,
-                       &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage};
+                       &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->scratch};
     for (double** b : bufs)
         if (*b) {
             (void)hipFree(*b);
@@ -321,7 +329,7 @@ mvtv_status spectral_plan(mvtv_problem* P) {
     SpecPlan& sp = P->spec;
     const long double pi = 3.141592653589793238462643383279502884L;
     for (int j = 0; j < P->g.p; ++j) {
-        const uint32_t m = P->g.m[j];
+        const uint32_t m = (P->slab && j == P->g.p - 1) ? uint32_t(P->m_global) : P->g.m[j];
         sp.tw_off[j] = uint32_t(tw.size());
         sp.twq_off[j] = uint32_t(twq.size());
         sp.lam_off[j] = uint32_t(lam.size());
@@ -415,7 +423,10 @@ void mvtv_default_opts(mvtv_admm_opts* o, int32_t variant) {
     o->ymean = 0.0;
 }
 
-mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) {
+}  // extern "C"
+
+namespace {
+mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc* sl, mvtv_problem** out) {
     if (!d || !out) return fail(MVTV_BAD_ARG, "null descriptor/output");
     *out = nullptr;
     if (d->p < 1 || d->p > MVTV_MAX_DIMS) return fail(MVTV_BAD_ARG, "p must be in 1..4");
@@ -423,8 +434,22 @@ mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) 
     if (d->block_order != MVTV_ORDER_CPP && d->block_order != MVTV_ORDER_PY) return fail(MVTV_BAD_ARG, "block_order");
     const int p = d->p;
     uint64_t N = 1;
+    // slab: the mesh is validated (and D built) with the global extent of dim p-1
+    int64_t mg[MVTV_MAX_DIMS];
+    for (int j = 0; j < MVTV_MAX_DIMS; ++j) mg[j] = d->m[j];
+    if (sl) {
+        if (p < 2) return fail(MVTV_BAD_ARG, "slab decomposition needs p >= 2");
+        if (sl->z_begin < 0 || sl->z_end <= sl->z_begin || sl->z_end > sl->m_global)
+            return fail(MVTV_BAD_ARG, "slab plane range");
+        if ((sl->ghost_lo != 0) != (sl->z_begin > 0) || (sl->ghost_hi != 0) != (sl->z_end < sl->m_global))
+            return fail(MVTV_BAD_ARG, "slab ghosts: one plane below unless z_begin = 0, one above unless z_end = m");
+        if (d->m[p - 1] != sl->z_end - sl->z_begin + (sl->ghost_lo ? 1 : 0) + (sl->ghost_hi ? 1 : 0))
+            return fail(MVTV_BAD_ARG, "local m[p-1] must be owned planes + ghosts");
+        mg[p - 1] = sl->m_global;
+    }
     for (int j = 0; j < p; ++j) {
-        if (d->m[j] < 2) return fail(MVTV_BAD_ARG, "every m_j must be >= 2");
+        if (d->m[j] < 2 && !(sl && j == p - 1)) return fail(MVTV_BAD_ARG, "every m_j must be >= 2");
+        if (mg[j] < 2) return fail(MVTV_BAD_ARG, "every m_j must be >= 2");
         N *= uint64_t(d->m[j]);
     }
     if (N >= (uint64_t(1) << 31)) return fail(MVTV_BAD_ARG, "N >= 2^31 nodes on one GPU");
@@ -466,7 +491,7 @@ mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) 
         if (popcount(nominal) >= 2 && !(nominal & 1)) {
             int lo = 0;
             while (!((nominal >> lo) & 1)) ++lo;
-            if (d->m[0] != d->m[lo]) {
+            if (mg[0] != mg[lo]) {
                 delete P;
                 return fail(MVTV_DIM_MISMATCH, "mixed partial of block " + std::to_string(b) +
                                                    ": m[0] != m[" + std::to_string(lo) + "]");
@@ -486,6 +511,19 @@ mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) 
         P->E += int64_t(len);
     }
     for (int k = nb; k < kMaxBlocks; ++k) g.w[k] = 0.0;
+    g.ibeg = 0;
+    g.iend = uint32_t(N);
+    if (sl) {
+        const uint32_t plane = uint32_t(N / uint64_t(d->m[p - 1]));
+        P->slab = true;
+        P->m_global = sl->m_global;
+        P->zb = sl->z_begin;
+        P->ze = sl->z_end;
+        P->g_lo = sl->ghost_lo ? 1 : 0;
+        P->g_hi = sl->ghost_hi ? 1 : 0;
+        g.ibeg = uint32_t(P->g_lo) * plane;
+        g.iend = uint32_t(N) - uint32_t(P->g_hi) * plane;
+    }
     P->grid = int(std::min<uint64_t>((N + kThreads - 1) / kThreads, kMaxGrid));
     if (const char* env = std::getenv("MVTV_PCG")) P->fused3d = std::strcmp(env, "classic") != 0;
 
@@ -524,7 +562,7 @@ mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) 
     P->host_st = reinterpret_cast<PcgState*>(P->host_red + 16);
     P->spec_mesh = true;
     for (int j = 0; j < p; ++j) {
-        const uint32_t mj = g.m[j];
+        const uint32_t mj = uint32_t(mg[j]);
         if ((mj & (mj - 1)) != 0 || mj > 4096) P->spec_mesh = false;
     }
     if (P->spec_mesh) s = spectral_plan(P);
@@ -537,6 +575,18 @@ mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) 
     }
     *out = P;
     return MVTV_OK;
+}
+}  // namespace
+
+extern "C" {
+
+mvtv_status mvtv_problem_create(const mvtv_problem_desc* d, mvtv_problem** out) {
+    return problem_create_impl(d, nullptr, out);
+}
+
+mvtv_status mvtv_problem_create_slab(const mvtv_problem_desc* d, const mvtv_slab_desc* slab, mvtv_problem** out) {
+    if (!slab) return fail(MVTV_BAD_ARG, "null slab descriptor");
+    return problem_create_impl(d, slab, out);
 }
 
 void mvtv_problem_destroy(mvtv_problem* P) {
@@ -1131,6 +1181,191 @@ mvtv_status mvtv_solve_spectral(mvtv_problem* P, double sigma, const double* b, 
         s = fail(MVTV_HIP_ERROR, "solve download");
     (void)hipFree(dx);
     return s;
+}
+
+// ------------------------------------------------------------------------------ slab decomposition
+}  // extern "C"
+namespace {
+mvtv_status slab_check(mvtv_problem* P) {
+    if (!P) return fail(MVTV_BAD_ARG, "null problem");
+    if (!P->slab) return fail(MVTV_BAD_ARG, "not a slab problem (mvtv_problem_create_slab)");
+    return MVTV_OK;
+}
+// geometry of the owned planes only (spectral passes along dims 0..p-2)
+Geom owned_geom(const mvtv_problem* P, size_t* off) {
+    Geom g = P->g;
+    const int p = g.p;
+    const uint32_t plane = g.N / g.m[p - 1];
+    const uint32_t nz = uint32_t(P->ze - P->zb);
+    g.m[p - 1] = nz;
+    g.N = plane * nz;
+    g.ibeg = 0;
+    g.iend = g.N;
+    if (off) *off = size_t(P->g_lo) * plane;
+    return g;
+}
+}  // namespace
+extern "C" {
+
+mvtv_status mvtv_slab_solve_fwd(mvtv_problem* P, double ca, double cb, double sigma) {
+    MVTV_TRY(slab_check(P));
+    if (!P->spec_mesh) return fail(MVTV_BAD_ARG, "slab solve needs power-of-two m_j <= 4096");
+    DeviceGuard dg(P->device);
+    size_t off = 0;
+    const Geom g = owned_geom(P, &off);
+    for (int d = 0; d < g.p - 1; ++d) {
+        const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
+        if (d == 0)
+            HIP_TRY(launch_dct_pass(P->spec, g, P->stream, 0, 0, P->oty + off, P->ga + off, ca, P->guprev + off, cb,
+                                    P->theta + off, sigma, 1.0));
+        else
+            HIP_TRY(launch_dct_pass(P->spec, g, P->stream, 0, d, P->theta + off, nullptr, 0.0, nullptr, 0.0,
+                                    P->theta + off, sigma, 1.0));
+        P->tstop(h);
+    }
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_slab_solve_mid(mvtv_problem* P, double* lines, int64_t q0, int64_t nq, double sigma) {
+    MVTV_TRY(slab_check(P));
+    if (!lines || nq <= 0 || q0 < 0) return fail(MVTV_BAD_ARG, "line chunk");
+    if ((nq & (nq - 1)) != 0) return fail(MVTV_BAD_ARG, "line chunk must be a power of two");
+    DeviceGuard dg(P->device);
+    Geom g = P->g;
+    const int p = g.p;
+    const uint32_t lines_total = g.N / g.m[p - 1];
+    if (uint64_t(q0) + uint64_t(nq) > lines_total) return fail(MVTV_BAD_ARG, "line chunk out of range");
+    // the chunk as a mesh: nq lines of m_global points, line index fastest (stride nq)
+    g.m[p - 1] = uint32_t(P->m_global);
+    g.stride[p - 1] = uint32_t(nq);
+    g.N = uint32_t(nq) * uint32_t(P->m_global);
+    const int h = P->tstart(MVTV_K_DCT);
+    const double inv_n = 1.0 / (double(lines_total) * double(P->m_global));
+    HIP_TRY(launch_dct_pass(P->spec, g, P->stream, 2, p - 1, lines, nullptr, 0.0, nullptr, 0.0, lines, sigma, 1.0,
+                            nullptr, uint32_t(q0), inv_n));
+    P->tstop(h);
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_slab_solve_inv(mvtv_problem* P) {
+    MVTV_TRY(slab_check(P));
+    DeviceGuard dg(P->device);
+    size_t off = 0;
+    const Geom g = owned_geom(P, &off);
+    for (int d = g.p - 2; d >= 0; --d) {
+        const int h = P->tstart(MVTV_K_DCT);
+        HIP_TRY(launch_dct_pass(P->spec, g, P->stream, 1, d, P->theta + off, nullptr, 0.0, nullptr, 0.0, P->theta + off,
+                                0.0, 1.0));
+        P->tstop(h);
+    }
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_slab_init(mvtv_problem* P) {
+    MVTV_TRY(slab_check(P));
+    DeviceGuard dg(P->device);
+    const Launch L = P->L();
+    // g_alpha = D^T D theta0 (needs both theta ghost planes); the owned planes are what is used
+    HIP_TRY(launch_apply_A(P->g, L, 1.0, W_NONE, nullptr, P->theta, P->ga, nullptr, nullptr));
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_slab_edge(mvtv_problem* P, int32_t umode, double t_old, double c_old, double t_new, double* red4) {
+    MVTV_TRY(slab_check(P));
+    DeviceGuard dg(P->device);
+    const Launch L = P->L();
+    int np = L.grid;
+    const int h = P->tstart(MVTV_K_EDGE_UPDATE);
+    if (P->e3d)
+        HIP_TRY(launch_edge3d(P->g, P->order, umode, P->stream, P->theta, P->edges, t_old, c_old, t_new, nullptr,
+                              P->partials, &np));
+    else
+        HIP_TRY(launch_edge_update(P->g, P->order, umode, L, P->theta, P->edges, t_old, c_old, t_new, nullptr,
+                                   P->partials));
+    P->tstop(h);
+    HIP_TRY(launch_finalize(P->stream, P->partials, np, ER_N, 1, 0, P->red, P->st));
+    HIP_TRY(hipMemcpyAsync(P->host_red, P->red, ER_N * sizeof(double), hipMemcpyDeviceToHost, P->stream));
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    if (red4)
+        for (int k = 0; k < ER_N; ++k) red4[k] = P->host_red[k];
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_slab_gather(mvtv_problem* P, int32_t umode, double t, double c_prev, double* red3) {
+    MVTV_TRY(slab_check(P));
+    DeviceGuard dg(P->device);
+    const Launch L = P->L();
+    int np = L.grid;
+    const bool expl = umode == U_EXPLICIT;
+    // explicit: P->guprev = D^T u; from z: P->gu = D^T u_new (with the dual residual against P->guprev), then swap
+    double* gout = expl ? P->guprev : P->gu;
+    const double* gprev = expl ? nullptr : P->guprev;
+    const int h = P->tstart(MVTV_K_GATHER);
+    if (P->e3d)
+        HIP_TRY(launch_gather3d(P->g, P->order, umode, P->stream, P->edges, t, expl ? nullptr : P->ga, gout, gprev,
+                                c_prev, P->partials, &np));
+    else
+        HIP_TRY(launch_gather(P->g, P->order, umode, L, P->edges, t, expl ? nullptr : P->ga, gout, gprev, c_prev,
+                              P->partials));
+    P->tstop(h);
+    HIP_TRY(launch_finalize(P->stream, P->partials, np, GR_N, 0, 0, P->red, P->st));
+    HIP_TRY(hipMemcpyAsync(P->host_red, P->red, GR_N * sizeof(double), hipMemcpyDeviceToHost, P->stream));
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    if (red3)
+        for (int k = 0; k < GR_N; ++k) red3[k] = P->host_red[k];
+    if (!expl) std::swap(P->guprev, P->gu);
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_copy2d(mvtv_problem* P, int32_t what, int64_t offset, int64_t rows, int64_t width, int64_t lib_pitch,
+                        int64_t ext_pitch, void* ext, int32_t to_ext) {
+    if (!P || !ext || rows < 0 || width < 0) return fail(MVTV_BAD_ARG, "null argument");
+    DeviceGuard dg(P->device);
+    double* base = nullptr;
+    size_t cap = 0;
+    switch (what) {
+        case MVTV_BUF_THETA: base = P->theta; cap = P->g.N; break;
+        case MVTV_BUF_EDGES: base = P->edges; cap = size_t(P->g.nb) * P->g.N; break;
+        case MVTV_BUF_SCRATCH: base = P->scratch; cap = P->scratch_n; break;
+        default: return fail(MVTV_BAD_ARG, "buffer id");
+    }
+    if (rows == 0 || width == 0) return MVTV_OK;
+    if (!base || offset < 0 || lib_pitch < width || ext_pitch < width ||
+        uint64_t(offset) + uint64_t(rows - 1) * uint64_t(lib_pitch) + uint64_t(width) > cap)
+        return fail(MVTV_BAD_ARG, "copy out of range");
+    double* lib = base + offset;
+    const size_t w = size_t(width) * sizeof(double);
+    if (to_ext)
+        HIP_TRY(hipMemcpy2DAsync(ext, size_t(ext_pitch) * sizeof(double), lib, size_t(lib_pitch) * sizeof(double), w,
+                                 size_t(rows), hipMemcpyDefault, P->stream));
+    else
+        HIP_TRY(hipMemcpy2DAsync(lib, size_t(lib_pitch) * sizeof(double), ext, size_t(ext_pitch) * sizeof(double), w,
+                                 size_t(rows), hipMemcpyDefault, P->stream));
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    return MVTV_OK;
+}
+
+double* mvtv_scratch(mvtv_problem* P, int64_t n) {
+    if (!P || n <= 0) return nullptr;
+    DeviceGuard dg(P->device);
+    if (P->scratch_n < size_t(n)) {
+        if (P->scratch) (void)hipFree(P->scratch);
+        P->scratch = nullptr;
+        P->scratch_n = 0;
+        if (alloc(&P->scratch, size_t(n)) != MVTV_OK) return nullptr;
+        P->scratch_n = size_t(n);
+    }
+    return P->scratch;
+}
+
+mvtv_status mvtv_sync(mvtv_problem* P) {
+    if (!P) return fail(MVTV_BAD_ARG, "null problem");
+    DeviceGuard dg(P->device);
+    return P->sync();
 }
 
 // ------------------------------------------------------------------------------ instrumentation

@@ -64,6 +64,7 @@ struct Geom {
     FastDiv fd[kMaxDims - 1];  // division by m0, m1, m2
     double w[kMaxBlocks];      // block weights, in block order
     double cS[16];             // D^T D coefficient per subset mask S of dims
+    uint32_t ibeg, iend;       // nodes the edge kernels update and reduce over (slab: owned planes)
 };
 
 // Per-node multi-index decode (column-major, dim 0 fastest).
@@ -197,7 +198,7 @@ struct SpecPlan {
 // ga != nullptr forms the input as in + ca*ga + cb*gb. In place (in == out) is allowed.
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
-                           double w0, const AdmmCtl* ctl = nullptr);
+                           double w0, const AdmmCtl* ctl = nullptr, uint32_t q_off = 0, double inv_n = 0.0);
 // z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /
 // launch_gather, *nparts workgroup rows
 bool edge3d_ok(const Geom& g);

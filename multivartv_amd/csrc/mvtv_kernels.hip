@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kThreads) void k_edge_update(Geom g, const double* 
         t_new = ctl->t_next;
     }
     double red[ER_N] = {0.0, 0.0, 0.0, 0.0};
-    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < g.N; i += gridDim.x * kThreads) {
+    for (uint32_t i = g.ibeg + blockIdx.x * kThreads + threadIdx.x; i < g.iend; i += gridDim.x * kThreads) {
         uint32_t c[kMaxDims];
         decode<P>(g, i, c);
         double a[NC];
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kThreads) void k_gather(Geom g, const double* __res
         c_prev = ctl->c_prev;
     }
     double red[GR_N] = {0.0, 0.0, 0.0};
-    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < g.N; i += gridDim.x * kThreads) {
+    for (uint32_t i = g.ibeg + blockIdx.x * kThreads + threadIdx.x; i < g.iend; i += gridDim.x * kThreads) {
         uint32_t c[kMaxDims];
         decode<P>(g, i, c);
         double ga = 0.0, gu = 0.0;

@@ -65,6 +65,7 @@ struct SpecArgs {
     uint32_t nlines;         // N / m
     int32_t d, p, L, tq;     // line dimension, dims, log2 m, lines per workgroup
     int32_t ls;              // log2 stride
+    uint32_t q_off;          // MID: global index of line 0 (slab-decomposed solve works on a line chunk)
     const AdmmCtl* ctl;      // asynchronous ADMM loop: sigma, ca = rho, cb = rho c_prev from the device
 };
 
@@ -202,9 +203,9 @@ __global__ __launch_bounds__(spec::NT) void k_dct(const SpecArgs a) {
 
     if (MODE == SPEC_MID && threadIdx.x < uint32_t(tq)) {
         // line q indexes dims 0..p-2 column-major (d = p - 1): split mu into c0 + c1 * lam_d(k)
-        const uint32_t q = q0 + threadIdx.x;
+        const uint32_t q = a.q_off + q0 + threadIdx.x;
         double lamv[kMaxDims] = {0, 0, 0, 0};
-        uint32_t rest = q < a.nlines ? q : 0u;
+        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
         for (int j = 0; j < a.p - 1; ++j) {
             const uint32_t qq = (j < a.p - 2) ? a.fd[j].div(rest) : 0u;
             const uint32_t c = rest - qq * a.m[j];
@@ -501,9 +502,9 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
     const double2* __restrict__ tw = a.tw;
 
     for (int l = t; MODE == SPEC_MID && l < a.tq; l += S::NT) {
-        const uint32_t q = q0 + l;
+        const uint32_t q = a.q_off + q0 + l;
         double lamv[kMaxDims] = {0, 0, 0, 0};
-        uint32_t rest = q < a.nlines ? q : 0u;
+        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
         for (int jj = 0; jj < a.p - 1; ++jj) {
             const uint32_t qq = (jj < a.p - 2) ? a.fd[jj].div(rest) : 0u;
             lamv[jj] = a.lam[a.lam_off[jj] + (rest - qq * a.m[jj])];
@@ -720,9 +721,10 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
 
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
-                           double w0, const AdmmCtl* ctl) {
+                           double w0, const AdmmCtl* ctl, uint32_t q_off, double inv_n) {
     SpecArgs a{};
     a.ctl = ctl;
+    a.q_off = q_off;
     a.in = in;
     a.ga = ga;
     a.gb = gb;
@@ -740,7 +742,7 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     for (int S = 0; S < 16; ++S) a.cS[S] = g.cS[S];
     a.sigma = sigma;
     a.w0 = w0;
-    a.inv_n = 1.0 / double(g.N);
+    a.inv_n = inv_n > 0.0 ? inv_n : 1.0 / double(g.N);   // 1 / (all mesh points): the inverse transforms' scale
     a.stride = g.stride[d];
     a.ls = 0;
     while ((1u << a.ls) < a.stride) ++a.ls;

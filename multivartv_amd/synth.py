@@ -54,21 +54,24 @@ def lattice_coords(m) -> list[np.ndarray]:
     return [np.arange(mj, dtype=np.float64) / max(mj - 1, 1) for mj in m]
 
 
-def towers(m, sigma: float = 0.5, seed: int = SEED, chunk: int = 1 << 22, threads: int = 0) -> np.ndarray:
-    """y = towers(x) + sigma * xi on the column-major lattice of shape m (float64, length prod(m)).
+def towers(m, sigma: float = 0.5, seed: int = SEED, chunk: int = 1 << 22, threads: int = 0, start: int = 0,
+           count: int | None = None) -> np.ndarray:
+    """y = towers(x) + sigma * xi on the column-major lattice of shape m (float64, length prod(m)),
+    or its flat index range [start, start + count) (a slab of planes of a decomposed mesh).
 
     Chunks are independent (counter-based noise), so large meshes are generated on a
     thread pool; the result does not depend on ``threads``.
     """
     m = [int(v) for v in m]
-    n = int(np.prod(m))
+    off = int(start)
+    n = int(np.prod(m)) - off if count is None else int(count)
     y = np.empty(n, dtype=np.float64)
     coords = lattice_coords(m)
     strides = np.cumprod([1] + m[:-1])
 
     def work(start):
         cnt = min(chunk, n - start)
-        flat = np.arange(start, start + cnt, dtype=np.int64)
+        flat = np.arange(off + start, off + start + cnt, dtype=np.int64)
         hi = np.ones(cnt, dtype=bool)
         lo = np.ones(cnt, dtype=bool)
         for j, mj in enumerate(m):
@@ -76,7 +79,7 @@ def towers(m, sigma: float = 0.5, seed: int = SEED, chunk: int = 1 << 22, thread
             hi &= xj > 0.8
             lo &= xj < 0.2
         f = np.where(hi, 1.0, np.where(lo, 0.5, 0.0))
-        y[start:start + cnt] = f + sigma * normal_noise(start, cnt, seed)
+        y[start:start + cnt] = f + sigma * normal_noise(off + start, cnt, seed)
 
     starts = range(0, n, chunk)
     nthreads = threads or min(16, os.cpu_count() or 1)
