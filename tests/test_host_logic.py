@@ -57,3 +57,20 @@ def test_fastdiv_formula():
         hi = (n * np.uint64(mul)) >> np.uint64(32)
         q = (hi + n) >> np.uint64(shift)
         np.testing.assert_array_equal(q, n // np.uint64(d))
+
+
+def test_slab_plane_bounds():
+    from multivartv_amd import slab
+    b = slab.plane_bounds(512, 8)
+    assert b[0] == 0 and b[-1] == 512 and np.all(np.diff(b) == 64)
+    b = slab.plane_bounds(10, 4)
+    assert b[0] == 0 and b[-1] == 10 and np.all(np.diff(b) >= 2)
+    with pytest.raises(ValueError):
+        slab.plane_bounds(3, 4)
+
+
+def test_slab_desc_layout_matches_header():
+    import ctypes
+    from multivartv_amd import slab
+    assert ctypes.sizeof(slab.SlabDesc) == 32          # int64 x3 + int32 x2 (include/mvtv/mvtv.h)
+    assert [f[0] for f in slab.SlabDesc._fields_] == ["m_global", "z_begin", "z_end", "ghost_lo", "ghost_hi"]
