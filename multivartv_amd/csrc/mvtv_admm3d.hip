@@ -346,4 +346,320 @@ hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, c
     return pick(std::integral_constant<int, 256>{});
 }
 
+// =============================================================================================
+// k_admm3d: edge update and D^T gather in ONE pass (the z state is read once and written once).
+//
+// The gather at (x,y,e) needs z_new at the in-plane backward neighbours (x-1, y), (x, y-1),
+// (x-1, y-1) of plane e, which other threads produce in the same step, so a workgroup stages
+// z_new of one plane in LDS. Its image is 64 x 16 cells with lane 0 on x = X0-1 and row 0 on
+// y = Y0-1: those halo cells recompute the neighbour tile's z_new (never stored) so the gather
+// of the 63 x 15 interior is complete. z_new goes to a second edge buffer (ping-pong), so a
+// halo or a chunk-start recompute always reads the previous iterate, never a value another
+// workgroup has already overwritten. The dim-2 backward corners come from the carried
+// in-plane sums of the previous plane (as in k_gather3d), so no plane is ever re-read.
+namespace f3d {
+constexpr int IW = 64, TX = IW - 1;
+int rows();   // image rows per workgroup (8, or 16 with MVTV_F3D_IH=16; 8 measured 2-3 % faster)
+}
+
+struct Fused3dArgs {
+    Geom g;
+    const double* theta;
+    const double* z_old;
+    double* z_new;
+    const double* theta_old;
+    double* g_alpha;
+    double* g_u;
+    const double* g_uprev;
+    double* partials;
+    double t_old, c_old, t_new, c_prev;
+    const AdmmCtl* ctl;
+    int tiles_x, tiles_y, zchunk, nblocks, zlo, zhi;
+};
+
+// partials: |r|^2, |D theta|^2, |alpha|^2, max dtheta, |g_u|^2, |s_B|^2, |s_A|^2 (max slot 3)
+template <int ORD, int UM, bool DTH, int NB, int IH>
+__global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
+    constexpr int P = 3, NC = 8;
+    constexpr int IW = f3d::IW, TX = f3d::TX, TY = IH - 1, NT = IW * IH;
+    const Geom& g = a.g;
+    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new, c_prev = a.c_prev;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        t_old = a.ctl->t_z;
+        c_old = a.ctl->c_prev;
+        t_new = a.ctl->t_next;
+        c_prev = a.ctl->c_prev;
+    }
+    __shared__ double sz[2][NB][IH][IW];
+    double red[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const bool valid = bid < a.nblocks;
+    if (valid) {
+        const int nt = a.tiles_x * a.tiles_y;
+        const int tz = bid / nt, rem = bid - tz * nt;
+        const int tyi = rem / a.tiles_x, txi = rem - tyi * a.tiles_x;
+        const int lane = int(threadIdx.x & 63), row = int(threadIdx.x >> 6);
+        const int x = txi * TX - 1 + lane, y = tyi * TY - 1 + row;
+        const int z0 = a.zlo + tz * a.zchunk, z1 = min(a.zhi, z0 + a.zchunk);
+        const int m0 = int(g.m[0]), m1 = int(g.m[1]), m2 = int(g.m[2]);
+        const bool cell = x >= 0 && y >= 0 && x < m0 && y < m1;     // computes z_new here
+        const bool inner = cell && lane > 0 && row > 0;              // owns outputs here
+        const uint32_t pl = uint32_t(m0) * uint32_t(m1);
+        const int xc = min(max(x, 0), m0 - 1), yc = min(max(y, 0), m1 - 1);
+        const uint32_t xo[2] = {uint32_t(xc), uint32_t(min(xc + 1, m0 - 1))};
+        const uint32_t yo[2] = {uint32_t(yc) * uint32_t(m0), uint32_t(min(yc + 1, m1 - 1)) * uint32_t(m0)};
+        const uint32_t ixy = yo[0] + xo[0];
+        const bool okx = x > 0, oky = y > 0;
+
+        // loads of one step: theta at plane e+1, z_old and g_uprev at plane e (issued a step ahead)
+        auto load_theta = [&](double (&th)[4], int e) {
+            const uint32_t zo = uint32_t(e) * pl;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) th[q] = cell ? a.theta[zo + yo[q >> 1] + xo[q & 1]] : 0.0;
+        };
+        auto load_z = [&](double (&zo)[NB], int e) {
+            const uint32_t i = uint32_t(e) * pl + ixy;
+#pragma unroll
+            for (int k = 0; k < NB; ++k) zo[k] = cell ? __builtin_nontemporal_load(a.z_old + uint64_t(k) * g.N + i) : 0.0;
+        };
+        // z_new of this cell at plane e from theta planes e (th0), e+1 (th1) and the old z
+        auto edge_cell = [&](int e, const double (&th0)[4], const double (&th1)[4], const double (&zo)[NB],
+                             double (&zn)[NB], bool own) {
+            const uint32_t i = uint32_t(e) * pl + ixy;
+            double v[NC];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                v[q] = th0[q];
+                v[q | 4] = th1[q];
+            }
+            if constexpr (DTH)
+                if (own) red[3] = fmax(red[3], fabs(v[0] - a.theta_old[i]));
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+#pragma unroll
+                for (int q = 0; q < NC; ++q)
+                    if (!((q >> j) & 1)) v[q | (1 << j)] = v[q] - v[q | (1 << j)];
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                const double d = g.w[k] * v[S];
+                const double uo = (UM == U_EXPLICIT) ? zo[k] : -c_old * clampd(zo[k], t_old);
+                const double z = cell ? d - uo : 0.0;
+                zn[k] = z;
+                if (own) {
+                    const double al = z - clampd(z, t_new);
+                    const double r = al - d;
+                    __builtin_nontemporal_store(z, a.z_new + uint64_t(k) * g.N + i);
+                    red[0] = fma(r, r, red[0]);
+                    red[1] = fma(d, d, red[1]);
+                    red[2] = fma(al, al, red[2]);
+                }
+            });
+        };
+        // in-plane backward sums Q_k of this (interior) cell from the LDS image of plane e
+        auto plane_q = [&](auto kc, int buf, double& qa, double& qu) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+            constexpr int SI = S & 3;
+            qa = 0.0;
+            qu = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if ((q & ~SI) != 0) continue;
+                const bool ok = (!(q & 1) || okx) && (!(q & 2) || oky);
+                const double v = ok ? sz[buf][k][row - ((q >> 1) & 1)][lane - (q & 1)] : 0.0;
+                const bool neg = __builtin_popcount(q) & 1;
+                const double cl = clampd(v, t_new);
+                const double al = v - cl;
+                qa = neg ? qa - al : qa + al;
+                qu = neg ? qu + cl : qu - cl;   // u = -clamp
+            }
+        };
+        double qa_prev[NB], qu_prev[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) qa_prev[k] = qu_prev[k] = 0.0;
+
+        double th0[4], th1[4], zo[NB], zn[NB];
+        if (z0 > 0) {   // carried sums of plane z0 - 1: recompute its z_new from the old state
+            load_theta(th0, z0 - 1);
+            load_theta(th1, z0);
+            load_z(zo, z0 - 1);
+            edge_cell(z0 - 1, th0, th1, zo, zn, false);
+#pragma unroll
+            for (int k = 0; k < NB; ++k) sz[1][k][row][lane] = zn[k];
+            lds_barrier();
+            if (inner) {
+                static_for<0, NB>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                    if constexpr ((S & 4) != 0) plane_q(kc, 1, qa_prev[k], qu_prev[k]);
+                });
+            }
+            lds_barrier();
+        }
+        load_theta(th0, z0);
+        load_theta(th1, min(z0 + 1, m2 - 1));
+        load_z(zo, z0);
+        double gp = inner ? __builtin_nontemporal_load(a.g_uprev + uint32_t(z0) * pl + ixy) : 0.0;
+        for (int e = z0; e < z1; ++e) {
+            const int buf = (e - z0) & 1;
+            edge_cell(e, th0, th1, zo, zn, inner);
+#pragma unroll
+            for (int k = 0; k < NB; ++k) sz[buf][k][row][lane] = zn[k];
+            // prefetch step e+1 while this step's gather runs
+            double nth[4], nzo[NB], ngp = 0.0;
+            if (e + 1 < z1) {
+                load_theta(nth, min(e + 2, m2 - 1));
+                load_z(nzo, e + 1);
+                ngp = inner ? __builtin_nontemporal_load(a.g_uprev + uint32_t(e + 1) * pl + ixy) : 0.0;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) nth[q] = 0.0;
+#pragma unroll
+                for (int k = 0; k < NB; ++k) nzo[k] = 0.0;
+            }
+            lds_barrier();
+            if (inner) {
+                double ga = 0.0, gu = 0.0;
+                static_for<0, NB>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                    double qa, qu;
+                    plane_q(kc, buf, qa, qu);
+                    double ca = qa, cu = qu;
+                    if constexpr ((S & 4) != 0) {
+                        ca -= qa_prev[k];
+                        cu -= qu_prev[k];
+                        qa_prev[k] = qa;
+                        qu_prev[k] = qu;
+                    }
+                    ga = fma(g.w[k], ca, ga);
+                    gu = fma(g.w[k], cu, gu);
+                });
+                const uint32_t i = uint32_t(e) * pl + ixy;
+                __builtin_nontemporal_store(ga, a.g_alpha + i);
+                __builtin_nontemporal_store(gu, a.g_u + i);
+                const double gpc = c_prev * gp;
+                const double db = gu - gpc, da = ga + gpc;
+                red[4] = fma(gu, gu, red[4]);
+                red[5] = fma(db, db, red[5]);
+                red[6] = fma(da, da, red[6]);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                th0[q] = th1[q];
+                th1[q] = nth[q];
+            }
+#pragma unroll
+            for (int k = 0; k < NB; ++k) zo[k] = nzo[k];
+            gp = ngp;
+            // the buffer written next step is the other one; the one after waits for this barrier
+        }
+    }
+    // block reduction (max in slot 3)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const double o = __shfl_down(red[k], off, 64);
+            red[k] = k == 3 ? fmax(red[k], o) : red[k] + o;
+        }
+    }
+    __shared__ double rs[NT / 64][7];
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 7; ++k) rs[w][k] = valid ? red[k] : 0.0;
+    __syncthreads();
+    if (threadIdx.x < 7) {
+        const int k = threadIdx.x;
+        double acc = rs[0][k];
+        for (int ww = 1; ww < NT / 64; ++ww) acc = k == 3 ? fmax(acc, rs[ww][k]) : acc + rs[ww][k];
+        a.partials[blockIdx.x * 7 + k] = acc;
+    }
+}
+
+int f3d::rows() {
+    static const int ih = [] {
+        const char* e = std::getenv("MVTV_F3D_IH");
+        return (e && std::atoi(e) == 16) ? 16 : 8;
+    }();
+    return ih;
+}
+
+namespace {
+Fused3dArgs f3d_args(const Geom& g) {
+    Fused3dArgs a{};
+    a.g = g;
+    a.zlo = int(g.ibeg / (g.m[0] * g.m[1]));
+    a.zhi = int(g.iend / (g.m[0] * g.m[1]));
+    a.tiles_x = int((g.m[0] + f3d::TX - 1) / f3d::TX);
+    a.tiles_y = int((g.m[1] + (f3d::rows() - 1) - 1) / (f3d::rows() - 1));
+    const int tiles = a.tiles_x * a.tiles_y;
+    static const int want = [] {
+        const char* e = std::getenv("MVTV_F3D_WG");
+        return e ? std::atoi(e) : 4096;
+    }();
+    const int nzp = std::max(1, a.zhi - a.zlo);
+    int nz = std::max(1, std::min(nzp, want / std::max(1, tiles)));
+    while (nz > 1 && ((nz * tiles + 7) / 8 * 8) * 7 > kMaxCgBlocks * kMaxRed) --nz;
+    a.zchunk = (nzp + nz - 1) / nz;
+    nz = (nzp + a.zchunk - 1) / a.zchunk;
+    a.nblocks = tiles * nz;
+    return a;
+}
+}  // namespace
+
+bool fused3d_ok(const Geom& g) {
+    if (g.p != 3 || std::getenv("MVTV_F3D_OFF")) return false;
+    const Fused3dArgs a = f3d_args(g);
+    return ((a.nblocks + 7) / 8 * 8) * 7 <= kMaxCgBlocks * kMaxRed;
+}
+
+hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
+                         double* z_new, double t_old, double c_old, double t_new, double c_prev,
+                         const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
+                         double* partials, int* nparts, const AdmmCtl* ctl) {
+    Fused3dArgs a = f3d_args(g);
+    a.theta = theta;
+    a.z_old = z_old;
+    a.z_new = z_new;
+    a.theta_old = theta_old;
+    a.g_alpha = g_alpha;
+    a.g_u = g_u;
+    a.g_uprev = g_uprev;
+    a.partials = partials;
+    a.t_old = t_old;
+    a.c_old = c_old;
+    a.t_new = t_new;
+    a.c_prev = c_prev;
+    a.ctl = ctl;
+    const int grid = (a.nblocks + 7) / 8 * 8;
+    *nparts = grid;
+    const bool dth = theta_old != nullptr;
+    auto pick = [&](auto ihc) {
+        constexpr int IH = decltype(ihc)::value;
+        auto go = [&](auto kern) {
+            klaunch(kern, dim3(grid), dim3(f3d::IW * IH), 0, s, a);
+            return hipGetLastError();
+        };
+        if (order == 0) {
+            if (umode == U_EXPLICIT)
+                return dth ? go(k_admm3d<0, U_EXPLICIT, true, 7, IH>) : go(k_admm3d<0, U_EXPLICIT, false, 7, IH>);
+            return dth ? go(k_admm3d<0, U_FROM_Z, true, 7, IH>) : go(k_admm3d<0, U_FROM_Z, false, 7, IH>);
+        }
+        if (g.nb == 6) {
+            if (umode == U_EXPLICIT)
+                return dth ? go(k_admm3d<1, U_EXPLICIT, true, 6, IH>) : go(k_admm3d<1, U_EXPLICIT, false, 6, IH>);
+            return dth ? go(k_admm3d<1, U_FROM_Z, true, 6, IH>) : go(k_admm3d<1, U_FROM_Z, false, 6, IH>);
+        }
+        if (umode == U_EXPLICIT)
+            return dth ? go(k_admm3d<1, U_EXPLICIT, true, 7, IH>) : go(k_admm3d<1, U_EXPLICIT, false, 7, IH>);
+        return dth ? go(k_admm3d<1, U_FROM_Z, true, 7, IH>) : go(k_admm3d<1, U_FROM_Z, false, 7, IH>);
+    };
+    if (f3d::rows() == 8) return pick(std::integral_constant<int, 8>{});
+    return pick(std::integral_constant<int, 16>{});
+}
+
 }  // namespace mvtv

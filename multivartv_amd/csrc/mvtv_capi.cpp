@@ -80,6 +80,8 @@ struct mvtv_problem {
     SpecPlan spec;                // spectral theta-solve tables (allocated when the mesh allows it)
     bool spec_mesh = false;       // every m_j a power of two <= 4096
     bool e3d = false;             // z-marching 3-D edge kernels
+    bool f3d = false;             // fused 3-D edge update + gather (needs the second edge buffer)
+    double* edges2 = nullptr;     // ping-pong partner of edges for the fused kernel
     AdmmCtl* ctl = nullptr;       // device control block of the asynchronous ADMM loop
     AdmmCtl* host_ctl = nullptr;  // pinned mirror
     int admm_hint = 0;            // ADMM iterations of the last converged run (enqueue-ahead depth)
@@ -173,7 +175,8 @@ mvtv_status alloc(double** ptr, size_t n) {
 
 void free_all(mvtv_problem* P) {
     double** bufs[] = {&P->oty, &P->wdiag, &P->theta, &P->edges, &P->ga, &P->gu, &P->guprev, &P->r,
-                       &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->scratch};
+                       &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->scratch,
+                       &P->edges2};
     for (double** b : bufs)
         if (*b) {
             (void)hipFree(*b);
@@ -567,6 +570,7 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
     }
     if (P->spec_mesh) s = spectral_plan(P);
     P->e3d = edge3d_ok(g);
+    P->f3d = !sl && fused3d_ok(g);
     if (s == MVTV_OK) s = mvtv_problem_set_data(P, d->oty, d->wdiag);
     if (s != MVTV_OK) {
         free_all(P);
@@ -724,6 +728,8 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     int np = L.grid;
 
     const bool track_theta = variant != MVTV_VARIANT_RCPP;
+    const bool fused = P->f3d;
+    if (fused && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
     double dtheta = 0.0;
     if (track_theta) {
         if (!P->thold) MVTV_TRY(alloc(&P->thold, P->g.N));
@@ -762,6 +768,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         c.eps_dual = c.eps_pri = tol;
         HIP_TRY(hipMemcpyAsync(P->ctl, &c, sizeof(AdmmCtl), hipMemcpyHostToDevice, P->stream));
         double* gbuf[2] = {P->guprev, P->gu};
+        double* ebuf[2] = {P->edges, P->edges2};
         auto enqueue = [&](int j) -> mvtv_status {
             double* gp = gbuf[j & 1];
             double* gn = gbuf[(j + 1) & 1];
@@ -770,6 +777,20 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
                 HIP_TRY(hipMemcpyAsync(P->thold, P->theta, size_t(P->g.N) * sizeof(double), hipMemcpyDeviceToDevice,
                                        P->stream));
             MVTV_TRY(spectral_solve(P, sigma, P->oty, P->ga, rho, gp, rho, P->theta, P->ctl));
+            if (fused) {   // z ping-pongs between the two edge buffers
+                int hh = P->tstart(MVTV_K_ADMM_FUSED);
+                int npf = 0;
+                HIP_TRY(launch_admm3d(P->g, P->order, um, P->stream, P->theta, ebuf[j & 1], ebuf[(j + 1) & 1], 0.0, 1.0,
+                                      0.0, 1.0, track_theta ? P->thold : nullptr, P->ga, gn, gp, P->partials, &npf,
+                                      P->ctl));
+                P->tstop(hh);
+                hh = P->tstart(MVTV_K_REDUCE);
+                HIP_TRY(launch_finalize(P->stream, P->partials, npf, ER_N + GR_N, -(1 << ER_DTH), 0, P->red, P->st, 0.0,
+                                        0, P->ctl));
+                HIP_TRY(launch_admm_control(P->stream, P->ctl, P->red));
+                P->tstop(hh);
+                return MVTV_OK;
+            }
             int hh = P->tstart(MVTV_K_EDGE_UPDATE);
             int npe = L.grid;
             if (P->e3d)
@@ -818,6 +839,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         P->harvest();
         if (o.fixed_iters <= 0 && c.status == 0) P->admm_hint = it_done + 1;
         if (it_done & 1) std::swap(P->guprev, P->gu);   // P->guprev holds D^T u of the current state
+        if (fused && (it_done & 1)) std::swap(P->edges, P->edges2);
         if (it_done > 0) P->edge_mode = U_FROM_Z;
         if (it_done > 0) P->t_z = c.t_z;
         P->c_state = c.c_prev;
@@ -885,32 +907,45 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         }
         // ---- z-update (soft threshold) and dual update over all edges -----------------------
         const double t_new = rho != 0.0 ? lambda / rho : INFINITY;
-        h = P->tstart(MVTV_K_EDGE_UPDATE);
-        np = L.grid;
-        if (P->e3d)
-            HIP_TRY(launch_edge3d(P->g, P->order, mode, P->stream, P->theta, P->edges, t_z, c_prev, t_new,
-                                  track_theta ? P->thold : nullptr, P->partials, &np));
-        else
-            HIP_TRY(launch_edge_update(P->g, P->order, mode, L, P->theta, P->edges, t_z, c_prev, t_new,
-                                       track_theta ? P->thold : nullptr, P->partials));
-        P->tstop(h);
-        h = P->tstart(MVTV_K_REDUCE);
-        HIP_TRY(launch_finalize(P->stream, P->partials, np, ER_N, 1, 0, P->red, P->st));
-        P->tstop(h);
-        mode = U_FROM_Z;
-        t_z = t_new;
-        // ---- D^T alpha, D^T u and the dual residual norms ---------------------------------------
-        h = P->tstart(MVTV_K_GATHER);
-        np = L.grid;
-        if (P->e3d)
-            HIP_TRY(launch_gather3d(P->g, P->order, U_FROM_Z, P->stream, P->edges, t_z, P->ga, gnew, gprev, c_prev,
-                                    P->partials, &np));
-        else
-            HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, L, P->edges, t_z, P->ga, gnew, gprev, c_prev, P->partials));
-        P->tstop(h);
-        h = P->tstart(MVTV_K_REDUCE);
-        HIP_TRY(launch_finalize(P->stream, P->partials, np, GR_N, 0, 0, P->red + ER_N, P->st));
-        P->tstop(h);
+        if (fused) {   // edge update + gather in one pass, z ping-pongs between the edge buffers
+            h = P->tstart(MVTV_K_ADMM_FUSED);
+            HIP_TRY(launch_admm3d(P->g, P->order, mode, P->stream, P->theta, P->edges, P->edges2, t_z, c_prev, t_new,
+                                  c_prev, track_theta ? P->thold : nullptr, P->ga, gnew, gprev, P->partials, &np));
+            P->tstop(h);
+            std::swap(P->edges, P->edges2);
+            h = P->tstart(MVTV_K_REDUCE);
+            HIP_TRY(launch_finalize(P->stream, P->partials, np, ER_N + GR_N, -(1 << ER_DTH), 0, P->red, P->st));
+            P->tstop(h);
+            mode = U_FROM_Z;
+            t_z = t_new;
+        } else {
+            h = P->tstart(MVTV_K_EDGE_UPDATE);
+            np = L.grid;
+            if (P->e3d)
+                HIP_TRY(launch_edge3d(P->g, P->order, mode, P->stream, P->theta, P->edges, t_z, c_prev, t_new,
+                                      track_theta ? P->thold : nullptr, P->partials, &np));
+            else
+                HIP_TRY(launch_edge_update(P->g, P->order, mode, L, P->theta, P->edges, t_z, c_prev, t_new,
+                                           track_theta ? P->thold : nullptr, P->partials));
+            P->tstop(h);
+            h = P->tstart(MVTV_K_REDUCE);
+            HIP_TRY(launch_finalize(P->stream, P->partials, np, ER_N, 1, 0, P->red, P->st));
+            P->tstop(h);
+            mode = U_FROM_Z;
+            t_z = t_new;
+            // ---- D^T alpha, D^T u and the dual residual norms ---------------------------------------
+            h = P->tstart(MVTV_K_GATHER);
+            np = L.grid;
+            if (P->e3d)
+                HIP_TRY(launch_gather3d(P->g, P->order, U_FROM_Z, P->stream, P->edges, t_z, P->ga, gnew, gprev, c_prev,
+                                        P->partials, &np));
+            else
+                HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, L, P->edges, t_z, P->ga, gnew, gprev, c_prev, P->partials));
+            P->tstop(h);
+            h = P->tstart(MVTV_K_REDUCE);
+            HIP_TRY(launch_finalize(P->stream, P->partials, np, GR_N, 0, 0, P->red + ER_N, P->st));
+            P->tstop(h);
+        }
         HIP_TRY(hipMemcpyAsync(P->host_red, P->red, (ER_N + GR_N) * sizeof(double), hipMemcpyDeviceToHost, P->stream));
         HIP_TRY(hipStreamSynchronize(P->stream));   // timing events are harvested after the loop
         const double* R = P->host_red;
@@ -1400,6 +1435,7 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
         case MVTV_K_PCG_FUSED: b = 8.0 * ((6.0 + w) * N); break;        // x, r, p (+W) in, x, r, p out
         case MVTV_K_DCT_FIRST: b = 8.0 * 4.0 * N; break;                 // oty, g_alpha, g_u in, x out
         case MVTV_K_DCT: b = 8.0 * 2.0 * N; break;                       // x in, x out
+        case MVTV_K_ADMM_FUSED: b = 8.0 * (4.0 * N + 2.0 * E); break;    // theta, z, g_uprev in; z', g_alpha, g_u out
         default: b = 0.0;
     }
     if (total_ms) *total_ms = P->ms[kid];
@@ -1411,7 +1447,7 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
 const char* mvtv_kernel_name(int32_t kid) {
     static const char* names[MVTV_K_COUNT] = {"edge_update", "gather_Dt", "pcg_init", "pcg_apply_A",
                                                "pcg_update", "pcg_direction", "reduce", "other", "pcg_fused3d",
-                                               "dct_first", "dct"};
+                                               "dct_first", "dct", "admm_fused"};
     return (kid >= 0 && kid < MVTV_K_COUNT) ? names[kid] : "?";
 }
 

@@ -16,6 +16,14 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 __device__ __forceinline__ double clampd(double z, double t) { return fmin(fmax(z, -t), t); }
 
+// Workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding
+// global load (s_waitcnt vmcnt(0)), which would drain a prefetch issued before the barrier.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Wave (64-lane) shuffle reduction, then across the block's waves through LDS. The last NMAX
 // slots are max-reductions, the others sums. Thread 0 writes this block's partials.
 template <int NR, int NMAX, int NT = kThreads>

@@ -111,7 +111,7 @@ enum WMode { W_NONE = 0, W_IDENTITY = 1, W_DIAG = 2 };
 
 constexpr int kThreads = 256;
 constexpr int kMaxGrid = 2048;   // grid-stride cap for streaming kernels (8 workgroups per CU)
-constexpr int kMaxRed = 4;
+constexpr int kMaxRed = 8;
 constexpr int kMaxCgBlocks = 8192;   // workgroups of the fused 3-D PCG (partials buffer rows)
 
 // ------------------------------------------------------------------ launchers
@@ -158,7 +158,7 @@ hipError_t launch_pcg_update(const Geom& g, const Launch& L, double sigma, int w
                              double* partials);
 hipError_t launch_pcg_pupdate(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
                               const double* r, double* p, const PcgState* st);
-// op: 0 plain (sums, ER_DTH-style max in the last nmax slots), 1 pcg-init, 2 pcg-after-Ap, 3 pcg-after-update,
+// op: 0 plain (sums; max in the last nmax slots, or in the slots of bitmask -nmax when nmax < 0), 1 pcg-init, 2 pcg-after-Ap, 3 pcg-after-update,
 // 4 cg3d prologue, 5 cg3d iteration
 hipError_t launch_finalize(hipStream_t s, const double* partials, int nparts, int nr, int nmax, int op, double* out,
                            PcgState* st, double rtol2 = 0.0, int maxit = 0, const AdmmCtl* ctl = nullptr);
@@ -202,6 +202,13 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
 // z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /
 // launch_gather, *nparts workgroup rows
 bool edge3d_ok(const Geom& g);
+// fused edge update + D^T gather for p = 3 (one pass over the edge state, z ping-pong buffers);
+// partials: 7 per workgroup in the order ER_* then GR_* (slot ER_DTH is a max)
+bool fused3d_ok(const Geom& g);
+hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
+                         double* z_new, double t_old, double c_old, double t_new, double c_prev,
+                         const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
+                         double* partials, int* nparts, const AdmmCtl* ctl = nullptr);
 hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
                          double t_old, double c_old, double t_new, const double* theta_old, double* partials,
                          int* nparts, const AdmmCtl* ctl = nullptr);

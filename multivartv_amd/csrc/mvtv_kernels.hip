@@ -346,7 +346,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     __shared__ double sm[1024];
     __shared__ double res[kMaxRed];
     for (int k = 0; k < nr; ++k) {
-        const bool mx = k >= nr - nmax;
+        const bool mx = nmax >= 0 ? k >= nr - nmax : ((-nmax >> k) & 1) != 0;
         double acc = mx ? 0.0 : 0.0;
         for (int b = threadIdx.x; b < nparts; b += 1024) {
             const double v = partials[b * nr + k];
