@@ -421,7 +421,8 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
         auto load_z = [&](double (&zo)[NB], int e) {
             const uint32_t i = uint32_t(e) * pl + ixy;
 #pragma unroll
-            for (int k = 0; k < NB; ++k) zo[k] = cell ? __builtin_nontemporal_load(a.z_old + uint64_t(k) * g.N + i) : 0.0;
+            // cached loads: the halo cells of the neighbouring tiles read the same words (L2 hits)
+            for (int k = 0; k < NB; ++k) zo[k] = cell ? a.z_old[uint64_t(k) * g.N + i] : 0.0;
         };
         // z_new of this cell at plane e from theta planes e (th0), e+1 (th1) and the old z
         auto edge_cell = [&](int e, const double (&th0)[4], const double (&th1)[4], const double (&zo)[NB],

@@ -18,7 +18,9 @@ import re
 import sys
 from collections import defaultdict
 
-NAMES = {"k_cg3d": "pcg_fused3d", "k_edge_update": "edge_update", "k_gather": "gather_Dt",
+NAMES = {"k_admm3d": "admm_fused", "k_edge3d": "edge_update", "k_gather3d": "gather_Dt", "k_dct8": "dct",
+         "k_dct": "dct",
+         "k_cg3d": "pcg_fused3d", "k_edge_update": "edge_update", "k_gather": "gather_Dt",
          "k_apply_A": "pcg_apply_A", "k_pcg_update": "pcg_update", "k_pcg_pupdate": "pcg_direction",
          "k_pcg_init": "pcg_init", "copy8": "copy8", "copy16": "copy16"}
 
@@ -28,6 +30,8 @@ def short(kname: str) -> str:
         if re.search(r"\b" + k + r"\b", kname):
             if k == "k_cg3d" and re.search(r"k_cg3d<\d+, 0>", kname):
                 return "pcg_init"
+            if k in ("k_dct8", "k_dct") and re.search(r"k_dct8?<[^>]*true, true", kname):
+                return "dct_first"   # the pass that forms b on load (FORMB)
             return v
     return kname.split("(")[0]
 
