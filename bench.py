@@ -185,7 +185,7 @@ def main():
     t_setup = time.perf_counter()
     y = towers(m, seed=SEED + D.rank)
     deltas = [(1.0 + 2e-4) / v for v in m]
-    P = mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP, device=D.local)
+    P = mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP, device=D.local % max(1, mv.device_count()))
     P.state_set(np.full(y.size, y.mean()), None, lam / 5.0)
     ymean = float(y.mean())
     del y
