@@ -364,10 +364,22 @@ mvtv_status spectral_plan(mvtv_problem* P) {
 // last dim's forward/divide/inverse in one pass, inverse DCT along dims p-2..0. All in place on x.
 mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, const double* ga, double ca,
                            const double* gb, double cb, double* x, const AdmmCtl* ctl = nullptr) {
+    // pass order: forward along dims order[0..p-2], forward/divide/inverse along order[p-1], inverse
+    // back; the MID dimension defaults to p-1 (MVTV_DCT_MID selects another one for experiments)
     const int p = P->g.p;
-    for (int d = 0; d < p; ++d) {
-        const bool first = d == 0;
-        const int mode = d == p - 1 ? 2 : 0;
+    static const int mid_env = [] {
+        const char* e = std::getenv("MVTV_DCT_MID");
+        return e ? std::atoi(e) : -1;
+    }();
+    const int mid = (mid_env >= 1 && mid_env < p) ? mid_env : p - 1;
+    int order[MVTV_MAX_DIMS], n = 0;
+    for (int d = 0; d < p; ++d)
+        if (d != mid) order[n++] = d;
+    order[n++] = mid;
+    for (int t = 0; t < p; ++t) {
+        const int d = order[t];
+        const bool first = t == 0;
+        const int mode = t == p - 1 ? 2 : 0;
         const int h = P->tstart(first ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
         if (first && ga)   // b = oty + ca*ga + cb*gb formed on load
             HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, oty, ga, ca, gb ? gb : ga, gb ? cb : 0.0, x,
@@ -377,9 +389,10 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
                                     sigma, 1.0, ctl));
         P->tstop(h);
     }
-    for (int d = p - 2; d >= 0; --d) {
+    for (int t = p - 2; t >= 0; --t) {
         const int h = P->tstart(MVTV_K_DCT);
-        HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 1, d, x, nullptr, 0.0, nullptr, 0.0, x, sigma, 1.0, ctl));
+        HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 1, order[t], x, nullptr, 0.0, nullptr, 0.0, x, sigma, 1.0,
+                                ctl));
         P->tstop(h);
     }
     return MVTV_OK;

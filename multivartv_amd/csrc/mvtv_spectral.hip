@@ -206,8 +206,10 @@ __global__ __launch_bounds__(spec::NT) void k_dct(const SpecArgs a) {
         const uint32_t q = a.q_off + q0 + threadIdx.x;
         double lamv[kMaxDims] = {0, 0, 0, 0};
         uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
-        for (int j = 0; j < a.p - 1; ++j) {
-            const uint32_t qq = (j < a.p - 2) ? a.fd[j].div(rest) : 0u;
+        const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
+        for (int j = 0; j < a.p; ++j) {
+            if (j == a.d) continue;
+            const uint32_t qq = (j < jlast) ? a.fd[j].div(rest) : 0u;
             const uint32_t c = rest - qq * a.m[j];
             lamv[j] = a.lam[a.lam_off[j] + c];
             rest = qq;
@@ -505,8 +507,11 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
         const uint32_t q = a.q_off + q0 + l;
         double lamv[kMaxDims] = {0, 0, 0, 0};
         uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
-        for (int jj = 0; jj < a.p - 1; ++jj) {
-            const uint32_t qq = (jj < a.p - 2) ? a.fd[jj].div(rest) : 0u;
+        // line q enumerates the dims other than d, dim 0 fastest
+        const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
+        for (int jj = 0; jj < a.p; ++jj) {
+            if (jj == a.d) continue;
+            const uint32_t qq = (jj < jlast) ? a.fd[jj].div(rest) : 0u;
             lamv[jj] = a.lam[a.lam_off[jj] + (rest - qq * a.m[jj])];
             rest = qq;
         }
