@@ -145,3 +145,23 @@ def test_async_loop_matches_host_loop(variant, monkeypatch):
     assert sa["iters"] == ss["iters"] and ra == rs and sa["status"] == ss["status"]
     assert _rel(ta, ts) <= 1e-12
     assert np.max(np.abs(ua - us)) <= 1e-12 * max(1.0, np.max(np.abs(us)))
+
+
+@pytest.mark.parametrize("weighted", [True, False])
+def test_fused_path_python_block_order(weighted):
+    """Python create_D block order (code/utils.py:138-149): 6 blocks when weighted, 7 unweighted;
+    the fused 3-D kernel's NB = 6 / 7 instantiations against the SuperLU oracle (10 iterations)."""
+    from multivartv_amd.synth import towers
+    m = [16, 16, 16]
+    y = towers(m, seed=99)
+    deltas = [0.3, 0.5, 0.7]
+    P = mv.Problem(m, y, deltas=deltas, order=mv.ORDER_PY, weighted=weighted)
+    assert P.nb == (6 if weighted else 7)
+    th, u, rho, st = P.admm(1.0, np.full(y.size, y.mean()), u=np.zeros(P.E), rho=0.2, fixed_iters=10)
+    P.close()
+    D = O.build_D(m, O.block_table(3, deltas if weighted else None, "py"))
+    ref = O.admm_rcpp(D, y, np.ones(y.size), 1.0, np.full(y.size, y.mean()), np.zeros(D.shape[0]), 0.2,
+                      fixed_iters=10)
+    assert st["theta_solver"] == mv.SOLVER_SPECTRAL and rho == ref.rho
+    assert _rel(th, ref.theta) <= 1e-10
+    assert np.max(np.abs(u - ref.u)) <= 1e-10 * max(1.0, np.max(np.abs(ref.u)))
