@@ -262,7 +262,16 @@ Edge3dArgs e3d_args(const Geom& g) {
 }
 }  // namespace
 
+bool edge4d_ok(const Geom& g);
+hipError_t launch_edge4d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
+                         double t_old, double c_old, double t_new, const double* theta_old, double* partials,
+                         int* nparts, const AdmmCtl* ctl);
+hipError_t launch_gather4d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
+                           double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
+                           int* nparts, const AdmmCtl* ctl);
+
 bool edge3d_ok(const Geom& g) {
+    if (g.p == 4) return edge4d_ok(g);
     if (g.p != 3 || std::getenv("MVTV_E3D_OFF")) return false;
     const Edge3dArgs a = e3d_args(g);
     return (a.nblocks + 7) / 8 * 8 <= kMaxCgBlocks;
@@ -271,6 +280,8 @@ bool edge3d_ok(const Geom& g) {
 hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
                          double t_old, double c_old, double t_new, const double* theta_old, double* partials,
                          int* nparts, const AdmmCtl* ctl) {
+    if (g.p == 4)
+        return launch_edge4d(g, order, umode, s, theta, edges, t_old, c_old, t_new, theta_old, partials, nparts, ctl);
     Edge3dArgs a = e3d_args(g);
     a.ctl = ctl;
     a.theta = theta;
@@ -310,6 +321,16 @@ hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, con
 hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                            double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
                            int* nparts, const AdmmCtl* ctl) {
+    if (g.p == 4) {
+        // 4-D: the marching gather (k_gather4d) reads ~65 neighbour words per cell through L1/L2 and
+        // measured slower at 128^4 (20.8 vs 18.4 ms) than the grid-stride kernel; opt-in only
+        static const bool marching = std::getenv("MVTV_G4D") != nullptr;
+        if (marching)
+            return launch_gather4d(g, order, umode, s, edges, t, g_alpha, g_u, g_uprev, c_prev, partials, nparts, ctl);
+        const int grid = int(std::min<uint64_t>((uint64_t(g.N) + kThreads - 1) / kThreads, kMaxGrid));
+        *nparts = grid;
+        return launch_gather(g, order, umode, Launch{s, grid}, edges, t, g_alpha, g_u, g_uprev, c_prev, partials, ctl);
+    }
     Edge3dArgs a = e3d_args(g);
     a.ctl = ctl;
     a.edges = const_cast<double*>(edges);   // read only in k_gather3d
@@ -661,6 +682,294 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
     };
     if (f3d::rows() == 8) return pick(std::integral_constant<int, 8>{});
     return pick(std::integral_constant<int, 16>{});
+}
+
+// =============================================================================================
+// 4-D (config 5, 128^4): the same marching scheme one dimension up. A thread owns an (x, y, z)
+// cell of the 3-D "plane" of dims 0..2 and walks dim 3; its in-plane neighbours (x+1, y+1, z+1
+// for D, x-1, y-1, z-1 for D^T) are other threads' own cells of the same step (L1/L2 hits), the
+// dim-3 neighbours come from registers (carried theta plane / carried backward sums).
+struct Edge4dArgs {
+    Geom g;
+    const double* theta;
+    double* edges;
+    const double* theta_old;
+    double* g_alpha;
+    double* g_u;
+    const double* g_uprev;
+    double* partials;
+    double t_old, c_old, t_new, t, c_prev;
+    const AdmmCtl* ctl;
+    int tiles_x, tiles_y, tiles_z, wchunk, nblocks, wlo, whi;
+};
+namespace e4d {
+constexpr int TX = 64, TY = 4, NT = TX * TY;
+}
+struct Tile4 {
+    int x, y, z, w0, w1;
+    bool valid;
+};
+__device__ __forceinline__ Tile4 tile4(const Edge4dArgs& a) {
+    Tile4 t{};
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    t.valid = bid < a.nblocks;
+    if (!t.valid) return t;
+    const int nt = a.tiles_x * a.tiles_y * a.tiles_z;
+    const int tw = bid / nt;
+    int rem = bid - tw * nt;
+    const int tz = rem / (a.tiles_x * a.tiles_y);
+    rem -= tz * a.tiles_x * a.tiles_y;
+    const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
+    t.x = tx * e4d::TX + int(threadIdx.x & 63);
+    t.y = ty * e4d::TY + int(threadIdx.x >> 6);
+    t.z = tz;
+    t.w0 = a.wlo + tw * a.wchunk;
+    t.w1 = min(a.whi, t.w0 + a.wchunk);
+    return t;
+}
+
+template <int ORD, int UM, bool DTH, int NB>
+__global__ __launch_bounds__(e4d::NT) void k_edge4d(const Edge4dArgs a) {
+    constexpr int P = 4, NC = 16, PC = 8;
+    const Geom& g = a.g;
+    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        t_old = a.ctl->t_z;
+        c_old = a.ctl->c_prev;
+        t_new = a.ctl->t_next;
+    }
+    double red[ER_N] = {0.0, 0.0, 0.0, 0.0};
+    const Tile4 T = tile4(a);
+    if (T.valid && T.x < int(g.m[0]) && T.y < int(g.m[1])) {
+        const uint32_t m0 = g.m[0], m01 = g.m[0] * g.m[1], pl = m01 * g.m[2];
+        const uint32_t xo[2] = {uint32_t(T.x), uint32_t(min(T.x + 1, int(g.m[0]) - 1))};
+        const uint32_t yo[2] = {uint32_t(T.y) * m0, uint32_t(min(T.y + 1, int(g.m[1]) - 1)) * m0};
+        const uint32_t zo[2] = {uint32_t(T.z) * m01, uint32_t(min(T.z + 1, int(g.m[2]) - 1)) * m01};
+        double th0[PC], th1[PC];
+        auto load_plane = [&](double (&th)[PC], int w) {
+            const uint32_t wo = uint32_t(w) * pl;
+#pragma unroll
+            for (int q = 0; q < PC; ++q) th[q] = a.theta[wo + zo[(q >> 2) & 1] + yo[(q >> 1) & 1] + xo[q & 1]];
+        };
+        load_plane(th0, T.w0);
+        for (int w = T.w0; w < T.w1; ++w) {
+            load_plane(th1, min(w + 1, int(g.m[3]) - 1));
+            const uint32_t i = uint32_t(w) * pl + zo[0] + yo[0] + xo[0];
+            double v[NC];
+#pragma unroll
+            for (int q = 0; q < PC; ++q) {
+                v[q] = th0[q];
+                v[q | PC] = th1[q];
+            }
+            if constexpr (DTH) red[ER_DTH] = fmax(red[ER_DTH], fabs(v[0] - a.theta_old[i]));
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+#pragma unroll
+                for (int q = 0; q < NC; ++q)
+                    if (!((q >> j) & 1)) v[q | (1 << j)] = v[q] - v[q | (1 << j)];
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                const double d = g.w[k] * v[S];
+                double* ep = a.edges + uint64_t(k) * g.N + i;
+                const double stored = __builtin_nontemporal_load(ep);
+                const double uo = (UM == U_EXPLICIT) ? stored : -c_old * clampd(stored, t_old);
+                const double z = d - uo;
+                const double al = z - clampd(z, t_new);
+                const double r = al - d;
+                __builtin_nontemporal_store(z, ep);
+                red[ER_R2] = fma(r, r, red[ER_R2]);
+                red[ER_D2] = fma(d, d, red[ER_D2]);
+                red[ER_A2] = fma(al, al, red[ER_A2]);
+            });
+#pragma unroll
+            for (int q = 0; q < PC; ++q) th0[q] = th1[q];
+        }
+    }
+    if (!T.valid)
+        for (int k = 0; k < ER_N; ++k) red[k] = 0.0;
+    block_reduce_store<ER_N, 1, e4d::NT>(red, a.partials);
+}
+
+template <int ORD, int UM, bool PREV, int NB>
+__global__ __launch_bounds__(e4d::NT) void k_gather4d(const Edge4dArgs a) {
+    constexpr int P = 4, PC = 8;
+    const Geom& g = a.g;
+    double tt = a.t, c_prev = a.c_prev;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        tt = a.ctl->t_next;
+        c_prev = a.ctl->c_prev;
+    }
+    double red[GR_N] = {0.0, 0.0, 0.0};
+    const Tile4 T = tile4(a);
+    if (T.valid && T.x < int(g.m[0]) && T.y < int(g.m[1])) {
+        const uint32_t m0 = g.m[0], m01 = g.m[0] * g.m[1], pl = m01 * g.m[2];
+        const bool okx = T.x > 0, oky = T.y > 0, okz = T.z > 0;
+        const uint32_t base = uint32_t(T.z) * m01 + uint32_t(T.y) * m0 + uint32_t(T.x);
+        uint32_t qoff[PC];
+        bool qok[PC];
+#pragma unroll
+        for (int q = 0; q < PC; ++q) {
+            const bool bx = q & 1, by = (q >> 1) & 1, bz = (q >> 2) & 1;
+            qok[q] = (!bx || okx) && (!by || oky) && (!bz || okz);
+            qoff[q] = qok[q] ? (bx ? 1u : 0u) + (by ? m0 : 0u) + (bz ? m01 : 0u) : 0u;
+        }
+        double qa_prev[NB], qu_prev[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) qa_prev[k] = qu_prev[k] = 0.0;
+        auto plane_q = [&](auto kc, int w, double& qa, double& qu) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+            constexpr int SI = S & 7;
+            const double* eb = a.edges + uint64_t(k) * g.N + uint32_t(w) * pl + base;
+            qa = 0.0;
+            qu = 0.0;
+#pragma unroll
+            for (int q = 0; q < PC; ++q) {
+                if ((q & ~SI) != 0) continue;
+                const double vv = *(eb - qoff[q]);
+                const double v = qok[q] ? vv : 0.0;
+                const bool neg = __builtin_popcount(q) & 1;
+                if constexpr (UM == U_FROM_Z) {
+                    const double cl = clampd(v, tt);
+                    const double al = v - cl;
+                    qa = neg ? qa - al : qa + al;
+                    qu = neg ? qu + cl : qu - cl;
+                } else {
+                    qu = neg ? qu - v : qu + v;
+                }
+            }
+        };
+        if (T.w0 > 0) {
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                if constexpr ((S & 8) != 0) plane_q(kc, T.w0 - 1, qa_prev[k], qu_prev[k]);
+            });
+        }
+        for (int w = T.w0; w < T.w1; ++w) {
+            double ga = 0.0, gu = 0.0;
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                double qa, qu;
+                plane_q(kc, w, qa, qu);
+                double ca = qa, cu = qu;
+                if constexpr ((S & 8) != 0) {
+                    ca -= qa_prev[k];
+                    cu -= qu_prev[k];
+                    qa_prev[k] = qa;
+                    qu_prev[k] = qu;
+                }
+                ga = fma(g.w[k], ca, ga);
+                gu = fma(g.w[k], cu, gu);
+            });
+            const uint32_t i = uint32_t(w) * pl + base;
+            if constexpr (UM == U_FROM_Z) __builtin_nontemporal_store(ga, a.g_alpha + i);
+            __builtin_nontemporal_store(gu, a.g_u + i);
+            red[GR_GU2] = fma(gu, gu, red[GR_GU2]);
+            if constexpr (PREV) {
+                const double gp = c_prev * __builtin_nontemporal_load(a.g_uprev + i);
+                const double db = gu - gp, da = ga + gp;
+                red[GR_S2B] = fma(db, db, red[GR_S2B]);
+                red[GR_S2A] = fma(da, da, red[GR_S2A]);
+            }
+        }
+    }
+    if (!T.valid)
+        for (int k = 0; k < GR_N; ++k) red[k] = 0.0;
+    block_reduce_store<GR_N, 0, e4d::NT>(red, a.partials);
+}
+
+namespace {
+Edge4dArgs e4d_args(const Geom& g) {
+    Edge4dArgs a{};
+    a.g = g;
+    const uint32_t pl = g.m[0] * g.m[1] * g.m[2];
+    a.wlo = int(g.ibeg / pl);
+    a.whi = int(g.iend / pl);
+    a.tiles_x = int((g.m[0] + e4d::TX - 1) / e4d::TX);
+    a.tiles_y = int((g.m[1] + e4d::TY - 1) / e4d::TY);
+    a.tiles_z = int(g.m[2]);
+    const int tiles = a.tiles_x * a.tiles_y * a.tiles_z;
+    const int nwp = std::max(1, a.whi - a.wlo);
+    int nw = std::max(1, std::min(nwp, 8192 / std::max(1, tiles)));
+    while (nw > 1 && ((nw * tiles + 7) / 8 * 8) > kMaxCgBlocks) --nw;
+    a.wchunk = (nwp + nw - 1) / nw;
+    nw = (nwp + a.wchunk - 1) / a.wchunk;
+    a.nblocks = tiles * nw;
+    return a;
+}
+}  // namespace
+
+bool edge4d_ok(const Geom& g) {
+    if (g.p != 4 || std::getenv("MVTV_E3D_OFF")) return false;
+    const Edge4dArgs a = e4d_args(g);
+    return (a.nblocks + 7) / 8 * 8 <= kMaxCgBlocks;
+}
+
+hipError_t launch_edge4d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
+                         double t_old, double c_old, double t_new, const double* theta_old, double* partials,
+                         int* nparts, const AdmmCtl* ctl) {
+    Edge4dArgs a = e4d_args(g);
+    a.theta = theta;
+    a.edges = edges;
+    a.theta_old = theta_old;
+    a.partials = partials;
+    a.t_old = t_old;
+    a.c_old = c_old;
+    a.t_new = t_new;
+    a.ctl = ctl;
+    const int grid = (a.nblocks + 7) / 8 * 8;
+    *nparts = grid;
+    const bool dth = theta_old != nullptr;
+    auto go = [&](auto kern) {
+        klaunch(kern, dim3(grid), dim3(e4d::NT), 0, s, a);
+        return hipGetLastError();
+    };
+    if (order == 0) {
+        if (umode == U_EXPLICIT) return dth ? go(k_edge4d<0, U_EXPLICIT, true, 15>) : go(k_edge4d<0, U_EXPLICIT, false, 15>);
+        return dth ? go(k_edge4d<0, U_FROM_Z, true, 15>) : go(k_edge4d<0, U_FROM_Z, false, 15>);
+    }
+    if (g.nb == 14) {
+        if (umode == U_EXPLICIT) return dth ? go(k_edge4d<1, U_EXPLICIT, true, 14>) : go(k_edge4d<1, U_EXPLICIT, false, 14>);
+        return dth ? go(k_edge4d<1, U_FROM_Z, true, 14>) : go(k_edge4d<1, U_FROM_Z, false, 14>);
+    }
+    if (umode == U_EXPLICIT) return dth ? go(k_edge4d<1, U_EXPLICIT, true, 15>) : go(k_edge4d<1, U_EXPLICIT, false, 15>);
+    return dth ? go(k_edge4d<1, U_FROM_Z, true, 15>) : go(k_edge4d<1, U_FROM_Z, false, 15>);
+}
+
+hipError_t launch_gather4d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
+                           double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
+                           int* nparts, const AdmmCtl* ctl) {
+    Edge4dArgs a = e4d_args(g);
+    a.edges = const_cast<double*>(edges);   // read only in k_gather4d
+    a.g_alpha = g_alpha;
+    a.g_u = g_u;
+    a.g_uprev = g_uprev;
+    a.partials = partials;
+    a.t = t;
+    a.c_prev = c_prev;
+    a.ctl = ctl;
+    const int grid = (a.nblocks + 7) / 8 * 8;
+    *nparts = grid;
+    const bool prev = g_uprev != nullptr;
+    auto go = [&](auto kern) {
+        klaunch(kern, dim3(grid), dim3(e4d::NT), 0, s, a);
+        return hipGetLastError();
+    };
+    if (order == 0) {
+        if (umode == U_EXPLICIT) return prev ? go(k_gather4d<0, U_EXPLICIT, true, 15>) : go(k_gather4d<0, U_EXPLICIT, false, 15>);
+        return prev ? go(k_gather4d<0, U_FROM_Z, true, 15>) : go(k_gather4d<0, U_FROM_Z, false, 15>);
+    }
+    if (g.nb == 14) {
+        if (umode == U_EXPLICIT) return prev ? go(k_gather4d<1, U_EXPLICIT, true, 14>) : go(k_gather4d<1, U_EXPLICIT, false, 14>);
+        return prev ? go(k_gather4d<1, U_FROM_Z, true, 14>) : go(k_gather4d<1, U_FROM_Z, false, 14>);
+    }
+    if (umode == U_EXPLICIT) return prev ? go(k_gather4d<1, U_EXPLICIT, true, 15>) : go(k_gather4d<1, U_EXPLICIT, false, 15>);
+    return prev ? go(k_gather4d<1, U_FROM_Z, true, 15>) : go(k_gather4d<1, U_FROM_Z, false, 15>);
 }
 
 }  // namespace mvtv
