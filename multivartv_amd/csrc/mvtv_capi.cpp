@@ -82,6 +82,8 @@ struct mvtv_problem {
     bool e3d = false;             // z-marching 3-D edge kernels
     bool f3d = false;             // fused 3-D edge update + gather (needs the second edge buffer)
     double* edges2 = nullptr;     // ping-pong partner of edges for the fused kernel
+    double* pcg_b = nullptr;      // right-hand side of the spectrally preconditioned PCG
+    double wmean = 1.0;           // mean(W): the preconditioner's identity weight
     AdmmCtl* ctl = nullptr;       // device control block of the asynchronous ADMM loop
     AdmmCtl* host_ctl = nullptr;  // pinned mirror
     int admm_hint = 0;            // ADMM iterations of the last converged run (enqueue-ahead depth)
@@ -176,7 +178,7 @@ mvtv_status alloc(double** ptr, size_t n) {
 void free_all(mvtv_problem* P) {
     double** bufs[] = {&P->oty, &P->wdiag, &P->theta, &P->edges, &P->ga, &P->gu, &P->guprev, &P->r,
                        &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->scratch,
-                       &P->edges2};
+                       &P->edges2, &P->pcg_b};
     for (double** b : bufs)
         if (*b) {
             (void)hipFree(*b);
@@ -363,7 +365,8 @@ mvtv_status spectral_plan(mvtv_problem* P) {
 // Direct solve (I + sigma D^T D) x = oty + ca*ga + cb*gb: forward DCT along dims 0..p-2, the
 // last dim's forward/divide/inverse in one pass, inverse DCT along dims p-2..0. All in place on x.
 mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, const double* ga, double ca,
-                           const double* gb, double cb, double* x, const AdmmCtl* ctl = nullptr) {
+                           const double* gb, double cb, double* x, const AdmmCtl* ctl = nullptr, double w0 = 1.0,
+                           const int32_t* skip = nullptr) {
     // pass order: forward along dims order[0..p-2], forward/divide/inverse along order[p-1], inverse
     // back; the MID dimension defaults to p-1 (MVTV_DCT_MID selects another one for experiments)
     const int p = P->g.p;
@@ -383,18 +386,78 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
         const int h = P->tstart(first ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
         if (first && ga)   // b = oty + ca*ga + cb*gb formed on load
             HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, oty, ga, ca, gb ? gb : ga, gb ? cb : 0.0, x,
-                                    sigma, 1.0, ctl));
+                                    sigma, w0, ctl, 0, 0.0, skip));
         else
             HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, first ? oty : x, nullptr, 0.0, nullptr, 0.0, x,
-                                    sigma, 1.0, ctl));
+                                    sigma, w0, ctl, 0, 0.0, skip));
         P->tstop(h);
     }
     for (int t = p - 2; t >= 0; --t) {
         const int h = P->tstart(MVTV_K_DCT);
-        HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 1, order[t], x, nullptr, 0.0, nullptr, 0.0, x, sigma, 1.0,
-                                ctl));
+        HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 1, order[t], x, nullptr, 0.0, nullptr, 0.0, x, sigma, w0,
+                                ctl, 0, 0.0, skip));
         P->tstop(h);
     }
+    return MVTV_OK;
+}
+
+// (W + sigma D^T D) x = oty + ca*ga + cb*gb by PCG with M = mean(W) I + sigma D^T D, applied exactly by
+// the spectral solve. Scalars stay on the device (PcgState, k_finalize ops 1-3); iterations enqueued
+// after convergence return at once (st->done), the host polls like pcg_solve.
+mvtv_status pcgs_solve(mvtv_problem* P, double sigma, const double* oty, const double* ga, double ca,
+                       const double* gb, double cb, double* x, double rtol, int maxit, int* iters, double* relres) {
+    const Launch L = P->L();
+    if (!P->p2) MVTV_TRY(alloc(&P->p2, P->g.N));
+    if (!P->pcg_b) MVTV_TRY(alloc(&P->pcg_b, P->g.N));
+    double *r = P->r, *z = P->q, *p = P->p, *q = P->p2, *b = P->pcg_b;
+    const double w0 = P->wmean > 0.0 ? P->wmean : 1.0;
+    int h = P->tstart(MVTV_K_PCG_INIT);
+    HIP_TRY(launch_apply_A(P->g, L, sigma, P->wmode, P->wdiag, x, q, nullptr, nullptr));
+    P->tstop(h);
+    HIP_TRY(launch_pcgs_vec(P->g, L, 0, oty, ga, ca, gb, cb, x, r, p, q, nullptr, b, P->st, nullptr, 0));
+    MVTV_TRY(spectral_solve(P, sigma, r, nullptr, 0.0, nullptr, 0.0, z, nullptr, w0, nullptr));
+    HIP_TRY(launch_pcgs_vec(P->g, L, 2, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, z, b, P->st, P->partials, 1));
+    HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 3, 0, 1, nullptr, P->st, rtol * rtol, maxit));
+    HIP_TRY(hipMemcpyAsync(p, z, size_t(P->g.N) * sizeof(double), hipMemcpyDeviceToDevice, P->stream));
+    const int32_t* skip = &P->st->done;
+    auto enqueue = [&]() -> mvtv_status {
+        int hh = P->tstart(MVTV_K_PCG_APPLY);
+        HIP_TRY(launch_apply_A(P->g, L, sigma, P->wmode, P->wdiag, p, q, P->partials, P->st));   // q = A p, p.q
+        P->tstop(hh);
+        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 0, 2, nullptr, P->st));         // alpha
+        hh = P->tstart(MVTV_K_PCG_UPDATE);
+        HIP_TRY(launch_pcgs_vec(P->g, L, 1, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, nullptr, b, P->st,
+                                nullptr, 0));
+        P->tstop(hh);
+        MVTV_TRY(spectral_solve(P, sigma, r, nullptr, 0.0, nullptr, 0.0, z, nullptr, w0, skip));   // z = M^-1 r
+        HIP_TRY(launch_pcgs_vec(P->g, L, 2, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, z, b, P->st,
+                                P->partials, 0));
+        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 3, 0, 3, nullptr, P->st));         // beta, done
+        hh = P->tstart(MVTV_K_PCG_DIRECTION);
+        HIP_TRY(launch_pcgs_vec(P->g, L, 3, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, z, b, P->st, nullptr, 0));
+        P->tstop(hh);
+        return MVTV_OK;
+    };
+    std::vector<size_t> mark;
+    int enq = 0;
+    int batch = P->pcg_hint > 0 ? std::max(2, P->pcg_hint - 2) : kPcgPoll;
+    for (;;) {
+        for (int bb = 0; bb < batch && enq < maxit; ++bb, ++enq) {
+            mark.push_back(P->pending.size());
+            MVTV_TRY(enqueue());
+        }
+        HIP_TRY(hipMemcpyAsync(P->host_st, P->st, sizeof(PcgState), hipMemcpyDeviceToHost, P->stream));
+        HIP_TRY(hipStreamSynchronize(P->stream));
+        const int done_iters = P->host_st->iter;
+        if (P->timing && done_iters < int(mark.size()))
+            for (size_t e = mark[size_t(done_iters)]; e < P->pending.size(); ++e) P->pending[e].kid = -1;
+        P->harvest();
+        if (P->host_st->done || enq >= maxit) break;
+        batch = 2;
+    }
+    *iters = P->host_st->iter;
+    P->pcg_hint = *iters;
+    *relres = P->host_st->bnorm2 > 0 ? std::sqrt(P->host_st->rnorm2 / P->host_st->bnorm2) : 0.0;
     return MVTV_OK;
 }
 
@@ -636,6 +699,9 @@ mvtv_status mvtv_problem_set_data(mvtv_problem* P, const double* oty, const doub
         if (!P->wdiag) MVTV_TRY(alloc(&P->wdiag, P->g.N));
         HIP_TRY(hipMemcpyAsync(P->wdiag, wdiag, bytes, hipMemcpyHostToDevice, P->stream));
         P->wmode = W_DIAG;
+        double acc = 0.0;
+        for (uint32_t i = 0; i < P->g.N; ++i) acc += wdiag[i];
+        P->wmean = acc / double(P->g.N);
     } else {
         P->wmode = W_IDENTITY;
     }
@@ -693,12 +759,15 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     const int pcg_maxit = o.pcg_max_iter > 0 ? o.pcg_max_iter : 20000;
     const Launch L = P->L();
     const double N = double(P->g.N), E = double(P->E);
-    if (o.theta_solver < MVTV_SOLVER_AUTO || o.theta_solver > MVTV_SOLVER_SPECTRAL)
+    if (o.theta_solver < MVTV_SOLVER_AUTO || o.theta_solver > MVTV_SOLVER_PCG_SPECTRAL)
         return fail(MVTV_BAD_ARG, "theta_solver");
     if (o.theta_solver == MVTV_SOLVER_SPECTRAL && !spectral_ok(P))
         return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and power-of-two m_j <= 4096");
+    if (o.theta_solver == MVTV_SOLVER_PCG_SPECTRAL && (!P->spec_mesh || P->wmode == W_NONE))
+        return fail(MVTV_BAD_ARG, "spectral preconditioner needs power-of-two m_j <= 4096");
     const bool spectral = o.theta_solver == MVTV_SOLVER_SPECTRAL ||
                           (o.theta_solver == MVTV_SOLVER_AUTO && spectral_ok(P));
+    const bool pcg_spec = o.theta_solver == MVTV_SOLVER_PCG_SPECTRAL;
 
     // ---- initial state: u explicit in the edge buffer, alpha_0 = D theta_0 ------------------
     double rho;
@@ -905,6 +974,9 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         double relres = 0.0;
         if (spectral)
             MVTV_TRY(spectral_solve(P, sigma, P->oty, P->ga, rho, gprev, rho * c_prev, P->theta));
+        else if (pcg_spec)
+            MVTV_TRY(pcgs_solve(P, sigma, P->oty, P->ga, rho, gprev, rho * c_prev, P->theta, rtol, pcg_maxit, &pit,
+                                &relres));
         else
             MVTV_TRY(pcg_solve(P, sigma, P->oty, P->ga, rho, gprev, rho * c_prev, P->theta, rtol, pcg_maxit, &pit,
                                &relres));
@@ -1027,7 +1099,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     P->c_state = c_prev;
     P->rho = rho;
     S.iters = it;
-    S.theta_solver = spectral ? MVTV_SOLVER_SPECTRAL : MVTV_SOLVER_PCG;
+    S.theta_solver = spectral ? MVTV_SOLVER_SPECTRAL : (pcg_spec ? MVTV_SOLVER_PCG_SPECTRAL : MVTV_SOLVER_PCG);
     S.rho = rho;
     S.status = status;
     S.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -176,6 +176,11 @@ hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n);
 // CG vector steps of lam_max_pinv (op 0 |x|^2 into partials, 1 x += c p & y -= c t, 2 x = p + c x)
 hipError_t launch_cg_vec(const Geom& g, const Launch& L, int op, double coef, double* x, double* y, const double* p,
                          const double* t, double* partials);
+// vector steps of PCG with the spectral preconditioner (mvtv_kernels.hip k_pcgs_vec): op 0 b and
+// r = b - q with |b|^2; 1 x, r update; 2 (r.z, |r|^2 [, |b|^2]) in PR layout; 3 p = z + beta p
+hipError_t launch_pcgs_vec(const Geom& g, const Launch& L, int op, const double* oty, const double* ga, double ca,
+                           const double* gb, double cb, double* x, double* r, double* p, const double* q,
+                           const double* z, double* b, const PcgState* st, double* partials, int with_b2);
 // per-workgroup max |D x| (one max-partial per workgroup, L.grid rows)
 hipError_t launch_dmaxabs(const Geom& g, int order, const Launch& L, const double* x, double* partials);
 // compact <-> padded edge layouts for one block segment [e0, e0+cnt) of block k
@@ -198,7 +203,8 @@ struct SpecPlan {
 // ga != nullptr forms the input as in + ca*ga + cb*gb. In place (in == out) is allowed.
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
-                           double w0, const AdmmCtl* ctl = nullptr, uint32_t q_off = 0, double inv_n = 0.0);
+                           double w0, const AdmmCtl* ctl = nullptr, uint32_t q_off = 0, double inv_n = 0.0,
+                           const int32_t* skip = nullptr);
 // z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /
 // launch_gather, *nparts workgroup rows
 bool edge3d_ok(const Geom& g);

@@ -471,6 +471,50 @@ __global__ __launch_bounds__(kThreads) void k_dmaxabs(Geom g, const double* __re
     block_reduce_store<1, 1>(red, partials);
 }
 
+// --------------------------------------------------------------------- PCG with the spectral preconditioner
+// M = wbar I + sigma D^T D (exact inverse by cosine transforms, mvtv_spectral.hip) for A = W + sigma D^T D.
+// op 0: b = oty + ca ga + cb gb, r = b - q (q = A x)
+// op 1: x += alpha p, r -= alpha q (alpha from the PCG state)
+// op 2: partials, 3 per workgroup: (|b|^2, r.z, |r|^2) = k_finalize op 1's layout when with_b2,
+//       else (r.z, |r|^2, 0) = op 3's
+// op 3: p = z + beta p
+__global__ __launch_bounds__(kThreads) void k_pcgs_vec(int op, uint32_t n, const double* __restrict__ oty,
+                                                       const double* __restrict__ ga, double ca,
+                                                       const double* __restrict__ gb, double cb,
+                                                       double* __restrict__ x, double* __restrict__ r,
+                                                       double* __restrict__ p, const double* __restrict__ q,
+                                                       const double* __restrict__ z, double* __restrict__ b,
+                                                       const PcgState* __restrict__ st, double* __restrict__ partials,
+                                                       int with_b2) {
+    // op 0 and the init reduction (with_b2) run before k_finalize op 1 resets st->done
+    if (op != 0 && !(op == 2 && with_b2) && st->done) return;
+    double red[3] = {0.0, 0.0, 0.0};
+    const double alpha = op == 1 ? st->alpha : 0.0, beta = op == 3 ? st->beta : 0.0;
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        if (op == 0) {
+            const double bi = fma(cb, gb[i], fma(ca, ga[i], oty[i]));
+            b[i] = bi;
+            r[i] = bi - q[i];
+        } else if (op == 1) {
+            x[i] = fma(alpha, p[i], x[i]);
+            r[i] = fma(-alpha, q[i], r[i]);
+        } else if (op == 2) {
+            const double ri = r[i];
+            if (with_b2) {
+                red[PR_B2] = fma(b[i], b[i], red[PR_B2]);
+                red[PR_RZ] = fma(ri, z[i], red[PR_RZ]);
+                red[PR_R2] = fma(ri, ri, red[PR_R2]);
+            } else {
+                red[0] = fma(ri, z[i], red[0]);
+                red[1] = fma(ri, ri, red[1]);
+            }
+        } else {
+            p[i] = fma(beta, p[i], z[i]);
+        }
+    }
+    if (op == 2) block_reduce_store<3, 0>(red, partials);
+}
+
 struct RedDims {
     uint64_t rd[kMaxDims];
     uint64_t stride[kMaxDims];
@@ -814,6 +858,14 @@ hipError_t launch_dmaxabs(const Geom& g, int order, const Launch& L, const doubl
         else klaunch(k_dmaxabs<P, 1>, dim3(L.grid), dim3(kThreads), 0, L.stream, g, x, partials);
         return hipGetLastError();
     });
+}
+
+hipError_t launch_pcgs_vec(const Geom& g, const Launch& L, int op, const double* oty, const double* ga, double ca,
+                           const double* gb, double cb, double* x, double* r, double* p, const double* q,
+                           const double* z, double* b, const PcgState* st, double* partials, int with_b2) {
+    klaunch(k_pcgs_vec, dim3(L.grid), dim3(kThreads), 0, L.stream, op, g.N, oty, ga, ca, gb, cb, x, r, p, q, z, b, st,
+            partials, with_b2);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n) {

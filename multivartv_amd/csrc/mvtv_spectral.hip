@@ -66,6 +66,7 @@ struct SpecArgs {
     int32_t d, p, L, tq;     // line dimension, dims, log2 m, lines per workgroup
     int32_t ls;              // log2 stride
     uint32_t q_off;          // MID: global index of line 0 (slab-decomposed solve works on a line chunk)
+    const int32_t* skip;     // != nullptr and *skip: return at once (preconditioner of a converged PCG)
     const AdmmCtl* ctl;      // asynchronous ADMM loop: sigma, ca = rho, cb = rho c_prev from the device
 };
 
@@ -186,6 +187,7 @@ __device__ __forceinline__ uint32_t line_addr(const SpecArgs& a, uint32_t q0, ui
 template <int MODE, bool D0, bool FORMB>
 __global__ __launch_bounds__(spec::NT) void k_dct(const SpecArgs a) {
     double sigma = a.sigma, ca = a.ca, cb = a.cb;   // locals: see k_dct8
+    if (a.skip && *a.skip) return;
     if (a.ctl) {
         if (a.ctl->done) return;
         sigma = a.ctl->sigma;
@@ -483,6 +485,7 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
     using S = spec8::ShapeK<L, TQW>;
     // scalars into locals: writing into the by-value argument struct would demote it to scratch
     double sigma = a.sigma, ca = a.ca, cb = a.cb;
+    if (a.skip && *a.skip) return;
     if (a.ctl) {
         if (a.ctl->done) return;
         sigma = a.ctl->sigma;
@@ -726,9 +729,10 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
 
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
-                           double w0, const AdmmCtl* ctl, uint32_t q_off, double inv_n) {
+                           double w0, const AdmmCtl* ctl, uint32_t q_off, double inv_n, const int32_t* skip) {
     SpecArgs a{};
     a.ctl = ctl;
+    a.skip = skip;
     a.q_off = q_off;
     a.in = in;
     a.ga = ga;
