@@ -214,3 +214,29 @@ def test_spectrally_preconditioned_pcg(case):
         assert _rel(th, ref.theta) <= 1e-9
     print(case, "PCG iterations: Jacobi", out[mv.SOLVER_PCG][3]["pcg_iters"], "spectral",
           out[mv.SOLVER_PCG_SPECTRAL][3]["pcg_iters"])
+
+
+@pytest.mark.parametrize("variant", [mv.VARIANT_RCPP, mv.VARIANT_CPP, mv.VARIANT_PY])
+def test_async_loop_max_counter(variant, monkeypatch):
+    """max_counter handling on the device matches the host loop: B stops with MAXITER after
+    max_counter - 1 iterations (rcpp…/solvers.cpp:129-132), A reports MAXITER (its throw,
+    cpp-code/solvers.cpp:122-124), C stops at max_counter iterations."""
+    from multivartv_amd.synth import towers
+    m = [16, 16, 16]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    res = {}
+    for mode in ("async", "sync"):
+        if mode == "sync":
+            monkeypatch.setenv("MVTV_ADMM_SYNC", "1")
+        else:
+            monkeypatch.delenv("MVTV_ADMM_SYNC", raising=False)
+        with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+            P.state_set(np.full(y.size, y.mean()), None, 0.2)
+            st = P.run(2.0, variant=variant, max_counter=6, tol=1e-12, ymean=float(y.mean()))
+            th, _, rho = P.state_get(want_u=False)
+        res[mode] = (st, th, rho)
+    (sa, ta, ra), (ss, ts, rs) = res["async"], res["sync"]
+    assert sa["status"] == ss["status"] == 1          # MVTV_MAXITER
+    assert sa["iters"] == ss["iters"] and ra == rs
+    assert _rel(ta, ts) <= 1e-12
