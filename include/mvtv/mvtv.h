@@ -150,6 +150,22 @@ mvtv_status mvtv_admm_run(mvtv_problem* prob, const mvtv_admm_opts* opts, double
 /* fitted values O theta for n points given their mesh index (fill_output_mbs_one, rcpp…/solvers.cpp:73) */
 mvtv_status mvtv_fitted(mvtv_problem* prob, const int64_t* mesh_index, int64_t n, double* fitted);
 
+/* ---- scattered data on the device ----------------------------------------------------
+ * axes: the mesh's sorted axis values, m[0] values of dim 0, then m[1] of dim 1, ... (the linspace
+ * axes of create_mesh, rcpp…/utils.cpp:234-254; mesh rows in column-major order). data: n x p,
+ * column-major (arma::mat). mesh_index_out [n] (may be NULL): the column-major mesh node of each
+ * point, i.e. the column of the 1 in row i of O. */
+/* nearest1 / nearest_interp_matrix (rcpp…/utils.cpp:267-304): first nearest mesh row per point */
+mvtv_status mvtv_nearest(mvtv_problem* prob, const double* axes, const double* data, int64_t n,
+                         int64_t* mesh_index_out);
+/* create_cache_objects (rcpp…/solvers.cpp:36-44) on the device: O from mvtv_nearest, then
+ * W = diag(O^T O) and O^T y (summed per node in data order) installed as the problem's data, as by
+ * mvtv_problem_set_data (W = I when every node holds exactly one point). */
+mvtv_status mvtv_problem_set_scattered(mvtv_problem* prob, const double* axes, const double* data, int64_t n,
+                                       const double* y, int64_t* mesh_index_out);
+/* mbs_predict (rcpp…/solvers.cpp:161-165): O(data) theta of the resident state, fits [n] */
+mvtv_status mvtv_predict(mvtv_problem* prob, const double* axes, const double* data, int64_t n, double* fits);
+
 /* ---- operators (inits.D*theta, inits.Dt*v, spcrosses*x, spsolve(spcrosses, b):
  *      rcpp…/solvers.cpp:112-126) ----------------------------------------------------- */
 mvtv_status mvtv_apply_D(mvtv_problem* prob, const double* theta, double* d_out);        /* [N] -> [E] */

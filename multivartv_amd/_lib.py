@@ -83,6 +83,9 @@ SIGNATURES = {
     "mvtv_state_get": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
     "mvtv_admm_run": (C.c_int, [C.c_void_p, C.POINTER(AdmmOpts), C.c_double, C.POINTER(AdmmStats)]),
     "mvtv_fitted": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int64, _dp]),
+    "mvtv_nearest": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, C.POINTER(C.c_int64)]),
+    "mvtv_problem_set_scattered": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, C.POINTER(C.c_int64)]),
+    "mvtv_predict": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp]),
     "mvtv_apply_D": (C.c_int, [C.c_void_p, _dp, _dp]),
     "mvtv_apply_Dt": (C.c_int, [C.c_void_p, _dp, _dp]),
     "mvtv_apply_A": (C.c_int, [C.c_void_p, C.c_double, _dp, _dp]),
@@ -260,6 +263,43 @@ class Problem:
         idx = np.ascontiguousarray(np.asarray(mesh_index, dtype=np.int64).ravel())
         out = np.empty(idx.size)
         _check(lib().mvtv_fitted(self._h, idx.ctypes.data_as(C.POINTER(C.c_int64)), idx.size, _ptr(out)))
+        return out
+
+    # ---- scattered data (nearest_interp_matrix, create_cache_objects, mbs_predict) -------------
+    def _axes_data(self, axes, data):
+        axes = [np.asarray(a, dtype=np.float64).ravel() for a in axes]
+        if len(axes) != self.p or any(a.size != mj for a, mj in zip(axes, self.m)):
+            raise ValueError("axes must hold m_j sorted values per dimension")
+        ax = np.ascontiguousarray(np.concatenate(axes))
+        d = np.asarray(data, dtype=np.float64)
+        d = d.reshape(-1, 1) if d.ndim == 1 else d
+        if d.shape[1] != self.p:
+            raise ValueError(f"data must be n x {self.p}")
+        return ax, np.asfortranarray(d), d.shape[0]
+
+    def nearest(self, axes, data):
+        """nearest1 (rcpp…/utils.cpp:280-287) on the GPU: column-major mesh node of each data row."""
+        ax, d, n = self._axes_data(axes, data)
+        idx = np.empty(n, dtype=np.int64)
+        _check(lib().mvtv_nearest(self._h, _ptr(ax), d.ctypes.data_as(_dp), n,
+                                  idx.ctypes.data_as(C.POINTER(C.c_int64))))
+        return idx
+
+    def set_scattered(self, axes, data, y):
+        """create_cache_objects (rcpp…/solvers.cpp:36-44) on the GPU: O^T y and diag(O^T O) become the
+        problem's data; returns the mesh node of each data row."""
+        ax, d, n = self._axes_data(axes, data)
+        yy = _f64(y, n)
+        idx = np.empty(n, dtype=np.int64)
+        _check(lib().mvtv_problem_set_scattered(self._h, _ptr(ax), d.ctypes.data_as(_dp), n, _ptr(yy),
+                                                idx.ctypes.data_as(C.POINTER(C.c_int64))))
+        return idx
+
+    def predict(self, axes, data):
+        """mbs_predict (rcpp…/solvers.cpp:161-165): O(data) theta of the resident state."""
+        ax, d, n = self._axes_data(axes, data)
+        out = np.empty(n)
+        _check(lib().mvtv_predict(self._h, _ptr(ax), d.ctypes.data_as(_dp), n, _ptr(out)))
         return out
 
     # ---- operators --------------------------------------------------------------------------

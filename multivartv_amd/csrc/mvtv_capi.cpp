@@ -1145,6 +1145,108 @@ mvtv_status mvtv_fitted(mvtv_problem* P, const int64_t* mesh_index, int64_t n, d
     return s;
 }
 
+}  // extern "C"
+
+namespace {
+// device scratch freed on scope exit (setup paths, not the iteration loop)
+struct TmpDev {
+    void* p = nullptr;
+    ~TmpDev() {
+        if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T* get() const { return static_cast<T*>(p); }
+};
+
+// axes checked on the host (finite, ascending per dim), then axes and data copied over and the
+// nearest node of every point computed into key (and idx when requested)
+mvtv_status nearest_on_device(mvtv_problem* P, const double* axes, const double* data, int64_t n, TmpDev& key,
+                              TmpDev& idx, bool want_idx) {
+    if (P->slab) return fail(MVTV_BAD_ARG, "scattered data on a slab problem: set it up on the whole mesh");
+    const int p = P->g.p;
+    size_t na = 0;
+    double span[MVTV_MAX_DIMS] = {0, 0, 0, 0};
+    for (int j = 0; j < p; ++j) {
+        const double* a = axes + na;
+        span[j] = a[P->g.m[j] - 1] - a[0];
+        for (uint32_t k = 0; k < P->g.m[j]; ++k)
+            if (!std::isfinite(a[k]) || (k > 0 && !(a[k] > a[k - 1])))
+                return fail(MVTV_BAD_ARG, "axes must be finite and strictly ascending per dimension");
+        na += P->g.m[j];
+    }
+    for (int64_t i = 0; i < n * p; ++i)
+        if (std::isnan(data[i])) return fail(MVTV_BAD_ARG, "NaN in data");
+    TmpDev daxes, ddata;
+    HIP_TRY(hipMalloc(&daxes.p, na * sizeof(double)));
+    HIP_TRY(hipMalloc(&ddata.p, size_t(std::max<int64_t>(n * p, 1)) * sizeof(double)));
+    HIP_TRY(hipMalloc(&key.p, size_t(std::max<int64_t>(n, 1)) * sizeof(uint32_t)));
+    if (want_idx) HIP_TRY(hipMalloc(&idx.p, size_t(std::max<int64_t>(n, 1)) * sizeof(int64_t)));
+    HIP_TRY(hipMemcpyAsync(daxes.p, axes, na * sizeof(double), hipMemcpyHostToDevice, P->stream));
+    if (n > 0)
+        HIP_TRY(hipMemcpyAsync(ddata.p, data, size_t(n * p) * sizeof(double), hipMemcpyHostToDevice, P->stream));
+    uint32_t m[MVTV_MAX_DIMS];
+    for (int j = 0; j < p; ++j) m[j] = P->g.m[j];
+    HIP_TRY(launch_nearest(P->stream, p, m, daxes.get<double>(), span, ddata.get<double>(), n, key.get<uint32_t>(),
+                           want_idx ? idx.get<int64_t>() : nullptr));
+    HIP_TRY(hipStreamSynchronize(P->stream));   // the temporaries above go out of scope
+    return MVTV_OK;
+}
+}  // namespace
+
+extern "C" {
+
+mvtv_status mvtv_nearest(mvtv_problem* P, const double* axes, const double* data, int64_t n, int64_t* mesh_index_out) {
+    if (!P || !axes || n < 0 || (n > 0 && (!data || !mesh_index_out))) return fail(MVTV_BAD_ARG, "null argument");
+    DeviceGuard dg(P->device);
+    TmpDev key, idx;
+    MVTV_TRY(nearest_on_device(P, axes, data, n, key, idx, true));
+    if (n > 0) {
+        HIP_TRY(hipMemcpyAsync(mesh_index_out, idx.p, size_t(n) * sizeof(int64_t), hipMemcpyDeviceToHost, P->stream));
+        HIP_TRY(hipStreamSynchronize(P->stream));
+    }
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_problem_set_scattered(mvtv_problem* P, const double* axes, const double* data, int64_t n,
+                                       const double* y, int64_t* mesh_index_out) {
+    if (!P || !axes || n < 0 || (n > 0 && (!data || !y))) return fail(MVTV_BAD_ARG, "null argument");
+    DeviceGuard dg(P->device);
+    TmpDev key, idx, dy, runs;
+    MVTV_TRY(nearest_on_device(P, axes, data, n, key, idx, mesh_index_out != nullptr));
+    if (mesh_index_out && n > 0)
+        HIP_TRY(hipMemcpyAsync(mesh_index_out, idx.p, size_t(n) * sizeof(int64_t), hipMemcpyDeviceToHost, P->stream));
+    HIP_TRY(hipMalloc(&dy.p, size_t(std::max<int64_t>(n, 1)) * sizeof(double)));
+    HIP_TRY(hipMalloc(&runs.p, sizeof(unsigned long long)));
+    if (n > 0) HIP_TRY(hipMemcpyAsync(dy.p, y, size_t(n) * sizeof(double), hipMemcpyHostToDevice, P->stream));
+    if (!P->wdiag) MVTV_TRY(alloc(&P->wdiag, P->g.N));
+    HIP_TRY(launch_scatter_sums(P->stream, key.get<uint32_t>(), dy.get<double>(), n, P->g.N, P->oty, P->wdiag,
+                                runs.get<unsigned long long>()));
+    unsigned long long hit = 0;
+    HIP_TRY(hipMemcpy(&hit, runs.p, sizeof(hit), hipMemcpyDeviceToHost));
+    // every node exactly one point <=> n == N and N nodes hit: W = I (the spectral solve applies)
+    if (uint64_t(n) == uint64_t(P->g.N) && hit == uint64_t(P->g.N)) {
+        P->wmode = W_IDENTITY;
+        P->wmean = 1.0;
+    } else {
+        P->wmode = W_DIAG;
+        P->wmean = double(n) / double(P->g.N);
+    }
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_predict(mvtv_problem* P, const double* axes, const double* data, int64_t n, double* fits) {
+    if (!P || !axes || n < 0 || (n > 0 && (!data || !fits))) return fail(MVTV_BAD_ARG, "null argument");
+    if (n == 0) return MVTV_OK;
+    DeviceGuard dg(P->device);
+    TmpDev key, idx, out;
+    MVTV_TRY(nearest_on_device(P, axes, data, n, key, idx, true));
+    HIP_TRY(hipMalloc(&out.p, size_t(n) * sizeof(double)));
+    HIP_TRY(launch_gather_index(P->stream, P->theta, idx.get<int64_t>(), n, out.get<double>()));
+    HIP_TRY(hipMemcpyAsync(fits, out.p, size_t(n) * sizeof(double), hipMemcpyDeviceToHost, P->stream));
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    return MVTV_OK;
+}
+
 // ------------------------------------------------------------------------------ operators
 mvtv_status mvtv_apply_D(mvtv_problem* P, const double* theta, double* d_out) {
     if (!P || !theta || !d_out) return fail(MVTV_BAD_ARG, "null argument");

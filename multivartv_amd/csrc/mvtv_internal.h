@@ -223,4 +223,11 @@ hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, c
                            int* nparts, const AdmmCtl* ctl = nullptr);
 hipError_t launch_gather_index(hipStream_t s, const double* theta, const int64_t* idx, int64_t n, double* out);
 
+// scattered-data setup (mvtv_scatter.hip)
+// axes_host_span[j] = axis_j[last] - axis_j[0] (host values; only the first guess of the bracket)
+hipError_t launch_nearest(hipStream_t s, int p, const uint32_t* m, const double* axes, const double* axes_host_span,
+                          const double* data, int64_t n, uint32_t* key, int64_t* idx_out);
+hipError_t launch_scatter_sums(hipStream_t s, uint32_t* key, const double* y, int64_t n, uint32_t N, double* oty,
+                               double* wdiag, unsigned long long* nruns);
+
 }  // namespace mvtv

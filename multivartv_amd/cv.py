@@ -48,9 +48,31 @@ def create_lambdas(n_lambda: int, problem: "_lib.Problem", lambdas=None) -> np.n
     return np.exp(np.linspace(np.log(lmax * 0.0001), np.log(lmax), int(n_lambda)))[::-1].copy()
 
 
-def _cache(mesh, m, deltas, x, yy, device, problem=None):
-    """create_cache_objects (rcpp…/solvers.cpp:36-44): O from the nearest mesh point -> W, O^T y."""
+def tensor_axes(mesh, m):
+    """The sorted axes of a column-major tensor mesh (create_mesh's layout), or None for any other mesh."""
+    mesh = np.asarray(mesh, dtype=np.float64)
+    if mesh.size != int(np.prod(m)) * len(m):
+        return None
+    mesh = mesh.reshape(int(np.prod(m)), len(m))
+    strides = np.cumprod([1] + list(m[:-1]))
+    axes = [mesh[strides[j] * np.arange(m[j]), j] for j in range(len(m))]
+    if any(np.any(np.diff(a) <= 0) for a in axes):
+        return None
+    grids = np.meshgrid(*axes, indexing="ij")
+    ok = all(np.array_equal(g.reshape(-1, order="F"), mesh[:, j]) for j, g in enumerate(grids))
+    return axes if ok else None
+
+
+def _cache(mesh, m, deltas, x, yy, device, problem=None, axes=None):
+    """create_cache_objects (rcpp…/solvers.cpp:36-44): O from the nearest mesh point -> W, O^T y.
+
+    On a tensor mesh (always, for create_mesh) O, diag(O^T O) and O^T y are built on the GPU
+    (Problem.set_scattered); any other mesh is matched on the host."""
     N = int(np.prod(m))
+    if axes is not None:
+        if problem is None:
+            problem = _lib.Problem(m, np.zeros(N), deltas=deltas, order=_lib.ORDER_CPP, weighted=True, device=device)
+        return problem, problem.set_scattered(axes, x, yy)
     idx = nearest_index(x, mesh)
     W, oty = interp_weights(idx, N, yy)
     wdiag = None if np.all(W == 1.0) else W
@@ -125,9 +147,10 @@ def mbs_impl(data, y, m, mesh=None, n_lambda=100, ftrue=None, lambdas=None, fold
     foldinds = kfoldinds(len(y), folds, seed) if folds > 1 else None
 
     state = {}
+    AXES = tensor_axes(MESH, m)
 
     def problem_for(x, yy):
-        P, idx = _cache(MESH, m, deltas, x, yy, device, state.get("P"))
+        P, idx = _cache(MESH, m, deltas, x, yy, device, state.get("P"), AXES)
         state["P"] = P
         return P, idx
 
@@ -151,7 +174,7 @@ def mbs_impl(data, y, m, mesh=None, n_lambda=100, ftrue=None, lambdas=None, fold
         tr, te = foldinds != f, foldinds == f
         P, _ = problem_for(data[tr], y[tr])
         thetas, _ = mbs_path(P, LAMBDAS, y[tr].mean())
-        ti = nearest_index(data[te], MESH)
+        ti = P.nearest(AXES, data[te]) if AXES is not None else nearest_index(data[te], MESH)
         yt = y[te]
         return np.array([np.sum((th[ti] - yt) ** 2) / yt.size for th in thetas]), None
 

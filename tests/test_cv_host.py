@@ -85,3 +85,17 @@ def test_distributed_paths_match_serial():
     for r in res:
         assert np.allclose(r[2], serial["cv.mses"], rtol=0, atol=0)
         assert r[3] == serial["lambda_minmse_ind"]
+
+
+def test_tensor_axes_recovers_create_mesh_axes():
+    rng = np.random.default_rng(0)
+    x = rng.uniform(-1, 3, size=(50, 3))
+    m = [4, 5, 6]
+    mesh = cv.create_mesh(x, m)
+    axes = cv.tensor_axes(mesh, m)
+    assert axes is not None
+    for j in range(3):
+        np.testing.assert_array_equal(axes[j], np.linspace(x[:, j].min() - 1e-4, x[:, j].max() + 1e-4, m[j]))
+    assert cv.tensor_axes(mesh[::-1], m) is None            # not column-major
+    assert cv.tensor_axes(mesh[:-1], m) is None             # wrong size
+    assert cv.tensor_axes(rng.uniform(size=mesh.shape), m) is None
