@@ -94,4 +94,32 @@ double mbs_mse(const mbs_one_object& model, const vec& y);       // :172-175
 void mbs_path(const mat& data, const vec& y, const vec& m, const mat& mesh, const vec& lambdas, const vec& ftrue,
               mbs_object& output, mbs_cache& cache, bool verbose = false);
 
+// ---- cross-validation driver: rcpp…/solvers.cpp:186-376 ----------------------------------------
+// kfoldinds (rcpp…/utils.cpp:367-376): the labels i % k, permuted. The reference shuffles with R's
+// RNG (arma::shuffle), which cannot be reproduced outside R; here the permutation sorts a seeded
+// splitmix64 key per position, exactly as multivartv_amd.cv.kfoldinds does.
+std::vector<int> kfoldinds(int64_t n, int k, uint64_t seed = 0);
+// create_lambdas (:186-200): flipud(exp(linspace(log(1e-4 lmax), log(lmax), n))), lmax = lam_max_pinv
+// on the GPU (mvtv_lambda_max); `lambdas` (may be null) is returned as given
+vec create_lambdas(int n_lambda, mbs_cache& inits, const vec* lambdas, bool verbose = false);
+// test_mse (:278-288): MSE of each path model's predictions at (data, y)
+vec test_mse(const mat& data, const vec& y, const mbs_object& path, int n_lambda);
+// mbs_fit_optimal (:261-274): cold refit at the lambda of the smallest row mean of mse_mat
+void mbs_fit_optimal(const mat& data, const vec& y, const vec& m, mbs_one_object& best_model, const mat& mesh,
+                     const vec& lambdas, const mat& mse_mat, mbs_cache& cache, bool verbose = false);
+
+// mbs_impl's result list (:368-373); models = listPATH(final_path, lambdas) (:292-302)
+struct mbs_impl_result {
+    mbs_one_object best;          // data, fitted, m, mesh, theta_hat, y of the chosen model
+    vec residuals;                // y - fitted
+    vec lambdas;                  // the grid (models[i].lambda)
+    mbs_object final_path;        // models[i].theta_hat / fitted, mses[i] = models[i].mse
+    int64_t lambda_minmse_ind = 0;   // 1-based, as R
+    vec cv_mses;                  // "cv.mses"
+};
+// mbs_impl (:305-376). mesh, ftrue, lambdas may be null (R's NULL). seed: kfoldinds.
+mbs_impl_result mbs_impl(const mat& data, const vec& y, const vec& m, const mat* mesh, int n_lambda,
+                         const vec* ftrue, const vec* lambdas, int folds, bool verbose = false, uint64_t seed = 0,
+                         int device = 0);
+
 }  // namespace mvtv

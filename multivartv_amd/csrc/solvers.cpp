@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <limits>
 
 namespace mvtv {
@@ -177,6 +178,39 @@ void create_cache_objects(const mat& data, const vec& y, const mat& mesh, const 
     int64_t N = 1;
     for (auto v : dims) N *= v;
     if (mesh.n_rows != N) throw std::invalid_argument("mesh rows != prod(m)");
+    if (data.n_cols != int64_t(dims.size()) || int64_t(y.size()) != data.n_rows)
+        throw std::invalid_argument("data must be n x p and y of length n");
+    const auto axes = tensor_axes(mesh, dims);
+    const bool reuse = cache.prob && cache.ntheta == N;   // the same mesh (CV fold): new data only
+    if (!reuse) {
+        if (cache.prob) mvtv_problem_destroy(cache.prob);
+        cache.prob = nullptr;
+        mvtv_problem_desc d{};
+        d.p = int32_t(dims.size());
+        for (size_t j = 0; j < dims.size(); ++j) {
+            d.m[j] = dims[j];
+            d.deltas[j] = deltas[j];
+        }
+        d.block_order = MVTV_ORDER_CPP;
+        d.weighted = 1;
+        const vec zeros(size_t(N), 0.0);
+        d.oty = zeros.data();
+        d.device = device;
+        check(mvtv_problem_create(&d, &cache.prob));
+        cache.ntheta = N;
+        cache.rowsD = mvtv_problem_edges(cache.prob);
+    }
+    cache.oidx.assign(size_t(data.n_rows), 0);
+    if (!axes.empty()) {
+        // tensor mesh (create_mesh): O, O^T O and O^T y built on the GPU (mvtv_problem_set_scattered)
+        vec flat;
+        for (const auto& a : axes) flat.insert(flat.end(), a.begin(), a.end());
+        cache.oty.clear();
+        cache.w.clear();
+        check(mvtv_problem_set_scattered(cache.prob, flat.data(), data.v.data(), data.n_rows, y.data(),
+                                         cache.oidx.data()));
+        return;
+    }
     cache.oidx = nearest_index(data, mesh);
     cache.oty.assign(size_t(N), 0.0);
     cache.w.assign(size_t(N), 0.0);
@@ -184,26 +218,7 @@ void create_cache_objects(const mat& data, const vec& y, const mat& mesh, const 
         cache.oty[size_t(cache.oidx[i])] += y[i];
         cache.w[size_t(cache.oidx[i])] += 1.0;
     }
-    if (cache.prob && cache.ntheta == N) {             // same mesh (CV fold): new data only
-        check(mvtv_problem_set_data(cache.prob, cache.oty.data(), cache.w.data()));
-        return;
-    }
-    if (cache.prob) mvtv_problem_destroy(cache.prob);
-    cache.prob = nullptr;
-    mvtv_problem_desc d{};
-    d.p = int32_t(dims.size());
-    for (size_t j = 0; j < dims.size(); ++j) {
-        d.m[j] = dims[j];
-        d.deltas[j] = deltas[j];
-    }
-    d.block_order = MVTV_ORDER_CPP;
-    d.weighted = 1;
-    d.oty = cache.oty.data();
-    d.wdiag = cache.w.data();
-    d.device = device;
-    check(mvtv_problem_create(&d, &cache.prob));
-    cache.ntheta = N;
-    cache.rowsD = mvtv_problem_edges(cache.prob);
+    check(mvtv_problem_set_data(cache.prob, cache.oty.data(), cache.w.data()));
 }
 
 void admm_update(const vec& /*y*/, mbs_cache& inits, vec& theta_init, double lambda, bool verbose, vec& u_init,
@@ -300,6 +315,128 @@ void mbs_path(const mat& data, const vec& y, const vec& m, const mat& mesh, cons
         output.minmse = output.mses[best];
         output.minmse_lambda = lambdas[best];
     }
+}
+
+std::vector<int> kfoldinds(int64_t n, int k, uint64_t seed) {
+    std::vector<uint64_t> key(size_t(std::max<int64_t>(n, 0)));
+    for (int64_t i = 0; i < n; ++i) {
+        uint64_t z = seed * 0xD1B54A32D192ED03ull + uint64_t(i) + 0x9E3779B97F4A7C15ull;   // splitmix64
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        key[size_t(i)] = z ^ (z >> 31);
+    }
+    std::vector<int64_t> perm(key.size());
+    for (size_t i = 0; i < perm.size(); ++i) perm[i] = int64_t(i);
+    std::stable_sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return key[size_t(a)] < key[size_t(b)]; });
+    std::vector<int> out(perm.size());
+    for (size_t i = 0; i < perm.size(); ++i) out[i] = int(perm[i] % k);
+    return out;
+}
+
+vec create_lambdas(int n_lambda, mbs_cache& inits, const vec* lambdas, bool verbose) {
+    if (lambdas) return *lambdas;
+    double lmax = 0.0;
+    int32_t it = 0;
+    check(mvtv_lambda_max(inits.prob, &lmax, &it));
+    vec grid = linspace(std::log(lmax * 0.0001), std::log(lmax), n_lambda);
+    vec out(grid.size());
+    for (size_t i = 0; i < grid.size(); ++i) out[grid.size() - 1 - i] = std::exp(grid[i]);   // flipud
+    if (verbose) std::printf("Lambda_max = %g\n", lmax);
+    return out;
+}
+
+vec test_mse(const mat& data, const vec& y, const mbs_object& path, int n_lambda) {
+    vec mses(size_t(std::max(n_lambda, 0)), 0.0);
+    if (path.models.empty()) return mses;
+    // every model of a path shares the mesh: one nearest-node map for all predictions
+    const auto idx = nearest_index(data, path.models[0].mesh);
+    for (int i = 0; i < n_lambda && size_t(i) < path.models.size(); ++i) {
+        vec fits(idx.size());
+        for (size_t k = 0; k < idx.size(); ++k) fits[k] = path.models[size_t(i)].theta_hat[size_t(idx[k])];
+        mses[size_t(i)] = mse(fits, y);
+    }
+    return mses;
+}
+
+void mbs_fit_optimal(const mat& data, const vec& y, const vec& m, mbs_one_object& best_model, const mat& mesh,
+                     const vec& lambdas, const mat& mse_mat, mbs_cache& cache, bool verbose) {
+    size_t best = 0;
+    double bestv = std::numeric_limits<double>::infinity();
+    for (int64_t i = 0; i < mse_mat.n_rows; ++i) {   // rowmean, first minimum
+        double s = 0.0;
+        for (int64_t j = 0; j < mse_mat.n_cols; ++j) s += mse_mat(i, j);
+        s /= double(mse_mat.n_cols);
+        if (s < bestv) {
+            bestv = s;
+            best = size_t(i);
+        }
+    }
+    vec theta(size_t(cache.ntheta), mean(y));
+    vec u(size_t(cache.rowsD), 0.0);
+    double rho = lambdas[0] / 5.0;
+    if (verbose) std::printf("Best lambda = %g\n", lambdas[best]);
+    mbs_one(data, y, m, best_model, mesh, u, rho, theta, lambdas[best], cache, verbose);
+}
+
+mbs_impl_result mbs_impl(const mat& data, const vec& y, const vec& m, const mat* mesh, int n_lambda,
+                         const vec* ftrue, const vec* lambdas, int folds, bool verbose, uint64_t seed, int device) {
+    mbs_impl_result R;
+    const mat MESH = mesh ? *mesh : create_mesh(data, m);
+    const vec deltas = create_deltas(data, m);
+    mbs_cache cache;
+    create_cache_objects(data, y, MESH, m, deltas, cache, device);
+    R.lambdas = create_lambdas(n_lambda, cache, lambdas, verbose);
+    const int nl = int(R.lambdas.size());
+    const vec FTRUE = ftrue ? *ftrue : y;
+    mat mse_mat(nl, std::max(folds, 1));
+    if (folds <= 1) {
+        mbs_path(data, y, m, MESH, R.lambdas, FTRUE, R.final_path, cache, verbose);
+        const vec t = test_mse(data, y, R.final_path, nl);
+        for (int i = 0; i < nl; ++i) mse_mat(i, 0) = t[size_t(i)];
+        mbs_fit_optimal(data, y, m, R.best, MESH, R.lambdas, mse_mat, cache, verbose);
+        R.cv_mses = t;
+    } else {
+        const auto fi = kfoldinds(data.n_rows, folds, seed);
+        for (int f = 0; f < folds; ++f) {
+            int64_t ntr = 0, nte = 0;
+            for (int v : fi) (v == f ? nte : ntr) += 1;
+            mat trx(ntr, data.n_cols), tex(nte, data.n_cols);
+            vec tr_y, te_y;
+            for (int64_t i = 0, a = 0, b = 0; i < data.n_rows; ++i) {
+                if (fi[size_t(i)] != f) {
+                    for (int64_t j = 0; j < data.n_cols; ++j) trx(a, j) = data(i, j);
+                    tr_y.push_back(y[size_t(i)]);
+                    ++a;
+                } else {
+                    for (int64_t j = 0; j < data.n_cols; ++j) tex(b, j) = data(i, j);
+                    te_y.push_back(y[size_t(i)]);
+                    ++b;
+                }
+            }
+            create_cache_objects(trx, tr_y, MESH, m, deltas, cache, device);
+            mbs_object path;
+            mbs_path(trx, tr_y, m, MESH, R.lambdas, tr_y, path, cache, verbose);
+            if (verbose) std::printf("Fold Complete: %d\n", f);
+            const vec t = test_mse(tex, te_y, path, nl);
+            for (int i = 0; i < nl; ++i) mse_mat(i, f) = t[size_t(i)];
+        }
+        create_cache_objects(data, y, MESH, m, deltas, cache, device);
+        mbs_path(data, y, m, MESH, R.lambdas, y, R.final_path, cache, verbose);
+        R.cv_mses.assign(size_t(nl), 0.0);
+        for (int i = 0; i < nl; ++i) {
+            double s = 0.0;
+            for (int f = 0; f < folds; ++f) s += mse_mat(i, f);
+            R.cv_mses[size_t(i)] = s / double(folds);
+        }
+    }
+    size_t best = 0;
+    for (size_t i = 1; i < R.cv_mses.size(); ++i)
+        if (R.cv_mses[i] < R.cv_mses[best]) best = i;
+    R.lambda_minmse_ind = int64_t(best) + 1;
+    if (folds > 1) R.best = R.final_path.models[best];
+    R.residuals.resize(y.size());
+    for (size_t i = 0; i < y.size(); ++i) R.residuals[i] = y[i] - R.best.fitted[i];
+    return R;
 }
 
 }  // namespace mvtv

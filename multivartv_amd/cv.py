@@ -17,7 +17,8 @@ for a single path: contiguous lambda chunks per rank, cold-started at each chunk
 (theta = mean y, u = 0, rho = lambda_head / 5).
 
 kfoldinds: the reference shuffles with R's RNG through arma::shuffle, which cannot be reproduced
-outside R; here the same round-robin labels are permuted by numpy's PCG64 seeded with ``seed``.
+outside R; here the same round-robin labels are permuted by sorting a seeded splitmix64 key per
+position, identically in C++ (mvtv::kfoldinds) and Python.
 """
 from __future__ import annotations
 
@@ -35,9 +36,22 @@ def create_mesh(data, m, eps: float = 1e-4):
     return np.stack([g.reshape(-1, order="F") for g in grids], axis=1)
 
 
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
 def kfoldinds(n: int, k: int, seed: int = 0) -> np.ndarray:
-    """rcpp…/utils.cpp:367-376: labels i % k, shuffled (seeded PCG64 instead of R's RNG)."""
-    return np.random.default_rng(seed).permutation(np.arange(n) % k).astype(np.int64)
+    """rcpp…/utils.cpp:367-376: labels i % k, shuffled. The permutation sorts a seeded splitmix64 key
+    per position (stable), the same as the C++ host API's mvtv::kfoldinds (csrc/solvers.cpp)."""
+    with np.errstate(over="ignore"):
+        base = np.uint64(seed) * np.uint64(0xD1B54A32D192ED03)
+        key = _splitmix64(base + np.arange(n, dtype=np.uint64))
+    perm = np.argsort(key, kind="stable")
+    return (perm % k).astype(np.int64)
 
 
 def create_lambdas(n_lambda: int, problem: "_lib.Problem", lambdas=None) -> np.ndarray:
