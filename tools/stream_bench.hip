@@ -52,6 +52,44 @@ __global__ void k_3r3w_march(const double* __restrict__ a, const double* __restr
     }
 }
 
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
+__global__ void k_copy16(const dvec2* __restrict__ a, dvec2* __restrict__ b, size_t n2) {
+    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n2; i += size_t(gridDim.x) * blockDim.x)
+        b[i] = a[i] * 1.0000001;
+}
+
+__global__ void k_copy8_nt(const double* __restrict__ a, double* __restrict__ b, size_t n) {
+    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+        __builtin_nontemporal_store(a[i] * 1.0000001, b + i);
+}
+
+__global__ void k_copy16_nt(const dvec2* __restrict__ a, dvec2* __restrict__ b, size_t n2) {
+    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n2; i += size_t(gridDim.x) * blockDim.x)
+        __builtin_nontemporal_store(a[i] * 1.0000001, b + i);
+}
+
+__global__ void k_3r3w16(const dvec2* __restrict__ a, const dvec2* __restrict__ b, const dvec2* __restrict__ c,
+                         dvec2* __restrict__ d, dvec2* __restrict__ e, dvec2* __restrict__ f, size_t n2) {
+    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n2; i += size_t(gridDim.x) * blockDim.x) {
+        const dvec2 x = a[i], y = b[i], z = c[i];
+        d[i] = x + 0.5 * y;
+        e[i] = y - 0.25 * z;
+        f[i] = z + x;
+    }
+}
+
+// 8-B lanes, but a contiguous chunk per wave instead of grid-stride (each wave streams 8 KB runs)
+__global__ void k_copy8_chunk(const double* __restrict__ a, double* __restrict__ b, size_t n) {
+    const size_t per = 1024;
+    const size_t nchunk = n / per;
+    for (size_t c = blockIdx.x * size_t(blockDim.x / 64) + threadIdx.x / 64; c < nchunk; c += size_t(gridDim.x) * (blockDim.x / 64)) {
+        const size_t base = c * per + (threadIdx.x & 63);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) b[base + 64 * k] = a[base + 64 * k] * 1.0000001;
+    }
+}
+
 int main() {
     const int m = 512;
     const size_t n = size_t(m) * m * m;
@@ -81,6 +119,18 @@ int main() {
     };
     timeit("read_1", 8.0 * n, [&] { hipLaunchKernelGGL(k_read, dim3(grid), dim3(block), 0, 0, buf[0], n, out); });
     timeit("copy_1r1w", 16.0 * n, [&] { hipLaunchKernelGGL(k_copy, dim3(grid), dim3(block), 0, 0, buf[0], buf[1], n); });
+    timeit("copy16_1r1w", 16.0 * n, [&] {
+        hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(block), 0, 0, (const dvec2*)buf[0], (dvec2*)buf[1], n / 2);
+    });
+    timeit("copy8_nt", 16.0 * n, [&] { hipLaunchKernelGGL(k_copy8_nt, dim3(grid), dim3(block), 0, 0, buf[0], buf[1], n); });
+    timeit("copy16_nt", 16.0 * n, [&] {
+        hipLaunchKernelGGL(k_copy16_nt, dim3(grid), dim3(block), 0, 0, (const dvec2*)buf[0], (dvec2*)buf[1], n / 2);
+    });
+    timeit("copy8_chunk", 16.0 * n, [&] { hipLaunchKernelGGL(k_copy8_chunk, dim3(grid), dim3(block), 0, 0, buf[0], buf[1], n); });
+    timeit("grid_3r3w16", 48.0 * n, [&] {
+        hipLaunchKernelGGL(k_3r3w16, dim3(grid), dim3(block), 0, 0, (const dvec2*)buf[0], (const dvec2*)buf[1],
+                           (const dvec2*)buf[2], (dvec2*)buf[3], (dvec2*)buf[4], (dvec2*)buf[5], n / 2);
+    });
     timeit("grid_3r3w", 48.0 * n, [&] {
         hipLaunchKernelGGL(k_3r3w, dim3(grid), dim3(block), 0, 0, buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], n);
     });
