@@ -147,6 +147,14 @@ mvtv_status mvtv_admm(mvtv_problem* prob, const mvtv_admm_opts* opts, double lam
 mvtv_status mvtv_state_set(mvtv_problem* prob, const double* theta, const double* u, double rho);
 mvtv_status mvtv_state_get(mvtv_problem* prob, double* theta, double* u, double* rho);
 mvtv_status mvtv_admm_run(mvtv_problem* prob, const mvtv_admm_opts* opts, double lambda, mvtv_admm_stats* stats);
+/* mbs_path's lambda loop (rcpp…/solvers.cpp:204-222) in one call: from theta_init [N], the variant's
+ * u0 and rho_init, the ADMM state (theta, u, rho) is carried on the device from each lambda to the
+ * next (:217-219). thetas_out [n_lambda x N] (may be NULL): theta after each lambda, lambda-major.
+ * rhos_out, stats [n_lambda] (may be NULL). The state stays resident (mvtv_state_get reads the last).
+ * Returns MVTV_MAXITER when some lambda hit max_counter (the loop goes on, as B breaks and goes on). */
+mvtv_status mvtv_path(mvtv_problem* prob, const mvtv_admm_opts* opts, const double* lambdas, int32_t n_lambda,
+                      const double* theta_init, double rho_init, double* thetas_out, double* rhos_out,
+                      mvtv_admm_stats* stats);
 /* fitted values O theta for n points given their mesh index (fill_output_mbs_one, rcpp…/solvers.cpp:73) */
 mvtv_status mvtv_fitted(mvtv_problem* prob, const int64_t* mesh_index, int64_t n, double* fitted);
 

@@ -82,6 +82,8 @@ SIGNATURES = {
     "mvtv_state_set": (C.c_int, [C.c_void_p, _dp, _dp, C.c_double]),
     "mvtv_state_get": (C.c_int, [C.c_void_p, _dp, _dp, _dp]),
     "mvtv_admm_run": (C.c_int, [C.c_void_p, C.POINTER(AdmmOpts), C.c_double, C.POINTER(AdmmStats)]),
+    "mvtv_path": (C.c_int, [C.c_void_p, C.POINTER(AdmmOpts), _dp, C.c_int32, _dp, C.c_double, _dp, _dp,
+                            C.POINTER(AdmmStats)]),
     "mvtv_fitted": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_int64, _dp]),
     "mvtv_nearest": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, C.POINTER(C.c_int64)]),
     "mvtv_problem_set_scattered": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, _dp, C.POINTER(C.c_int64)]),
@@ -258,6 +260,22 @@ class Problem:
         if not (s == MVTV_OK or (s == MVTV_MAXITER and allow_maxiter)):
             _check(s)
         return st.as_dict()
+
+    def path(self, lambdas, theta_init, rho_init, variant=VARIANT_RCPP, want_thetas=True, **opts):
+        """mbs_path's warm-started lambda loop in one C call (mvtv_path): (thetas [n x N] or None,
+        rhos [n], stats list)."""
+        o = default_opts(variant, **opts)
+        lam = _f64(lambdas)
+        n = lam.size
+        th0 = _f64(theta_init, self.N)
+        thetas = np.empty((n, self.N)) if want_thetas else None
+        rhos = np.empty(n)
+        sts = (AdmmStats * max(n, 1))()
+        s = lib().mvtv_path(self._h, C.byref(o), _ptr(lam), n, _ptr(th0), float(rho_init),
+                            None if thetas is None else thetas.ctypes.data_as(_dp), _ptr(rhos), sts)
+        if s not in (MVTV_OK, MVTV_MAXITER):
+            _check(s)
+        return thetas, rhos, [sts[i].as_dict() for i in range(n)]
 
     def fitted(self, mesh_index):
         idx = np.ascontiguousarray(np.asarray(mesh_index, dtype=np.int64).ravel())

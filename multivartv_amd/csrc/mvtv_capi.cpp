@@ -1119,6 +1119,25 @@ mvtv_status mvtv_admm(mvtv_problem* P, const mvtv_admm_opts* opts, double lambda
     return s;
 }
 
+mvtv_status mvtv_path(mvtv_problem* P, const mvtv_admm_opts* opts, const double* lambdas, int32_t n_lambda,
+                      const double* theta_init, double rho_init, double* thetas_out, double* rhos_out,
+                      mvtv_admm_stats* stats) {
+    if (!P || !opts || !theta_init || n_lambda < 0 || (n_lambda > 0 && !lambdas))
+        return fail(MVTV_BAD_ARG, "null argument");
+    MVTV_TRY(mvtv_state_set(P, theta_init, nullptr, rho_init));
+    mvtv_status worst = MVTV_OK;
+    for (int32_t i = 0; i < n_lambda; ++i) {
+        mvtv_admm_stats st{};
+        const mvtv_status s = mvtv_admm_run(P, opts, lambdas[i], &st);
+        if (s == MVTV_MAXITER) worst = MVTV_MAXITER;
+        else if (s != MVTV_OK) return s;
+        if (stats) stats[i] = st;
+        if (thetas_out) MVTV_TRY(mvtv_state_get(P, thetas_out + size_t(i) * P->g.N, nullptr, nullptr));
+        if (rhos_out) rhos_out[i] = P->rho;
+    }
+    return worst;
+}
+
 mvtv_status mvtv_fitted(mvtv_problem* P, const int64_t* mesh_index, int64_t n, double* fitted) {
     if (!P || (n > 0 && (!mesh_index || !fitted))) return fail(MVTV_BAD_ARG, "null argument");
     if (n == 0) return MVTV_OK;

@@ -98,17 +98,13 @@ def _cache(mesh, m, deltas, x, yy, device, problem=None, axes=None):
 
 
 def mbs_path(problem: "_lib.Problem", lambdas, ymean: float, theta0=None, rho0=None):
-    """rcpp…/solvers.cpp:204-222 on the resident state: returns (thetas, stats) per lambda."""
+    """rcpp…/solvers.cpp:204-222 on the resident state (one mvtv_path call): returns (thetas, stats)
+    per lambda."""
     lambdas = np.asarray(lambdas, dtype=np.float64)
     th0 = np.full(problem.N, float(ymean)) if theta0 is None else theta0
-    problem.state_set(th0, None, float(lambdas[0]) / 5.0 if rho0 is None else float(rho0))   # u0 = 0 (B)
-    thetas, stats = [], []
-    for lam in lambdas:
-        st = problem.run(float(lam))
-        th, _, _ = problem.state_get(want_u=False)
-        thetas.append(th)
-        stats.append(st)
-    return thetas, stats
+    r0 = float(lambdas[0]) / 5.0 if rho0 is None else float(rho0)   # u0 = 0 (B)
+    thetas, _, stats = problem.path(lambdas, th0, r0)
+    return list(thetas), stats
 
 
 def _dist(group):

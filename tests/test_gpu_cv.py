@@ -105,3 +105,24 @@ def test_mbs_impl_two_ranks_match_serial():
         assert np.array_equal(np.array(r[1]), serial["cv.mses"])
         assert r[2] == serial["lambda_minmse_ind"]
     assert np.array_equal(np.array(res[0][3]), serial["theta_hat"])
+
+
+def test_mvtv_path_equals_per_lambda_runs():
+    """mvtv_path (one C call) against state_set + one mvtv_admm_run per lambda: bit-identical."""
+    x, y = _scattered(600, 2, seed=21)
+    m = [16, 12]
+    mesh = cv.create_mesh(x, m)
+    deltas = O.create_deltas_rcpp(x, m)
+    idx = O.nearest_index(x, mesh)
+    N = int(np.prod(m))
+    W = np.bincount(idx, minlength=N).astype(float)
+    oty = np.bincount(idx, weights=y, minlength=N)
+    lams = np.exp(np.linspace(np.log(1.0), np.log(0.01), 6))
+    with mv.Problem(m, oty, wdiag=W, deltas=deltas, order=mv.ORDER_CPP) as P:
+        th, rhos, st = P.path(lams, np.full(N, y.mean()), lams[0] / 5)
+        P.state_set(np.full(N, y.mean()), None, lams[0] / 5)
+        for i, lam in enumerate(lams):
+            s = P.run(float(lam))
+            t, _, r = P.state_get(want_u=False)
+            np.testing.assert_array_equal(th[i], t)
+            assert rhos[i] == r and st[i]["iters"] == s["iters"]

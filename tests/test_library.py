@@ -10,6 +10,7 @@ import pytest
 
 import multivartv_amd as mv
 from multivartv_amd import _lib
+from multivartv_amd import slab  # noqa: F401  (registers the slab entry points in _lib.SIGNATURES)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "mvtv", "mvtv.h")
