@@ -699,9 +699,30 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
 }
 
 // ------------------------------------------------------------------------------ launcher
+// strided (d > 0) passes of long lines: twice the default tile (one 148-KB workgroup per CU) so a
+// line position is a 64-B (L = 11) / 128-B (L = 10) row instead of 32 / 64 B. 2-D 2048^2: the two
+// strided passes 49 -> 28 us, 3670 -> 4320 ADMM it/s (MVTV_DCT_WIDE=0 restores the default tile)
+template <int L>
+constexpr int wide_tq() { return (L >= 10 && L <= 12) ? 2 * spec8::Shape<L>::TQ : 0; }
+
 template <int L>
 static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
     using S = spec8::Shape<L>;
+    if constexpr (wide_tq<L>() > 0) {
+        static const bool wide = [] {
+            const char* e = std::getenv("MVTV_DCT_WIDE");
+            return !e || std::atoi(e) != 0;
+        }();
+        if (wide && !d0 && a.tq == S::TQ && uint32_t(wide_tq<L>()) <= a.stride) {
+            constexpr int TW = wide_tq<L>();
+            a.tq = TW;
+            const dim3 grid((a.nlines + uint32_t(TW) - 1) / uint32_t(TW)), block(spec8::ShapeK<L, TW>::NT);
+            if (mode == SPEC_FWD) klaunch(k_dct8<L, SPEC_FWD, false, false, TW>, grid, block, 0, s, a);
+            else if (mode == SPEC_INV) klaunch(k_dct8<L, SPEC_INV, false, false, TW>, grid, block, 0, s, a);
+            else klaunch(k_dct8<L, SPEC_MID, false, false, TW>, grid, block, 0, s, a);
+            return;
+        }
+    }
     // tile size: 16 lines (128-B rows for d > 0) measured best; 8 lines (64-B rows) cost +50 % per
     // pass and 32 lines (one 150-KB workgroup per CU) +6 % at 512^3
     const dim3 grid((a.nlines + uint32_t(a.tq) - 1) / uint32_t(a.tq)), block(S::NT);
