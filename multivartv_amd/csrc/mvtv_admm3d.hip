@@ -269,6 +269,10 @@ hipError_t launch_edge4d(const Geom& g, int order, int umode, hipStream_t s, con
 hipError_t launch_gather4d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                            double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
                            int* nparts, const AdmmCtl* ctl);
+bool gather4_ok(const Geom& g);
+hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
+                          double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
+                          int* nparts, const AdmmCtl* ctl, double* scratch);
 
 bool edge3d_ok(const Geom& g) {
     if (g.p == 4) return edge4d_ok(g);
@@ -320,8 +324,11 @@ hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, con
 
 hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                            double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
-                           int* nparts, const AdmmCtl* ctl) {
+                           int* nparts, const AdmmCtl* ctl, double* scratch4) {
     if (g.p == 4) {
+        if (scratch4 && gather4_ok(g))
+            return launch_gather4(g, order, umode, s, edges, t, g_alpha, g_u, g_uprev, c_prev, partials, nparts, ctl,
+                                  scratch4);
         // 4-D: the marching gather (k_gather4d) reads ~65 neighbour words per cell through L1/L2 and
         // measured slower at 128^4 (20.8 vs 18.4 ms) than the grid-stride kernel; opt-in only
         static const bool marching = std::getenv("MVTV_G4D") != nullptr;
@@ -981,6 +988,242 @@ hipError_t launch_gather4d(const Geom& g, int order, int umode, hipStream_t s, c
     }
     if (umode == U_EXPLICIT) return prev ? go(k_gather4d<1, U_EXPLICIT, true, 15>) : go(k_gather4d<1, U_EXPLICIT, false, 15>);
     return prev ? go(k_gather4d<1, U_FROM_Z, true, 15>) : go(k_gather4d<1, U_FROM_Z, false, 15>);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 4-D gather in two passes (default for p = 4). D^T is separable per block: the dim-3 (w) backward
+// difference factors out, D^T(alpha) = G0 + (1 - s_w) Gw, where G0 / Gw sum the (x, y, z) gathers
+// of the blocks without / with dim 3 in S'. Pass A marches dim 2 at a fixed w like k_gather3d
+// (x-1, y-1 from L1/L2, z-1 from carried sums) and writes G0 and Gw (alpha and u parts); pass B
+// walks w with Gw(w-1) in registers and forms g_alpha, g_u and the dual-residual sums. Both passes
+// stream; no neighbour along dim 3 (16 MB away at 128^4) is ever re-read from HBM.
+struct Gather4Args {
+    Geom g;
+    const double* edges;
+    double* s0a;     // G0 alpha / u and Gw alpha / u: 4 N-arrays of scratch
+    double* s0u;
+    double* swa;
+    double* swu;
+    double* g_alpha;
+    double* g_u;
+    const double* g_uprev;
+    double* partials;
+    double t, c_prev;
+    const AdmmCtl* ctl;
+    int tiles_x, tiles_y, zchunk, nzc, nblocks, wa, wb;   // pass A: planes w in [wa, wb)
+    int wlo, whi, wchunk, nwc, n3, nblocks_b;            // pass B: owned planes [wlo, whi)
+};
+namespace g4 {
+constexpr int TX = 64, TY = 4, NT = TX * TY, NTB = 256;
+}
+
+template <int ORD, int UM, int NB>
+__global__ __launch_bounds__(g4::NT) void k_gather4a(const Gather4Args a) {
+    constexpr int P = 4;
+    const Geom& g = a.g;
+    double tt = a.t;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        tt = a.ctl->t_next;
+    }
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    if (bid >= a.nblocks) return;
+    const int nt = a.tiles_x * a.tiles_y;
+    const int tw = bid / (nt * a.nzc);
+    int rem = bid - tw * nt * a.nzc;
+    const int tz = rem / nt;
+    rem -= tz * nt;
+    const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
+    const int x = tx * g4::TX + int(threadIdx.x & 63), y = ty * g4::TY + int(threadIdx.x >> 6);
+    const int w = a.wa + tw;
+    const int z0 = tz * a.zchunk, z1 = min(int(g.m[2]), z0 + a.zchunk);
+    if (x >= int(g.m[0]) || y >= int(g.m[1])) return;
+    const uint32_t m0 = g.m[0], m01 = g.m[0] * g.m[1], pl = m01 * g.m[2];
+    const bool okx = x > 0, oky = y > 0;
+    const uint32_t base = uint32_t(w) * pl + uint32_t(y) * m0 + uint32_t(x);
+    const uint32_t qoff[4] = {0u, okx ? 1u : 0u, oky ? m0 : 0u, (okx ? 1u : 0u) + (oky ? m0 : 0u)};
+    const bool qok[4] = {true, okx, oky, okx && oky};
+    double qa_prev[NB], qu_prev[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) qa_prev[k] = qu_prev[k] = 0.0;
+    auto plane_q = [&](auto kc, int e, double& qa, double& qu) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+        constexpr int SI = S & 3;
+        const double* eb = a.edges + uint64_t(k) * g.N + uint32_t(e) * m01 + base;
+        qa = 0.0;
+        qu = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if ((q & ~SI) != 0) continue;
+            const double vv = *(eb - qoff[q]);
+            const double v = qok[q] ? vv : 0.0;
+            const bool neg = __builtin_popcount(q) & 1;
+            if constexpr (UM == U_FROM_Z) {
+                const double cl = clampd(v, tt);
+                const double al = v - cl;
+                qa = neg ? qa - al : qa + al;
+                qu = neg ? qu + cl : qu - cl;
+            } else {
+                qu = neg ? qu - v : qu + v;
+            }
+        }
+    };
+    if (z0 > 0) {
+        static_for<0, NB>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+            if constexpr ((S & 4) != 0) plane_q(kc, z0 - 1, qa_prev[k], qu_prev[k]);
+        });
+    }
+    for (int e = z0; e < z1; ++e) {
+        double a0 = 0.0, u0 = 0.0, aw = 0.0, uw = 0.0;
+        static_for<0, NB>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+            double qa, qu;
+            plane_q(kc, e, qa, qu);
+            double ca = qa, cu = qu;
+            if constexpr ((S & 4) != 0) {
+                ca -= qa_prev[k];
+                cu -= qu_prev[k];
+                qa_prev[k] = qa;
+                qu_prev[k] = qu;
+            }
+            if constexpr ((S & 8) != 0) {
+                aw = fma(g.w[k], ca, aw);
+                uw = fma(g.w[k], cu, uw);
+            } else {
+                a0 = fma(g.w[k], ca, a0);
+                u0 = fma(g.w[k], cu, u0);
+            }
+        });
+        const uint32_t i = uint32_t(e) * m01 + base;
+        if constexpr (UM == U_FROM_Z) {
+            __builtin_nontemporal_store(a0, a.s0a + i);
+            __builtin_nontemporal_store(aw, a.swa + i);
+        }
+        __builtin_nontemporal_store(u0, a.s0u + i);
+        __builtin_nontemporal_store(uw, a.swu + i);
+    }
+}
+
+template <int UM, bool PREV>
+__global__ __launch_bounds__(g4::NTB) void k_gather4b(const Gather4Args a) {
+    double c_prev = a.c_prev;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        c_prev = a.ctl->c_prev;
+    }
+    double red[GR_N] = {0.0, 0.0, 0.0};
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const int per = (a.n3 + g4::NTB - 1) / g4::NTB;   // workgroups per w-chunk
+    const int wc = bid / per;
+    const int i3 = (bid - wc * per) * g4::NTB + int(threadIdx.x);
+    if (bid < a.nblocks_b && i3 < a.n3) {
+        const uint32_t pl = uint32_t(a.n3);
+        const int w0 = a.wlo + wc * a.wchunk, w1 = min(a.whi, w0 + a.wchunk);
+        double pa = 0.0, pu = 0.0;   // Gw at plane w - 1 (zero below the mesh)
+        if (w0 > 0) {
+            const uint32_t j = uint32_t(w0 - 1) * pl + uint32_t(i3);
+            if constexpr (UM == U_FROM_Z) pa = a.swa[j];
+            pu = a.swu[j];
+        }
+        for (int w = w0; w < w1; ++w) {
+            const uint32_t i = uint32_t(w) * pl + uint32_t(i3);
+            double ga = 0.0, wa_ = 0.0;
+            if constexpr (UM == U_FROM_Z) {
+                wa_ = __builtin_nontemporal_load(a.swa + i);
+                ga = __builtin_nontemporal_load(a.s0a + i) + (wa_ - pa);
+                pa = wa_;
+            }
+            const double wu = __builtin_nontemporal_load(a.swu + i);
+            const double gu = __builtin_nontemporal_load(a.s0u + i) + (wu - pu);
+            pu = wu;
+            if constexpr (UM == U_FROM_Z) __builtin_nontemporal_store(ga, a.g_alpha + i);
+            __builtin_nontemporal_store(gu, a.g_u + i);
+            red[GR_GU2] = fma(gu, gu, red[GR_GU2]);
+            if constexpr (PREV) {
+                const double gp = c_prev * __builtin_nontemporal_load(a.g_uprev + i);
+                const double db = gu - gp, da = ga + gp;
+                red[GR_S2B] = fma(db, db, red[GR_S2B]);
+                red[GR_S2A] = fma(da, da, red[GR_S2A]);
+            }
+        }
+    }
+    block_reduce_store<GR_N, 0, g4::NTB>(red, a.partials);
+}
+
+bool gather4_ok(const Geom& g) {
+    if (g.p != 4 || std::getenv("MVTV_G4D") || std::getenv("MVTV_G4_OFF")) return false;
+    const uint32_t pl = g.m[0] * g.m[1] * g.m[2];
+    const int nwp = int(g.iend / pl) - int(g.ibeg / pl);
+    const int per = int((pl + g4::NTB - 1) / g4::NTB);
+    // pass B: at least one w-chunk per workgroup row, within the partials buffer
+    return per <= kMaxCgBlocks && nwp >= 1;
+}
+
+hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
+                          double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
+                          int* nparts, const AdmmCtl* ctl, double* scratch) {
+    Gather4Args a{};
+    a.g = g;
+    a.edges = edges;
+    a.s0a = scratch;
+    a.s0u = scratch + size_t(g.N);
+    a.swa = scratch + 2 * size_t(g.N);
+    a.swu = scratch + 3 * size_t(g.N);
+    a.g_alpha = g_alpha;
+    a.g_u = g_u;
+    a.g_uprev = g_uprev;
+    a.partials = partials;
+    a.t = t;
+    a.c_prev = c_prev;
+    a.ctl = ctl;
+    const uint32_t pl = g.m[0] * g.m[1] * g.m[2];
+    a.wlo = int(g.ibeg / pl);
+    a.whi = int(g.iend / pl);
+    a.wa = std::max(0, a.wlo - 1);   // Gw of the plane below the owned range (slab ghost) too
+    a.wb = a.whi;
+    a.tiles_x = int((g.m[0] + g4::TX - 1) / g4::TX);
+    a.tiles_y = int((g.m[1] + g4::TY - 1) / g4::TY);
+    const int per_w = a.tiles_x * a.tiles_y;
+    const int nw = a.wb - a.wa;
+    a.nzc = std::max(1, std::min(int(g.m[2]), 8192 / std::max(1, per_w * nw)));
+    a.zchunk = int((g.m[2] + a.nzc - 1) / a.nzc);
+    a.nzc = int((g.m[2] + a.zchunk - 1) / a.zchunk);
+    a.nblocks = per_w * a.nzc * nw;
+    // pass B: w-chunks so that the grid fills the chip a few times, within the partials rows
+    a.n3 = int(pl);
+    const int per = (a.n3 + g4::NTB - 1) / g4::NTB;
+    const int nwo = std::max(1, a.whi - a.wlo);
+    a.nwc = std::max(1, std::min(nwo, std::min(4096, kMaxCgBlocks) / std::max(1, per)));
+    a.wchunk = (nwo + a.nwc - 1) / a.nwc;
+    a.nwc = (nwo + a.wchunk - 1) / a.wchunk;
+    a.nblocks_b = per * a.nwc;
+    const bool expl = umode == U_EXPLICIT;
+    auto goa = [&](auto kern) {
+        klaunch(kern, dim3((a.nblocks + 7) / 8 * 8), dim3(g4::NT), 0, s, a);
+        return hipGetLastError();
+    };
+    hipError_t e;
+    if (order == 0) e = expl ? goa(k_gather4a<0, U_EXPLICIT, 15>) : goa(k_gather4a<0, U_FROM_Z, 15>);
+    else if (g.nb == 14) e = expl ? goa(k_gather4a<1, U_EXPLICIT, 14>) : goa(k_gather4a<1, U_FROM_Z, 14>);
+    else e = expl ? goa(k_gather4a<1, U_EXPLICIT, 15>) : goa(k_gather4a<1, U_FROM_Z, 15>);
+    if (e != hipSuccess) return e;
+    if (g_timed_b.start) {   // the caller timed both passes
+        g_timed = g_timed_b;
+        g_timed_b = TimedLaunch{};
+    }
+    const int gridb = (a.nblocks_b + 7) / 8 * 8;
+    *nparts = gridb;
+    const bool prev = g_uprev != nullptr;
+    auto gob = [&](auto kern) {
+        klaunch(kern, dim3(gridb), dim3(g4::NTB), 0, s, a);
+        return hipGetLastError();
+    };
+    if (expl) return prev ? gob(k_gather4b<U_EXPLICIT, true>) : gob(k_gather4b<U_EXPLICIT, false>);
+    return prev ? gob(k_gather4b<U_FROM_Z, true>) : gob(k_gather4b<U_FROM_Z, false>);
 }
 
 }  // namespace mvtv

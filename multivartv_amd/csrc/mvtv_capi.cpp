@@ -83,6 +83,7 @@ struct mvtv_problem {
     bool f3d = false;             // fused 3-D edge update + gather (needs the second edge buffer)
     double* edges2 = nullptr;     // ping-pong partner of edges for the fused kernel
     double* pcg_b = nullptr;      // right-hand side of the spectrally preconditioned PCG
+    double* g4 = nullptr;         // 4 N-arrays: the two-pass 4-D gather's partial sums
     double wmean = 1.0;           // mean(W): the preconditioner's identity weight
     AdmmCtl* ctl = nullptr;       // device control block of the asynchronous ADMM loop
     AdmmCtl* host_ctl = nullptr;  // pinned mirror
@@ -136,6 +137,18 @@ struct mvtv_problem {
         if (h >= 0 && g_timed.start) pending[h].kid = -1;   // the launcher enqueued nothing
         g_timed = TimedLaunch{};
     }
+    // second launch of a two-kernel launcher (armed in g_timed_b, moved to g_timed by the launcher)
+    int tstart_b(int kid) {
+        if (!timing) return -1;
+        Pending pd{get_event(), get_event(), kid};
+        g_timed_b = TimedLaunch{pd.a, pd.b};
+        pending.push_back(pd);
+        return int(pending.size()) - 1;
+    }
+    void tstop_b(int h) {
+        if (h >= 0 && g_timed_b.start) pending[h].kid = -1;
+        g_timed_b = TimedLaunch{};
+    }
     void harvest() {  // call after a stream sync
         for (auto& pd : pending) {
             float t = 0.f;
@@ -178,7 +191,7 @@ mvtv_status alloc(double** ptr, size_t n) {
 void free_all(mvtv_problem* P) {
     double** bufs[] = {&P->oty, &P->wdiag, &P->theta, &P->edges, &P->ga, &P->gu, &P->guprev, &P->r,
                        &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->scratch,
-                       &P->edges2, &P->pcg_b};
+                       &P->edges2, &P->pcg_b, &P->g4};
     for (double** b : bufs)
         if (*b) {
             (void)hipFree(*b);
@@ -646,6 +659,7 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
     }
     if (P->spec_mesh) s = spectral_plan(P);
     P->e3d = edge3d_ok(g);
+    if (s == MVTV_OK && P->e3d && g.p == 4 && gather4_ok(g)) s = alloc(&P->g4, 4 * size_t(N));
     P->f3d = !sl && fused3d_ok(g);
     if (s == MVTV_OK) s = mvtv_problem_set_data(P, d->oty, d->wdiag);
     if (s != MVTV_OK) {
@@ -797,7 +811,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         int np0 = L.grid;
         if (P->e3d)
             HIP_TRY(launch_gather3d(P->g, P->order, U_EXPLICIT, P->stream, P->edges, 0.0, nullptr, gprev, nullptr, 1.0,
-                                    P->partials, &np0));
+                                    P->partials, &np0, nullptr, P->g4));
         else
             HIP_TRY(launch_gather(P->g, P->order, U_EXPLICIT, L, P->edges, 0.0, nullptr, gprev, nullptr, 1.0,
                                   P->partials));
@@ -886,14 +900,16 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
             HIP_TRY(launch_finalize(P->stream, P->partials, npe, ER_N, 1, 0, P->red, P->st, 0.0, 0, P->ctl));
             P->tstop(hh);
             hh = P->tstart(MVTV_K_GATHER);
+            const int hb = P->tstart_b(MVTV_K_GATHER4B);
             int npg = L.grid;
             if (P->e3d)
                 HIP_TRY(launch_gather3d(P->g, P->order, U_FROM_Z, P->stream, P->edges, 0.0, P->ga, gn, gp, 1.0,
-                                        P->partials, &npg, P->ctl));
+                                        P->partials, &npg, P->ctl, P->g4));
             else
                 HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, L, P->edges, 0.0, P->ga, gn, gp, 1.0, P->partials,
                                       P->ctl));
             P->tstop(hh);
+            P->tstop_b(hb);
             hh = P->tstart(MVTV_K_REDUCE);
             HIP_TRY(launch_finalize(P->stream, P->partials, npg, GR_N, 0, 0, P->red + ER_N, P->st, 0.0, 0, P->ctl));
             HIP_TRY(launch_admm_control(P->stream, P->ctl, P->red));
@@ -1020,13 +1036,15 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
             t_z = t_new;
             // ---- D^T alpha, D^T u and the dual residual norms ---------------------------------------
             h = P->tstart(MVTV_K_GATHER);
+            const int hb = P->tstart_b(MVTV_K_GATHER4B);
             np = L.grid;
             if (P->e3d)
                 HIP_TRY(launch_gather3d(P->g, P->order, U_FROM_Z, P->stream, P->edges, t_z, P->ga, gnew, gprev, c_prev,
-                                        P->partials, &np));
+                                        P->partials, &np, nullptr, P->g4));
             else
                 HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, L, P->edges, t_z, P->ga, gnew, gprev, c_prev, P->partials));
             P->tstop(h);
+            P->tstop_b(hb);
             h = P->tstart(MVTV_K_REDUCE);
             HIP_TRY(launch_finalize(P->stream, P->partials, np, GR_N, 0, 0, P->red + ER_N, P->st));
             P->tstop(h);
@@ -1548,7 +1566,7 @@ mvtv_status mvtv_slab_gather(mvtv_problem* P, int32_t umode, double t, double c_
     const int h = P->tstart(MVTV_K_GATHER);
     if (P->e3d)
         HIP_TRY(launch_gather3d(P->g, P->order, umode, P->stream, P->edges, t, expl ? nullptr : P->ga, gout, gprev,
-                                c_prev, P->partials, &np));
+                                c_prev, P->partials, &np, nullptr, P->g4));
     else
         HIP_TRY(launch_gather(P->g, P->order, umode, L, P->edges, t, expl ? nullptr : P->ga, gout, gprev, c_prev,
                               P->partials));
@@ -1631,7 +1649,10 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
     double b = 0.0;
     switch (kid) {
         case MVTV_K_EDGE_UPDATE: b = 8.0 * (N + 2.0 * E); break;        // theta in, z in/out
-        case MVTV_K_GATHER: b = 8.0 * (E + 3.0 * N); break;             // z in, g_uprev in, g_alpha/g_u out
+        case MVTV_K_GATHER:   // z in, g_uprev in, g_alpha/g_u out; 4-D two-pass: z in, 4 partial sums out
+            b = P->g4 ? 8.0 * (E + 4.0 * N) : 8.0 * (E + 3.0 * N);
+            break;
+        case MVTV_K_GATHER4B: b = 8.0 * 7.0 * N; break;                // 4 partial sums, g_uprev in; g_alpha/g_u out
         case MVTV_K_PCG_INIT:   // classic: oty, ga, gb, x (+W) in, r, p out; fused 3-D: r out only
             b = 8.0 * (((P->g.p == 3 && P->fused3d) ? 5.0 : 6.0) + w) * N;
             break;
@@ -1653,7 +1674,7 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
 const char* mvtv_kernel_name(int32_t kid) {
     static const char* names[MVTV_K_COUNT] = {"edge_update", "gather_Dt", "pcg_init", "pcg_apply_A",
                                                "pcg_update", "pcg_direction", "reduce", "other", "pcg_fused3d",
-                                               "dct_first", "dct", "admm_fused"};
+                                               "dct_first", "dct", "admm_fused", "gather4_b"};
     return (kid >= 0 && kid < MVTV_K_COUNT) ? names[kid] : "?";
 }
 

@@ -128,6 +128,7 @@ struct TimedLaunch {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 extern thread_local TimedLaunch g_timed;
+extern thread_local TimedLaunch g_timed_b;   // a two-kernel launcher's second launch
 
 template <typename F, typename... Args>
 inline void klaunch(F kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, Args... args) {
@@ -218,9 +219,11 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
 hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
                          double t_old, double c_old, double t_new, const double* theta_old, double* partials,
                          int* nparts, const AdmmCtl* ctl = nullptr);
+// scratch4: 4 N-arrays for the two-pass 4-D gather (p = 4); nullptr selects the one-pass kernels
 hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                            double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
-                           int* nparts, const AdmmCtl* ctl = nullptr);
+                           int* nparts, const AdmmCtl* ctl = nullptr, double* scratch4 = nullptr);
+bool gather4_ok(const Geom& g);
 hipError_t launch_gather_index(hipStream_t s, const double* theta, const int64_t* idx, int64_t n, double* out);
 
 // scattered-data setup (mvtv_scatter.hip)

@@ -19,6 +19,7 @@
 namespace mvtv {
 
 thread_local TimedLaunch g_timed;
+thread_local TimedLaunch g_timed_b;
 
 // Jacobi diagonal of W + sigma * sum_S cS[S] (x)_{j in S} L_j at a node with multi-index c:
 // the 1-D Neumann Laplacian's diagonal is (c > 0) + (c < m - 1).

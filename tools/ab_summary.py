@@ -20,5 +20,5 @@ for d in sorted(glob.glob(os.path.join(root, "*")), key=lambda p: int(os.path.ba
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") == "FETCH_SIZE":
                 vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024 * 2)
-    out = {k: round(statistics.median(v) / 1e9, 3) for k, v in vals.items() if k in ("admm_fused", "dct", "dct_first")}
+    out = {k: round(statistics.median(v) / 1e9, 3) for k, v in vals.items() if k in ("admm_fused", "dct", "dct_first", "gather_Dt", "edge_update")}
     print(case, "FETCH GB (median per launch):", out)
