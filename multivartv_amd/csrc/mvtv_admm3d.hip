@@ -1043,9 +1043,9 @@ __global__ __launch_bounds__(g4::NT) void k_gather4a(const Gather4Args a) {
     const uint32_t base = uint32_t(w) * pl + uint32_t(y) * m0 + uint32_t(x);
     const uint32_t qoff[4] = {0u, okx ? 1u : 0u, oky ? m0 : 0u, (okx ? 1u : 0u) + (oky ? m0 : 0u)};
     const bool qok[4] = {true, okx, oky, okx && oky};
-    double qa_prev[NB], qu_prev[NB];
-#pragma unroll
-    for (int k = 0; k < NB; ++k) qa_prev[k] = qu_prev[k] = 0.0;
+    // the dim-2 difference is carried per output group, not per block: for each of G0 / Gw (alpha
+    // and u) the weighted in-plane sums of the blocks with dim 2 in S' at plane e - 1
+    double ca0 = 0.0, cu0 = 0.0, caw = 0.0, cuw = 0.0;
     auto plane_q = [&](auto kc, int e, double& qa, double& qu) {
         constexpr int k = decltype(kc)::value;
         constexpr int S = sprime_mask(block_code(k, P, ORD), P);
@@ -1073,31 +1073,48 @@ __global__ __launch_bounds__(g4::NT) void k_gather4a(const Gather4Args a) {
         static_for<0, NB>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-            if constexpr ((S & 4) != 0) plane_q(kc, z0 - 1, qa_prev[k], qu_prev[k]);
+            if constexpr ((S & 4) != 0) {
+                double qa, qu;
+                plane_q(kc, z0 - 1, qa, qu);
+                if constexpr ((S & 8) != 0) {
+                    caw = fma(g.w[k], qa, caw);
+                    cuw = fma(g.w[k], qu, cuw);
+                } else {
+                    ca0 = fma(g.w[k], qa, ca0);
+                    cu0 = fma(g.w[k], qu, cu0);
+                }
+            }
         });
     }
     for (int e = z0; e < z1; ++e) {
-        double a0 = 0.0, u0 = 0.0, aw = 0.0, uw = 0.0;
+        // this plane's sums: all blocks (s*) and those with dim 2 in S' (n*, carried to plane e + 1)
+        double sa0 = 0.0, su0 = 0.0, saw = 0.0, suw = 0.0, na0 = 0.0, nu0 = 0.0, naw = 0.0, nuw = 0.0;
         static_for<0, NB>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
             double qa, qu;
             plane_q(kc, e, qa, qu);
-            double ca = qa, cu = qu;
-            if constexpr ((S & 4) != 0) {
-                ca -= qa_prev[k];
-                cu -= qu_prev[k];
-                qa_prev[k] = qa;
-                qu_prev[k] = qu;
-            }
             if constexpr ((S & 8) != 0) {
-                aw = fma(g.w[k], ca, aw);
-                uw = fma(g.w[k], cu, uw);
+                saw = fma(g.w[k], qa, saw);
+                suw = fma(g.w[k], qu, suw);
+                if constexpr ((S & 4) != 0) {
+                    naw = fma(g.w[k], qa, naw);
+                    nuw = fma(g.w[k], qu, nuw);
+                }
             } else {
-                a0 = fma(g.w[k], ca, a0);
-                u0 = fma(g.w[k], cu, u0);
+                sa0 = fma(g.w[k], qa, sa0);
+                su0 = fma(g.w[k], qu, su0);
+                if constexpr ((S & 4) != 0) {
+                    na0 = fma(g.w[k], qa, na0);
+                    nu0 = fma(g.w[k], qu, nu0);
+                }
             }
         });
+        const double a0 = sa0 - ca0, u0 = su0 - cu0, aw = saw - caw, uw = suw - cuw;
+        ca0 = na0;
+        cu0 = nu0;
+        caw = naw;
+        cuw = nuw;
         const uint32_t i = uint32_t(e) * m01 + base;
         if constexpr (UM == U_FROM_Z) {
             __builtin_nontemporal_store(a0, a.s0a + i);
