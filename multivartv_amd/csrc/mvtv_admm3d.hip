@@ -406,6 +406,7 @@ struct Fused3dArgs {
 };
 
 // partials: |r|^2, |D theta|^2, |alpha|^2, max dtheta, |g_u|^2, |s_B|^2, |s_A|^2 (max slot 3)
+// (IH = 10 at 5 waves per SIMD was tried: 96 VGPRs only with 96 B/lane of spills, 2.1x slower)
 template <int ORD, int UM, bool DTH, int NB, int IH>
 __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
     constexpr int P = 3, NC = 8;
@@ -516,9 +517,9 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
                 qu = neg ? qu + cl : qu - cl;   // u = -clamp
             }
         };
-        double qa_prev[NB], qu_prev[NB];
-#pragma unroll
-        for (int k = 0; k < NB; ++k) qa_prev[k] = qu_prev[k] = 0.0;
+        // the dim-2 difference is carried as two weighted sums (alpha, u) over the blocks with dim 2
+        // in S', not per block
+        double qa_prev = 0.0, qu_prev = 0.0;
 
         double th0[4], th1[4], zo[NB], zn[NB];
         if (z0 > 0) {   // carried sums of plane z0 - 1: recompute its z_new from the old state
@@ -533,7 +534,12 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
                 static_for<0, NB>([&](auto kc) {
                     constexpr int k = decltype(kc)::value;
                     constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                    if constexpr ((S & 4) != 0) plane_q(kc, 1, qa_prev[k], qu_prev[k]);
+                    if constexpr ((S & 4) != 0) {
+                        double qa, qu;
+                        plane_q(kc, 1, qa, qu);
+                        qa_prev = fma(g.w[k], qa, qa_prev);
+                        qu_prev = fma(g.w[k], qu, qu_prev);
+                    }
                 });
             }
             lds_barrier();
@@ -561,22 +567,23 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
             }
             lds_barrier();
             if (inner) {
-                double ga = 0.0, gu = 0.0;
+                double ga = 0.0, gu = 0.0, na = 0.0, nu = 0.0;
                 static_for<0, NB>([&](auto kc) {
                     constexpr int k = decltype(kc)::value;
                     constexpr int S = sprime_mask(block_code(k, P, ORD), P);
                     double qa, qu;
                     plane_q(kc, buf, qa, qu);
-                    double ca = qa, cu = qu;
+                    ga = fma(g.w[k], qa, ga);
+                    gu = fma(g.w[k], qu, gu);
                     if constexpr ((S & 4) != 0) {
-                        ca -= qa_prev[k];
-                        cu -= qu_prev[k];
-                        qa_prev[k] = qa;
-                        qu_prev[k] = qu;
+                        na = fma(g.w[k], qa, na);
+                        nu = fma(g.w[k], qu, nu);
                     }
-                    ga = fma(g.w[k], ca, ga);
-                    gu = fma(g.w[k], cu, gu);
                 });
+                ga -= qa_prev;
+                gu -= qu_prev;
+                qa_prev = na;
+                qu_prev = nu;
                 const uint32_t i = uint32_t(e) * pl + ixy;
                 __builtin_nontemporal_store(ga, a.g_alpha + i);
                 __builtin_nontemporal_store(gu, a.g_u + i);
