@@ -658,7 +658,14 @@ Fused3dArgs f3d_args(const Geom& g) {
 }
 }  // namespace
 
+bool fused2d_ok(const Geom& g);
+hipError_t launch_admm2d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
+                         double* z_new, double t_old, double c_old, double t_new, double c_prev,
+                         const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
+                         double* partials, int* nparts, const AdmmCtl* ctl);
+
 bool fused3d_ok(const Geom& g) {
+    if (g.p == 2) return fused2d_ok(g);
     if (g.p != 3 || std::getenv("MVTV_F3D_OFF")) return false;
     const Fused3dArgs a = f3d_args(g);
     return ((a.nblocks + 7) / 8 * 8) * 7 <= kMaxCgBlocks * kMaxRed;
@@ -668,6 +675,9 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
                          double* z_new, double t_old, double c_old, double t_new, double c_prev,
                          const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
                          double* partials, int* nparts, const AdmmCtl* ctl) {
+    if (g.p == 2)
+        return launch_admm2d(g, order, umode, s, theta, z_old, z_new, t_old, c_old, t_new, c_prev, theta_old, g_alpha,
+                             g_u, g_uprev, partials, nparts, ctl);
     Fused3dArgs a = f3d_args(g);
     a.theta = theta;
     a.z_old = z_old;
@@ -1248,6 +1258,253 @@ hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, co
     };
     if (expl) return prev ? gob(k_gather4b<U_EXPLICIT, true>) : gob(k_gather4b<U_EXPLICIT, false>);
     return prev ? gob(k_gather4b<U_FROM_Z, true>) : gob(k_gather4b<U_FROM_Z, false>);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_admm2d: the fused edge update + D^T gather for p = 2 (configs 2 and 4). A wave owns 64 columns
+// (lane 0 on x = X0-1 as halo, 63 interior) over a chunk of rows and marches dim 1: the x-1
+// neighbour of the gather comes from the lane below (shuffle), the y-1 neighbour from two carried
+// group sums. No LDS and no barrier; waves are independent. z ping-pongs like k_admm3d.
+namespace f2d {
+constexpr int TX = 63, NT = 256;
+}
+template <int ORD, int UM, bool DTH, int NB>
+__global__ __launch_bounds__(f2d::NT) void k_admm2d(const Fused3dArgs a) {
+    constexpr int P = 2, NC = 4;
+    const Geom& g = a.g;
+    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new, c_prev = a.c_prev;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        t_old = a.ctl->t_z;
+        c_old = a.ctl->c_prev;
+        t_new = a.ctl->t_next;
+        c_prev = a.ctl->c_prev;
+    }
+    double red[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const int wv = bid * (f2d::NT / 64) + int(threadIdx.x >> 6);   // this wave's (tile, chunk)
+    const int nwaves = a.nblocks;
+    if (bid * (f2d::NT / 64) < nwaves && wv < nwaves) {
+        const int lane = int(threadIdx.x & 63);
+        const int tc = wv / a.tiles_x, txi = wv - tc * a.tiles_x;
+        const int x = txi * f2d::TX - 1 + lane;
+        const int m0 = int(g.m[0]), m1 = int(g.m[1]);
+        const int y0 = tc * a.zchunk, y1 = min(m1, y0 + a.zchunk);
+        const bool cell = x >= 0 && x < m0;
+        const bool own = cell && lane > 0;
+        const int xc = min(max(x, 0), m0 - 1);
+        const uint32_t xo[2] = {uint32_t(xc), uint32_t(min(xc + 1, m0 - 1))};
+        const bool okx = x > 0;
+        auto load_row = [&](double (&th)[2], int y) {
+            const uint32_t yo = uint32_t(min(y, m1 - 1)) * uint32_t(m0);
+            th[0] = cell ? a.theta[yo + xo[0]] : 0.0;
+            th[1] = cell ? a.theta[yo + xo[1]] : 0.0;
+        };
+        auto load_z = [&](double (&zo)[NB], int y) {
+            const uint32_t i = uint32_t(y) * uint32_t(m0) + uint32_t(xc);
+#pragma unroll
+            for (int k = 0; k < NB; ++k) zo[k] = cell ? a.z_old[uint64_t(k) * g.N + i] : 0.0;
+        };
+        // z_new of this cell at row y from theta rows y (r0), y+1 (r1) and the old z
+        auto edge_cell = [&](int y, const double (&r0)[2], const double (&r1)[2], const double (&zo)[NB],
+                             double (&zn)[NB], bool mine) {
+            const uint32_t i = uint32_t(y) * uint32_t(m0) + uint32_t(xc);
+            double v[NC] = {r0[0], r0[1], r1[0], r1[1]};
+            if constexpr (DTH)
+                if (mine) red[3] = fmax(red[3], fabs(v[0] - a.theta_old[i]));
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+#pragma unroll
+                for (int q = 0; q < NC; ++q)
+                    if (!((q >> j) & 1)) v[q | (1 << j)] = v[q] - v[q | (1 << j)];
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                const double d = g.w[k] * v[S];
+                const double uo = (UM == U_EXPLICIT) ? zo[k] : -c_old * clampd(zo[k], t_old);
+                const double z = cell ? d - uo : 0.0;
+                zn[k] = z;
+                if (mine) {
+                    const double al = z - clampd(z, t_new);
+                    const double r = al - d;
+                    __builtin_nontemporal_store(z, a.z_new + uint64_t(k) * g.N + i);
+                    red[0] = fma(r, r, red[0]);
+                    red[1] = fma(d, d, red[1]);
+                    red[2] = fma(al, al, red[2]);
+                }
+            });
+        };
+        // in-row sums of block k at this cell: own z_new and (dim 0 in S') the lane below's
+        auto row_q = [&](auto kc, const double (&zn)[NB], double& qa, double& qu) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+            const double v0 = zn[k];
+            const double cl0 = clampd(v0, t_new);
+            qa = v0 - cl0;
+            qu = -cl0;
+            if constexpr ((S & 1) != 0) {
+                const double vl = __shfl_up(v0, 1, 64);
+                const double v1 = okx ? vl : 0.0;
+                const double cl1 = clampd(v1, t_new);
+                qa -= v1 - cl1;
+                qu += cl1;
+            }
+        };
+        double ca = 0.0, cu = 0.0;   // carried: weighted row sums of the blocks with dim 1 in S' at y-1
+        double r0[2], r1[2], zo[NB], zn[NB];
+        if (y0 > 0) {
+            load_row(r0, y0 - 1);
+            load_row(r1, y0);
+            load_z(zo, y0 - 1);
+            edge_cell(y0 - 1, r0, r1, zo, zn, false);
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                double qa, qu;
+                row_q(kc, zn, qa, qu);
+                if constexpr ((S & 2) != 0) {
+                    ca = fma(g.w[k], qa, ca);
+                    cu = fma(g.w[k], qu, cu);
+                }
+            });
+        }
+        load_row(r0, y0);
+        load_row(r1, y0 + 1);
+        load_z(zo, y0);
+        double gp = own ? __builtin_nontemporal_load(a.g_uprev + uint32_t(y0) * uint32_t(m0) + uint32_t(xc)) : 0.0;
+        for (int y = y0; y < y1; ++y) {
+            edge_cell(y, r0, r1, zo, zn, own);
+            double nr[2], nzo[NB], ngp = 0.0;
+            if (y + 1 < y1) {
+                load_row(nr, y + 2);
+                load_z(nzo, y + 1);
+                ngp = own ? __builtin_nontemporal_load(a.g_uprev + uint32_t(y + 1) * uint32_t(m0) + uint32_t(xc)) : 0.0;
+            } else {
+                nr[0] = nr[1] = 0.0;
+#pragma unroll
+                for (int k = 0; k < NB; ++k) nzo[k] = 0.0;
+            }
+            double ga = 0.0, gu = 0.0, na = 0.0, nu = 0.0;
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                double qa, qu;
+                row_q(kc, zn, qa, qu);
+                ga = fma(g.w[k], qa, ga);
+                gu = fma(g.w[k], qu, gu);
+                if constexpr ((S & 2) != 0) {
+                    na = fma(g.w[k], qa, na);
+                    nu = fma(g.w[k], qu, nu);
+                }
+            });
+            ga -= ca;
+            gu -= cu;
+            ca = na;
+            cu = nu;
+            if (own) {
+                const uint32_t i = uint32_t(y) * uint32_t(m0) + uint32_t(xc);
+                __builtin_nontemporal_store(ga, a.g_alpha + i);
+                __builtin_nontemporal_store(gu, a.g_u + i);
+                const double gpc = c_prev * gp;
+                const double db = gu - gpc, da = ga + gpc;
+                red[4] = fma(gu, gu, red[4]);
+                red[5] = fma(db, db, red[5]);
+                red[6] = fma(da, da, red[6]);
+            }
+            r0[0] = r1[0];
+            r0[1] = r1[1];
+            r1[0] = nr[0];
+            r1[1] = nr[1];
+#pragma unroll
+            for (int k = 0; k < NB; ++k) zo[k] = nzo[k];
+            gp = ngp;
+        }
+    }
+    // block reduction (max in slot 3)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const double o = __shfl_down(red[k], off, 64);
+            red[k] = k == 3 ? fmax(red[k], o) : red[k] + o;
+        }
+    }
+    __shared__ double rs[f2d::NT / 64][7];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 7; ++k) rs[w][k] = red[k];
+    __syncthreads();
+    if (threadIdx.x < 7) {
+        const int k = threadIdx.x;
+        double acc = rs[0][k];
+        for (int ww = 1; ww < f2d::NT / 64; ++ww) acc = k == 3 ? fmax(acc, rs[ww][k]) : acc + rs[ww][k];
+        a.partials[blockIdx.x * 7 + k] = acc;
+    }
+}
+
+namespace {
+Fused3dArgs f2d_args(const Geom& g) {
+    Fused3dArgs a{};
+    a.g = g;
+    a.tiles_x = int((g.m[0] + f2d::TX - 1) / f2d::TX);
+    static const int want = [] {
+        const char* e = std::getenv("MVTV_F2D_WAVES");
+        return e ? std::atoi(e) : 2048;   // 2048^2: 2048 waves 75.8 us, 4096 81.8, 8192 81.0
+    }();
+    const int m1 = int(g.m[1]);
+    int nc = std::max(1, std::min(m1 / 8, want / std::max(1, a.tiles_x)));   // rows per chunk >= 8
+    const int wpb = f2d::NT / 64;
+    while (nc > 1 && ((nc * a.tiles_x + wpb - 1) / wpb + 7) / 8 * 8 * 7 > kMaxCgBlocks * kMaxRed) --nc;
+    a.zchunk = (m1 + nc - 1) / nc;
+    nc = (m1 + a.zchunk - 1) / a.zchunk;
+    a.nblocks = a.tiles_x * nc;   // waves
+    return a;
+}
+}  // namespace
+
+bool fused2d_ok(const Geom& g) {
+    if (g.p != 2 || std::getenv("MVTV_F2D_OFF") || g.ibeg != 0 || g.iend != g.N) return false;
+    const Fused3dArgs a = f2d_args(g);
+    const int wg = (a.nblocks + f2d::NT / 64 - 1) / (f2d::NT / 64);
+    return ((wg + 7) / 8 * 8) * 7 <= kMaxCgBlocks * kMaxRed;
+}
+
+hipError_t launch_admm2d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
+                         double* z_new, double t_old, double c_old, double t_new, double c_prev,
+                         const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
+                         double* partials, int* nparts, const AdmmCtl* ctl) {
+    Fused3dArgs a = f2d_args(g);
+    a.theta = theta;
+    a.z_old = z_old;
+    a.z_new = z_new;
+    a.theta_old = theta_old;
+    a.g_alpha = g_alpha;
+    a.g_u = g_u;
+    a.g_uprev = g_uprev;
+    a.partials = partials;
+    a.t_old = t_old;
+    a.c_old = c_old;
+    a.t_new = t_new;
+    a.c_prev = c_prev;
+    a.ctl = ctl;
+    const int wg = (a.nblocks + f2d::NT / 64 - 1) / (f2d::NT / 64);
+    const int grid = (wg + 7) / 8 * 8;
+    *nparts = grid;
+    const bool dth = theta_old != nullptr;
+    auto go = [&](auto kern) {
+        klaunch(kern, dim3(grid), dim3(f2d::NT), 0, s, a);
+        return hipGetLastError();
+    };
+    if (order == 0) {
+        if (umode == U_EXPLICIT) return dth ? go(k_admm2d<0, U_EXPLICIT, true, 3>) : go(k_admm2d<0, U_EXPLICIT, false, 3>);
+        return dth ? go(k_admm2d<0, U_FROM_Z, true, 3>) : go(k_admm2d<0, U_FROM_Z, false, 3>);
+    }
+    if (g.nb == 2) {
+        if (umode == U_EXPLICIT) return dth ? go(k_admm2d<1, U_EXPLICIT, true, 2>) : go(k_admm2d<1, U_EXPLICIT, false, 2>);
+        return dth ? go(k_admm2d<1, U_FROM_Z, true, 2>) : go(k_admm2d<1, U_FROM_Z, false, 2>);
+    }
+    if (umode == U_EXPLICIT) return dth ? go(k_admm2d<1, U_EXPLICIT, true, 3>) : go(k_admm2d<1, U_EXPLICIT, false, 3>);
+    return dth ? go(k_admm2d<1, U_FROM_Z, true, 3>) : go(k_admm2d<1, U_FROM_Z, false, 3>);
 }
 
 }  // namespace mvtv
