@@ -126,3 +126,17 @@ def test_mvtv_path_equals_per_lambda_runs():
             t, _, r = P.state_get(want_u=False)
             np.testing.assert_array_equal(th[i], t)
             assert rhos[i] == r and st[i]["iters"] == s["iters"]
+
+
+def test_mvtv_path_edge_cases():
+    """Empty lambda grid, no theta output, bad arguments (the ABI's status codes)."""
+    m = [8, 8]
+    with mv.Problem(m, np.random.default_rng(0).standard_normal(64)) as P:
+        th, rhos, st = P.path([], np.zeros(64), 0.1)
+        assert th.shape == (0, 64) and rhos.size == 0 and st == []
+        th, rhos, st = P.path([0.5, 0.2], np.zeros(64), 0.1, want_thetas=False)
+        assert th is None and rhos.size == 2 and len(st) == 2
+        t_last, _, r_last = P.state_get(want_u=False)
+        assert r_last == rhos[-1]
+        with pytest.raises(mv.MvtvError):
+            P.path([-1.0], np.zeros(64), 0.1)
