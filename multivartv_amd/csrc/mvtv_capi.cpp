@@ -82,6 +82,10 @@ struct mvtv_problem {
     bool e3d = false;             // z-marching 3-D edge kernels
     bool f3d = false;             // fused 3-D edge update + gather (needs the second edge buffer)
     double* edges2 = nullptr;     // ping-pong partner of edges for the fused kernel
+    double* edges3 = nullptr;     // MVTV_EBUF3=1: z rotates over three buffers. On boxes where the fused
+                                  // launches alternate fast / slow, the slow ones are those writing into
+                                  // `edges` (measured 4.60 / 4.97 ms alternating -> 4.60 / 4.53 / 5.00):
+                                  // placement-dependent, so it stays opt-in (+7.5 GB at 512^3)
     double* pcg_b = nullptr;      // right-hand side of the spectrally preconditioned PCG
     double* g4 = nullptr;         // 4 N-arrays: the two-pass 4-D gather's partial sums
     double wmean = 1.0;           // mean(W): the preconditioner's identity weight
@@ -191,7 +195,7 @@ mvtv_status alloc(double** ptr, size_t n) {
 void free_all(mvtv_problem* P) {
     double** bufs[] = {&P->oty, &P->wdiag, &P->theta, &P->edges, &P->ga, &P->gu, &P->guprev, &P->r,
                        &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->scratch,
-                       &P->edges2, &P->pcg_b, &P->g4};
+                       &P->edges2, &P->pcg_b, &P->g4, &P->edges3};
     for (double** b : bufs)
         if (*b) {
             (void)hipFree(*b);
@@ -826,6 +830,12 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     const bool track_theta = variant != MVTV_VARIANT_RCPP;
     const bool fused = P->f3d;
     if (fused && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
+    static const bool rot3 = [] {
+        const char* e = std::getenv("MVTV_EBUF3");
+        return e && std::atoi(e) != 0;
+    }();
+    if (fused && rot3 && !P->edges3) MVTV_TRY(alloc(&P->edges3, size_t(P->g.nb) * P->g.N));
+    const int nbuf = (fused && P->edges3) ? 3 : 2;
     double dtheta = 0.0;
     if (track_theta) {
         if (!P->thold) MVTV_TRY(alloc(&P->thold, P->g.N));
@@ -864,7 +874,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         c.eps_dual = c.eps_pri = tol;
         HIP_TRY(hipMemcpyAsync(P->ctl, &c, sizeof(AdmmCtl), hipMemcpyHostToDevice, P->stream));
         double* gbuf[2] = {P->guprev, P->gu};
-        double* ebuf[2] = {P->edges, P->edges2};
+        double* ebuf[3] = {P->edges, P->edges2, P->edges3};
         auto enqueue = [&](int j) -> mvtv_status {
             double* gp = gbuf[j & 1];
             double* gn = gbuf[(j + 1) & 1];
@@ -876,7 +886,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
             if (fused) {   // z ping-pongs between the two edge buffers
                 int hh = P->tstart(MVTV_K_ADMM_FUSED);
                 int npf = 0;
-                HIP_TRY(launch_admm3d(P->g, P->order, um, P->stream, P->theta, ebuf[j & 1], ebuf[(j + 1) & 1], 0.0, 1.0,
+                HIP_TRY(launch_admm3d(P->g, P->order, um, P->stream, P->theta, ebuf[j % nbuf], ebuf[(j + 1) % nbuf], 0.0, 1.0,
                                       0.0, 1.0, track_theta ? P->thold : nullptr, P->ga, gn, gp, P->partials, &npf,
                                       P->ctl));
                 P->tstop(hh);
@@ -937,7 +947,13 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         P->harvest();
         if (o.fixed_iters <= 0 && c.status == 0) P->admm_hint = it_done + 1;
         if (it_done & 1) std::swap(P->guprev, P->gu);   // P->guprev holds D^T u of the current state
-        if (fused && (it_done & 1)) std::swap(P->edges, P->edges2);
+        if (fused && nbuf == 3) {   // the state is in ebuf[it_done % 3]
+            P->edges = ebuf[it_done % 3];
+            P->edges2 = ebuf[(it_done + 1) % 3];
+            P->edges3 = ebuf[(it_done + 2) % 3];
+        } else if (fused && (it_done & 1)) {
+            std::swap(P->edges, P->edges2);
+        }
         if (it_done > 0) P->edge_mode = U_FROM_Z;
         if (it_done > 0) P->t_z = c.t_z;
         P->c_state = c.c_prev;
