@@ -113,7 +113,7 @@ __global__ __launch_bounds__(NT) void k_edge3d(const Edge3dArgs a) {
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
                 {
                     const double d = g.w[k] * v[S];
-                    double* ep = a.edges + uint64_t(k) * g.N + i;
+                    double* ep = a.edges + eix(g, k, i);
                     const double stored = __builtin_nontemporal_load(ep);
                     const double uo = (UM == U_EXPLICIT) ? stored : -c_old * clampd(stored, t_old);
                     const double z = d - uo;
@@ -165,13 +165,13 @@ __global__ __launch_bounds__(NT) void k_gather3d(const Edge3dArgs a) {
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
             constexpr int SI = S & 3;   // in-plane part of the difference set
-            const double* eb = a.edges + uint64_t(k) * g.N + uint32_t(e) * pl + base_xy;
+            const uint32_t ic = uint32_t(e) * pl + base_xy;
             qa = 0.0;
             qu = 0.0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 if ((q & ~SI) != 0) continue;   // corner q subset of S
-                const double vv = *(eb - qoff[q]);
+                const double vv = a.edges[eix(g, k, ic - qoff[q])];
                 const double v = qok[q] ? vv : 0.0;
                 const bool neg = __builtin_popcount(q) & 1;
                 if constexpr (UM == U_FROM_Z) {
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
                 const bool need = cell && (!hrow || (S & 2)) && (!hlane || (S & 1));
-                const double* src = a.z_old + uint64_t(k) * g.N + i;
+                const double* src = a.z_old + eix(g, k, i);
                 zo[k] = need ? *src : 0.0;
             });
         };
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
                 if (own) {
                     const double al = z - clampd(z, t_new);
                     const double r = al - d;
-                    __builtin_nontemporal_store(z, a.z_new + uint64_t(k) * g.N + i);
+                    __builtin_nontemporal_store(z, a.z_new + eix(g, k, i));
                     red[0] = fma(r, r, red[0]);
                     red[1] = fma(d, d, red[1]);
                     red[2] = fma(al, al, red[2]);

@@ -665,6 +665,12 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
     P->e3d = edge3d_ok(g);
     if (s == MVTV_OK && P->e3d && g.p == 4 && gather4_ok(g)) s = alloc(&P->g4, 4 * size_t(N));
     P->f3d = !sl && fused3d_ok(g);
+    {   // chunked edge layout for the 3-D fused path (MVTV_EAOS=0 keeps block-major): the fused kernel's
+        // launches 2-4 % shorter at 512^3 on the same box (4.21 -> 4.13 ms, 5.2-5.36 -> 5.13 ms)
+        const char* e = std::getenv("MVTV_EAOS");
+        const bool want = e ? std::atoi(e) != 0 : true;
+        g.eaos = (want && P->f3d && g.p == 3 && g.N % 64 == 0) ? 1u : 0u;
+    }
     if (s == MVTV_OK) s = mvtv_problem_set_data(P, d->oty, d->wdiag);
     if (s != MVTV_OK) {
         free_all(P);

@@ -65,7 +65,16 @@ struct Geom {
     double w[kMaxBlocks];      // block weights, in block order
     double cS[16];             // D^T D coefficient per subset mask S of dims
     uint32_t ibeg, iend;       // nodes the edge kernels update and reduce over (slab: owned planes)
+    uint32_t eaos;             // edge layout: 0 block-major z[k][N]; 1 64-node chunks z[N/64][nb][64]
 };
+
+// Offset of block k's word at node i in the edge buffer. Block-major keeps each block a separate
+// stream; the chunked layout (eaos, p = 3 fused problems) puts all blocks of 64 consecutive nodes in
+// one 64 * nb-word run, so the fused kernel's z traffic is one stream instead of nb.
+__host__ __device__ __forceinline__ uint64_t eix(const Geom& g, int k, uint32_t i) {
+    return g.eaos ? (((uint64_t(i >> 6) * uint32_t(g.nb) + uint32_t(k)) << 6) | uint64_t(i & 63u))
+                  : uint64_t(k) * g.N + i;
+}
 
 // Per-node multi-index decode (column-major, dim 0 fastest).
 template <int P>

@@ -111,7 +111,7 @@ __global__ __launch_bounds__(kThreads) void k_edge_update(Geom g, const double* 
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
             if (k < g.nb) {
                 const double d = g.w[k] * a[S];
-                const uint64_t e = uint64_t(k) * g.N + i;
+                const uint64_t e = eix(g, k, i);
                 const double stored = edges[e];
                 const double uo = (UM == U_EXPLICIT) ? stored : -c_old * clampd(stored, t_old);
                 const double z = d - uo;
@@ -151,7 +151,6 @@ __global__ __launch_bounds__(kThreads) void k_gather(Geom g, const double* __res
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
             if (k < g.nb) {
                 double aa = 0.0, au = 0.0;
-                const double* eb = edges + uint64_t(k) * g.N;
 #pragma unroll
                 for (int T = 0; T < NC; ++T) {
                     if ((T & ~S) != 0) continue;   // T subset of S
@@ -163,7 +162,7 @@ __global__ __launch_bounds__(kThreads) void k_gather(Geom g, const double* __res
                             ok = ok && (c[j] > 0);
                             idx -= g.stride[j];
                         }
-                    const double vv = eb[ok ? idx : i];
+                    const double vv = edges[eix(g, k, ok ? idx : i)];
                     const double v = ok ? vv : 0.0;
                     const bool neg = __builtin_popcount(T) & 1;
                     if constexpr (UM == U_FROM_Z) {
@@ -218,7 +217,7 @@ __global__ __launch_bounds__(kThreads) void k_apply_D(Geom g, const double* __re
         static_for<0, NC - 1>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-            if (k < g.nb) edges[uint64_t(k) * g.N + i] = g.w[k] * a[S];
+            if (k < g.nb) edges[eix(g, k, i)] = g.w[k] * a[S];
         });
     }
 }
@@ -237,7 +236,7 @@ __global__ __launch_bounds__(kThreads) void k_edges_fill_valid(Geom g, double* _
 #pragma unroll
                 for (int j = 0; j < P; ++j)
                     if ((S >> j) & 1) valid = valid && (c[j] + 1 < g.m[j]);
-                edges[uint64_t(k) * g.N + i] = valid ? value : 0.0;
+                edges[eix(g, k, i)] = valid ? value : 0.0;
             }
         });
     }
@@ -520,6 +519,8 @@ struct RedDims {
     uint64_t rd[kMaxDims];
     uint64_t stride[kMaxDims];
     int p;
+    Geom g;   // edge layout (eix)
+    int k;
 };
 
 __global__ void k_edges_import(RedDims rdd, uint64_t base, uint64_t e0, uint64_t cnt,
@@ -531,7 +532,7 @@ __global__ void k_edges_import(RedDims rdd, uint64_t base, uint64_t e0, uint64_t
             idx += (e - q * rdd.rd[j]) * rdd.stride[j];
             e = q;
         }
-        padded[base + idx] = compact[t];
+        padded[eix(rdd.g, rdd.k, uint32_t(idx))] = compact[t];
     }
 }
 
@@ -545,7 +546,7 @@ __global__ void k_edges_export(RedDims rdd, uint64_t base, uint64_t e0, uint64_t
             idx += (e - q * rdd.rd[j]) * rdd.stride[j];
             e = q;
         }
-        const double v = padded[base + idx];
+        const double v = padded[eix(rdd.g, rdd.k, uint32_t(idx))];
         compact[t] = (umode == U_FROM_Z) ? -c_ * clampd(v, t_) : v;
     }
 }
@@ -616,6 +617,8 @@ RedDims red_dims(const Geom& g, int order, int k) {
         r.rd[j] = g.m[j] - ((S >> j) & 1);
         r.stride[j] = g.stride[j];
     }
+    r.g = g;
+    r.k = k;
     return r;
 }
 
