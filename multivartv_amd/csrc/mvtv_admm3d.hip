@@ -387,6 +387,7 @@ hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, c
 // in-plane sums of the previous plane (as in k_gather3d), so no plane is ever re-read.
 namespace f3d {
 constexpr int IW = 64, TX = IW - 1;
+constexpr int SW = 16;   // strip image width: the last m0 % 63 (1..15) columns of dim 0
 int rows();   // image rows per workgroup (8, or 16 with MVTV_F3D_IH=16; 8 measured 2-3 % faster)
 }
 
@@ -403,36 +404,22 @@ struct Fused3dArgs {
     double t_old, c_old, t_new, c_prev;
     const AdmmCtl* ctl;
     int tiles_x, tiles_y, zchunk, nblocks, zlo, zhi;
+    int strip, tpz;   // k_admm3d: ragged-edge strip tiles on / tiles per z chunk
 };
 
 // partials: |r|^2, |D theta|^2, |alpha|^2, max dtheta, |g_u|^2, |s_B|^2, |s_A|^2 (max slot 3)
 // (IH = 10 at 5 waves per SIMD was tried: 96 VGPRs only with 96 B/lane of spills, 2.1x slower)
-template <int ORD, int UM, bool DTH, int NB, int IH>
-__global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
+template <int ORD, int UM, bool DTH, int NB, int IW, int IH>
+__device__ __forceinline__ void admm3d_tile(const Fused3dArgs& a, double* __restrict__ szr, double (&red)[7], int xh,
+                                            int yh, int rows_used, int z0, int z1, double t_old, double c_old,
+                                            double t_new, double c_prev) {
     constexpr int P = 3, NC = 8;
-    constexpr int IW = f3d::IW, TX = f3d::TX, TY = IH - 1, NT = IW * IH;
     const Geom& g = a.g;
-    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new, c_prev = a.c_prev;
-    if (a.ctl) {
-        if (a.ctl->done) return;
-        t_old = a.ctl->t_z;
-        c_old = a.ctl->c_prev;
-        t_new = a.ctl->t_next;
-        c_prev = a.ctl->c_prev;
-    }
-    __shared__ double sz[2][NB][IH][IW];
-    double red[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    const bool valid = bid < a.nblocks;
-    if (valid) {
-        const int nt = a.tiles_x * a.tiles_y;
-        const int tz = bid / nt, rem = bid - tz * nt;
-        const int tyi = rem / a.tiles_x, txi = rem - tyi * a.tiles_x;
-        const int lane = int(threadIdx.x & 63), row = int(threadIdx.x >> 6);
-        const int x = txi * TX - 1 + lane, y = tyi * TY - 1 + row;
-        const int z0 = a.zlo + tz * a.zchunk, z1 = min(a.zhi, z0 + a.zchunk);
+    {
+        const int lane = int(threadIdx.x) % IW, row = int(threadIdx.x) / IW;
+        const int x = xh + lane, y = yh + row;
         const int m0 = int(g.m[0]), m1 = int(g.m[1]), m2 = int(g.m[2]);
-        const bool cell = x >= 0 && y >= 0 && x < m0 && y < m1;     // computes z_new here
+        const bool cell = row < rows_used && x >= 0 && y >= 0 && x < m0 && y < m1;     // computes z_new here
         const bool inner = cell && lane > 0 && row > 0;              // owns outputs here
         const uint32_t pl = uint32_t(m0) * uint32_t(m1);
         const int xc = min(max(x, 0), m0 - 1), yc = min(max(y, 0), m1 - 1);
@@ -509,7 +496,7 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
             for (int q = 0; q < 4; ++q) {
                 if ((q & ~SI) != 0) continue;
                 const bool ok = (!(q & 1) || okx) && (!(q & 2) || oky);
-                const double v = ok ? sz[buf][k][row - ((q >> 1) & 1)][lane - (q & 1)] : 0.0;
+                const double v = ok ? szr[((buf * NB + k) * IH + row - ((q >> 1) & 1)) * IW + lane - (q & 1)] : 0.0;
                 const bool neg = __builtin_popcount(q) & 1;
                 const double cl = clampd(v, t_new);
                 const double al = v - cl;
@@ -528,7 +515,7 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
             load_z(zo, z0 - 1);
             edge_cell(z0 - 1, th0, th1, zo, zn, false);
 #pragma unroll
-            for (int k = 0; k < NB; ++k) sz[1][k][row][lane] = zn[k];
+            for (int k = 0; k < NB; ++k) szr[((NB + k) * IH + row) * IW + lane] = zn[k];
             lds_barrier();
             if (inner) {
                 static_for<0, NB>([&](auto kc) {
@@ -552,7 +539,7 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
             const int buf = (e - z0) & 1;
             edge_cell(e, th0, th1, zo, zn, inner);
 #pragma unroll
-            for (int k = 0; k < NB; ++k) sz[buf][k][row][lane] = zn[k];
+            for (int k = 0; k < NB; ++k) szr[((buf * NB + k) * IH + row) * IW + lane] = zn[k];
             // prefetch step e+1 while this step's gather runs
             double nth[4], nzo[NB], ngp = 0.0;
             if (e + 1 < z1) {
@@ -604,6 +591,49 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
             // the buffer written next step is the other one; the one after waits for this barrier
         }
     }
+}
+
+// m0 = 63 q + r with 1 <= r <= 15 (512 = 8 * 63 + 8): instead of a (q+1)-th 64-lane tile that
+// computes r + 1 columns with 64 lanes, a 16 x (NT/16) strip image covers those columns for G
+// consecutive main y-tiles (tile order per group: G rows of main tiles, then the strip). The
+// per-cell arithmetic and its order are the same in either image, so the fields are unchanged.
+template <int ORD, int UM, bool DTH, int NB, int IH>
+__global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
+    constexpr int IW = f3d::IW, TX = f3d::TX, TY = IH - 1, NT = IW * IH;
+    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new, c_prev = a.c_prev;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        t_old = a.ctl->t_z;
+        c_old = a.ctl->c_prev;
+        t_new = a.ctl->t_next;
+        c_prev = a.ctl->c_prev;
+    }
+    __shared__ double szr[2 * NB * NT];
+    double red[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const bool valid = bid < a.nblocks;
+    if (valid) {
+        const int tz = bid / a.tpz, rem = bid - tz * a.tpz;
+        const int z0 = a.zlo + tz * a.zchunk, z1 = min(a.zhi, z0 + a.zchunk);
+        if (a.strip) {
+            constexpr int SH = NT / f3d::SW, G = (SH - 1) / TY;
+            const int per = G * a.tiles_x + 1;
+            const int grp = rem / per, o = rem - grp * per;
+            if (o == G * a.tiles_x) {
+                admm3d_tile<ORD, UM, DTH, NB, f3d::SW, SH>(a, szr, red, a.tiles_x * TX - 1, grp * G * TY - 1,
+                                                           G * TY + 1, z0, z1, t_old, c_old, t_new, c_prev);
+            } else {
+                const int tyi = grp * G + o / a.tiles_x, txi = o - (o / a.tiles_x) * a.tiles_x;
+                if (tyi < a.tiles_y)
+                    admm3d_tile<ORD, UM, DTH, NB, IW, IH>(a, szr, red, txi * TX - 1, tyi * TY - 1, IH, z0, z1, t_old,
+                                                          c_old, t_new, c_prev);
+            }
+        } else {
+            const int tyi = rem / a.tiles_x, txi = rem - tyi * a.tiles_x;
+            admm3d_tile<ORD, UM, DTH, NB, IW, IH>(a, szr, red, txi * TX - 1, tyi * TY - 1, IH, z0, z1, t_old, c_old,
+                                                  t_new, c_prev);
+        }
+    }
     // block reduction (max in slot 3)
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -641,9 +671,22 @@ Fused3dArgs f3d_args(const Geom& g) {
     a.g = g;
     a.zlo = int(g.ibeg / (g.m[0] * g.m[1]));
     a.zhi = int(g.iend / (g.m[0] * g.m[1]));
-    a.tiles_x = int((g.m[0] + f3d::TX - 1) / f3d::TX);
-    a.tiles_y = int((g.m[1] + (f3d::rows() - 1) - 1) / (f3d::rows() - 1));
-    const int tiles = a.tiles_x * a.tiles_y;
+    const int TY = f3d::rows() - 1, m0 = int(g.m[0]), r0 = m0 % f3d::TX;
+    static const bool strip_on = [] {
+        const char* e = std::getenv("MVTV_F3D_STRIP");
+        return !e || std::atoi(e) != 0;
+    }();
+    a.tiles_y = int((int(g.m[1]) + TY - 1) / TY);
+    a.strip = strip_on && m0 >= f3d::TX && r0 >= 1 && r0 <= f3d::SW - 1;
+    if (a.strip) {
+        const int G = (f3d::IW * (TY + 1) / f3d::SW - 1) / TY;   // main y-tiles per strip tile
+        a.tiles_x = m0 / f3d::TX;
+        a.tpz = (a.tiles_y + G - 1) / G * (G * a.tiles_x + 1);
+    } else {
+        a.tiles_x = (m0 + f3d::TX - 1) / f3d::TX;
+        a.tpz = a.tiles_x * a.tiles_y;
+    }
+    const int tiles = a.tpz;
     static const int want = [] {
         const char* e = std::getenv("MVTV_F3D_WG");
         return e ? std::atoi(e) : 4096;

@@ -1,0 +1,32 @@
+"""Fused 3-D edge kernel (k_admm3d) on meshes whose dim 0 leaves a ragged last column block
+(m0 = 63 q + r): r in 1..15 runs the 16-wide strip tiles, r >= 16 the 64-lane tiles. Each run is
+checked against the C oracle (oracle/c/mvtv_oracle.c, variant B of rcpp…/solvers.cpp:96-136,
+pinned to the golden fixtures in test_oracle_c.py) over fixed ADMM iterations: rho exactly, theta
+and u to 1e-9 of their max (both sides solve to PCG rtol 1e-13, or exactly by DCT on the GPU)."""
+import numpy as np
+import pytest
+
+mv = pytest.importorskip("multivartv_amd")
+c_oracle = pytest.importorskip("oracle.c_oracle")
+from multivartv_amd.synth import towers  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,iters", [(64, 8), (72, 6), (80, 6), (128, 4)],
+                         ids=["r1_strip", "r9_strip", "r17_tiles", "r2_strip"])
+def test_fused_ragged_dim0_matches_oracle(n, iters):
+    m = [n, n, n]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    lam = 1.0
+    th0 = np.full(y.size, y.mean())
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        th, u, rho, st = P.admm(lam, th0, u=np.zeros(P.E), rho=lam / 5, fixed_iters=iters, pcg_rtol=1e-13)
+        E = P.E
+    ref_th = th0.copy()
+    ref_u = np.zeros(E)
+    rs = c_oracle.admm_rcpp(m, y, lam, ref_th, ref_u, lam / 5, deltas, fixed_iters=iters, pcg_rtol=1e-13)
+    assert rho == rs["rho"]
+    assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
+    assert np.max(np.abs(u - ref_u)) <= 1e-9 * max(1.0, np.max(np.abs(ref_u)))
