@@ -43,10 +43,13 @@ def test_single_rank_slab_matches(m, lam, fixed):
     S.close()
 
 
-def _rank_main(rank, world, port, m, lam, fixed, q):
+def _rank_main(rank, world, port, m, lam, fixed, q, backend="gloo"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        import torch
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     y = towers(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     b = slab.plane_bounds(m[-1], world)
@@ -78,3 +81,25 @@ def test_multi_rank_slab_matches(m, lam, world):
     for r in res:
         assert r[1] == st["iters"] and r[2] == rho
     assert _rel(np.concatenate([r[3] for r in res]), th) <= 1e-11
+
+
+@pytest.mark.parametrize("fixed", [7, 0])
+def test_rccl_transport_single_rank(fixed):
+    """The "nccl" (RCCL) transport: exchange buffers are device tensors and the all-to-all
+    transposes run through RCCL. One rank on the box's one GPU (RCCL refuses two ranks on one
+    device), so this covers the device-buffer path and RCCL's self all-to-all, not xGMI."""
+    import torch.multiprocessing as mp
+    m, lam = [16, 16, 16], 1.0
+    y, deltas, th, rho, st = _reference(m, lam, fixed)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rank_main, args=(0, 1, port, m, lam, fixed, q, "nccl"))
+    p.start()
+    r = q.get(timeout=100)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert r[1] == st["iters"] and r[2] == rho
+    assert _rel(r[3], th) <= 1e-11
