@@ -10,8 +10,9 @@ rtol 1e-10. Inputs are resident in HBM before timing starts.
 Multi-GPU (torchrun, one process per GPU): every rank fits its own independent
 512^3 mesh (noise seed + rank) — the embarrassingly parallel "independent mesh
 fits" sharding of the north star — so value = total iterations/s of all ranks
-and scaling is weak. torch.distributed (gloo, host scalars) provides the
-barriers, the max-over-ranks time and the final global residual all-reduce.
+and scaling is weak. torch.distributed (RCCL by default, MVTV_DIST_BACKEND=gloo
+for host scalars) provides the barriers, the max-over-ranks time and the final
+global residual all-reduce.
 """
 from __future__ import annotations
 
@@ -65,7 +66,8 @@ class Dist:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.dist = None
         self.backend = backend
-        if self.world > 1:
+        # MVTV_DIST_FORCE=1 creates the process group at world size 1 too (rehearsal under torchrun)
+        if self.world > 1 or os.environ.get("MVTV_DIST_FORCE") == "1":
             import torch.distributed as dist
             if backend == "nccl":
                 import torch
@@ -177,7 +179,9 @@ def main():
     a = parse()
     if a.mode == "slab" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
         return slab_main(a)
-    D = Dist()
+    # the independent fits share nothing but the barrier, the max time and the final residual
+    # all-reduce: RCCL (device scalars) by default, MVTV_DIST_BACKEND=gloo for host scalars
+    D = Dist(os.environ.get("MVTV_DIST_BACKEND", "nccl"))
     if mv.device_count() < 1:
         raise SystemExit("bench.py: no HIP device")
     m = [a.size] * a.dims
@@ -277,7 +281,8 @@ def main():
                                    f"lambda={lam}, fixed-iteration mode",
                        "theta_solver": used,
                        "mesh": m, "nodes": N, "edges": E, "pcg_rtol": a.pcg_rtol, "pcg_iters_mean": round(kbar_all, 2),
-                       "parallelism": "independent mesh fits, one per GPU" if D.world > 1 else "single GPU"},
+                       "parallelism": (f"independent mesh fits, one per GPU ({'RCCL' if D.backend == 'nccl' else D.backend} "
+                                       f"barrier / max-time / residual all-reduce)") if D.world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": pmc, "bytes_per_launch": tim[dom]["bytes_per_launch"],
