@@ -407,4 +407,100 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
     return go(k_cg3d<W_IDENTITY, 2>);
 }
 
+
+// ------------------------------------------------------------------------------------ k_apply3d
+// q = (W + sigma D^T D) x on a whole 3-D mesh: the ADMM start's g_alpha = D^T D theta_0
+// (rcpp…/solvers.cpp:101, alpha_0 = D theta_0) and the operator checks. A thread owns one
+// (dim 0, dim 1) column over a chunk of dim-2 planes and marches dim 2: each plane is read once
+// per thread as its 3 x 3 in-plane neighbourhood (L1/L2 serve the 8 neighbours) and reduced to the
+// two in-plane sums of the 8-weight symmetric stencil (dz = 0 layer, dz = +-1 layer); q(z) =
+// s1(z-1) + s0(z) + s1(z+1) with half-sample mirrored neighbours (the Neumann structure of
+// D^T D, as in k_cg3d). 2N words of HBM traffic against ~27 L2 reads per cell of the generic
+// grid-stride k_apply_A.
+struct Apply3dArgs {
+    const double* x;
+    double* q;
+    const double* wdiag;
+    double K[8];
+    int m0, m1, m2, tiles_x, tiles_y, zchunk, nblocks;
+};
+
+template <int WM>
+__global__ __launch_bounds__(256) void k_apply3d(const Apply3dArgs a) {
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    if (bid >= a.nblocks) return;
+    const int nt = a.tiles_x * a.tiles_y;
+    const int tz = bid / nt, rem = bid - tz * nt;
+    const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
+    const int x = tx * 64 + int(threadIdx.x & 63), y = ty * 4 + int(threadIdx.x >> 6);
+    const int m0 = a.m0, m1 = a.m1, m2 = a.m2;
+    if (x >= m0 || y >= m1) return;   // no barriers below
+    const int z0 = tz * a.zchunk, z1 = min(m2, z0 + a.zchunk);
+    const size_t pl = size_t(m0) * size_t(m1);
+    const int xl = mirror(x - 1, m0), xr = mirror(x + 1, m0);
+    const size_t yd = size_t(mirror(y - 1, m1)) * m0, yc = size_t(y) * m0, yu = size_t(mirror(y + 1, m1)) * m0;
+    const double K0 = a.K[0], K1 = a.K[1], K2 = a.K[2], K3 = a.K[3];
+    const double K4 = a.K[4], K5 = a.K[5], K6 = a.K[6], K7 = a.K[7];
+    // in-plane sums of plane e: s0 (dz = 0 weights), s1 (dz = +-1 weights)
+    auto sums = [&](int e, double& s0, double& s1) {
+        const double* P = a.x + size_t(e) * pl;
+        const double c = P[yc + x];
+        const double h = P[yc + xl] + P[yc + xr];
+        const double v = P[yd + x] + P[yu + x];
+        const double d = (P[yd + xl] + P[yd + xr]) + (P[yu + xl] + P[yu + xr]);
+        s0 = fma(K0, c, fma(K1, h, fma(K2, v, K3 * d)));
+        s1 = fma(K4, c, fma(K5, h, fma(K6, v, K7 * d)));
+    };
+    double s0c, s1c, s0n, s1n, s1m;
+    sums(z0, s0c, s1c);
+    if (z0 > 0) sums(z0 - 1, s0n, s1m);
+    else s1m = s1c;
+    for (int z = z0; z < z1; ++z) {
+        if (z + 1 < m2) sums(z + 1, s0n, s1n);
+        else s1n = s1c, s0n = s0c;
+        const size_t i = size_t(z) * pl + yc + x;
+        double out = s1m + s0c + s1n;
+        if (WM == W_DIAG) out = fma(a.wdiag[i], a.x[i], out);
+        __builtin_nontemporal_store(out, a.q + i);
+        s1m = s1c;
+        s0c = s0n;
+        s1c = s1n;
+    }
+}
+
+hipError_t launch_apply3d(const Geom& g, hipStream_t s, double sigma, int wmode, const double* wdiag,
+                          const double* x, double* q) {
+    Apply3dArgs a{};
+    a.m0 = int(g.m[0]);
+    a.m1 = int(g.m[1]);
+    a.m2 = int(g.m[2]);
+    a.tiles_x = (a.m0 + 63) / 64;
+    a.tiles_y = (a.m1 + 3) / 4;
+    const int tiles = a.tiles_x * a.tiles_y;
+    int nz = std::max(1, std::min(a.m2, 8192 / std::max(1, tiles)));
+    a.zchunk = (a.m2 + nz - 1) / nz;
+    nz = (a.m2 + a.zchunk - 1) / a.zchunk;
+    a.nblocks = tiles * nz;
+    const int grid = (a.nblocks + 7) / 8 * 8;
+    for (int t = 0; t < 8; ++t) {   // the k_cg3d weights: K(o) = sigma sum_S cS[S] prod_j f_j(o_j)
+        double kk = 0.0;
+        for (int S = 1; S < 8; ++S) {
+            double prod = g.cS[S];
+            for (int j = 0; j < 3; ++j) {
+                const bool off = (t >> j) & 1;
+                prod *= ((S >> j) & 1) ? (off ? -1.0 : 2.0) : (off ? 0.0 : 1.0);
+            }
+            kk += prod;
+        }
+        a.K[t] = sigma * kk;
+    }
+    if (wmode == W_IDENTITY) a.K[0] += 1.0;
+    a.x = x;
+    a.q = q;
+    a.wdiag = wdiag;
+    if (wmode == W_DIAG) klaunch(k_apply3d<W_DIAG>, dim3(grid), dim3(256), 0, s, a);
+    else klaunch(k_apply3d<W_NONE>, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 }  // namespace mvtv

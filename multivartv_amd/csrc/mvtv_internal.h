@@ -177,6 +177,8 @@ hipError_t launch_finalize(hipStream_t s, const double* partials, int nparts, in
 hipError_t launch_admm_control(hipStream_t s, AdmmCtl* ctl, const double* red);
 // fused 3-D Chronopoulos-Gear PCG (mvtv_cg3d.hip): mode 0 prologue, 1 first iteration, 2 iteration;
 // partials get 4 values per workgroup (gamma, delta, |r|^2, |b|^2), *nblocks_out workgroups
+hipError_t launch_apply3d(const Geom& g, hipStream_t s, double sigma, int wmode, const double* wdiag,
+                          const double* x, double* q);
 hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int wmode, const double* wdiag,
                        double* x, const double* r_in, const double* p_in, double* r_out, double* p_out,
                        const double* oty, const double* ga, double ca,
