@@ -8,7 +8,7 @@ if [ -n "$AB_TESTS" ]; then
   env $AB_TEST_ENV timeout -k 10 300 python -u -m pytest $AB_TESTS -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/ab/tests.log 2>&1 || { tail -20 gpurun_out/ab/tests.log; exit 1; }
   tail -2 gpurun_out/ab/tests.log
 fi
-for rep in 1 2; do
+for rep in $(seq 1 ${AB_REPS:-2}); do
   for e in base $AB_ENVS; do
     if [ "$e" = base ]; then ev=""; else ev="$e"; fi
     env $ev timeout -k 10 200 python bench.py --no-cpu --pcg-steps 0 --steps ${AB_STEPS:-30} --warmup 3 > gpurun_out/ab/$e.$rep.json 2> gpurun_out/ab/$e.$rep.err || { echo "bench $e failed"; tail -5 gpurun_out/ab/$e.$rep.err; exit 1; }
