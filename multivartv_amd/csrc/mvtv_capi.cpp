@@ -82,7 +82,7 @@ struct mvtv_problem {
     bool e3d = false;             // z-marching 3-D edge kernels
     bool f3d = false;             // fused 3-D edge update + gather (needs the second edge buffer)
     double* edges2 = nullptr;     // ping-pong partner of edges for the fused kernel
-    double* edges3 = nullptr;     // third z buffer of the spectral loop (default when it fits). On boxes where the fused
+    double* edges3 = nullptr;     // third z buffer of the spectral loop (MVTV_EBUF3=1). On boxes where the fused
                                   // launches alternate fast / slow, the slow ones are those writing into
                                   // `edges` (measured 4.60 / 4.97 ms alternating -> 4.60 / 4.53 / 5.00);
                                   // +7.5 GB at 512^3
@@ -836,12 +836,11 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     const bool track_theta = variant != MVTV_VARIANT_RCPP;
     const bool fused = P->f3d;
     if (fused && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
-    // z rotates over three buffers when a third fits with 16 GiB to spare (MVTV_EBUF3=0 / 1 forces):
-    // same-box A/B at 512^3, fused kernel 5.13 -> 5.04 ms over 4 process pairs, up to -5 % on
-    // boxes whose launches alternate fast / slow (profiles/r01/v8_ebuf3_ab.txt)
+    // MVTV_EBUF3=1: z rotates over three buffers (when the third fits with 16 GiB to spare). Opt-in:
+    // over five boxes it is as often slower as faster than two (profiles/r01/v8_ebuf3_ab.txt)
     static const int rot3_env = [] {
         const char* e = std::getenv("MVTV_EBUF3");
-        return e ? std::atoi(e) : -1;
+        return e ? std::atoi(e) : 0;
     }();
     if (fused && spectral && rot3_env != 0 && !P->edges3) {
         const size_t ne = size_t(P->g.nb) * P->g.N;
