@@ -16,4 +16,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $R/gpurun_out/rel
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $R/gpurun_out/rel/prof_write -o run --output-format csv -- python3 $R/bench.py --no-cpu --pcg-steps 2 --steps 2 --warmup 1 > $R/gpurun_out/rel/prof_write.log 2>&1 &&
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $R/gpurun_out/rel/calib_fetch -o run --output-format csv -- $R/tools/bin/pmc_calib > $R/gpurun_out/rel/calib_fetch.log 2>&1 &&
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $R/gpurun_out/rel/calib_write -o run --output-format csv -- $R/tools/bin/pmc_calib > $R/gpurun_out/rel/calib_write.log 2>&1
-echo "tests rc=$rc release rc=$?"
+rc2=$?; cd $R; [ $rc2 -eq 0 ] && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/rel/smoke.log 2>&1; echo "tests rc=$rc release rc=$rc2 smoke rc=$?"
