@@ -687,12 +687,19 @@ Fused3dArgs f3d_args(const Geom& g) {
         a.tpz = a.tiles_x * a.tiles_y;
     }
     const int tiles = a.tpz;
-    static const int want = [] {
-        const char* e = std::getenv("MVTV_F3D_WG");
-        return e ? std::atoi(e) : 4096;
-    }();
+    // dim-2 chunks: ~4096 workgroups, or up to ~8192 while a chunk keeps >= 32 planes (each chunk
+    // recomputes one plane). 512^3: 6 -> 13 chunks, fused kernel -2 % on two boxes, each setting
+    // timed in one process (tools/zchunk_probe.py, profiles/r01/v10_zchunk_probe.txt)
+    const char* wge = std::getenv("MVTV_F3D_WG");   // read per launch set-up: the probe varies it
     const int nzp = std::max(1, a.zhi - a.zlo);
-    int nz = std::max(1, std::min(nzp, want / std::max(1, tiles)));
+    int nz;
+    if (wge) {
+        nz = std::max(1, std::min(nzp, std::atoi(wge) / std::max(1, tiles)));
+    } else {
+        const int nz4 = std::max(1, std::min(nzp, 4096 / std::max(1, tiles)));
+        const int nz8 = std::min(std::min(nzp, 8192 / std::max(1, tiles)), nzp / 32);
+        nz = std::max(nz4, nz8);
+    }
     while (nz > 1 && ((nz * tiles + 7) / 8 * 8) * 7 > kMaxCgBlocks * kMaxRed) --nz;
     a.zchunk = (nzp + nz - 1) / nz;
     nz = (nzp + a.zchunk - 1) / a.zchunk;
