@@ -388,7 +388,7 @@ hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, c
 namespace f3d {
 constexpr int IW = 64, TX = IW - 1;
 constexpr int SW = 16;   // strip image width: the last m0 % 63 (1..15) columns of dim 0
-int rows();   // image rows per workgroup (8, or 16 with MVTV_F3D_IH=16; 8 measured 2-3 % faster)
+int rows();   // image rows per workgroup (16, or 8 with MVTV_F3D_IH=8)
 }
 
 struct Fused3dArgs {
@@ -657,12 +657,12 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
     }
 }
 
-int f3d::rows() {
-    static const int ih = [] {
-        const char* e = std::getenv("MVTV_F3D_IH");
-        return (e && std::atoi(e) == 16) ? 16 : 8;
-    }();
-    return ih;
+// 16 image rows (one 1024-thread workgroup per CU) by default: 2.6-5 % faster than 8 rows (two
+// 512-thread workgroups per CU) with every setting timed inside one process on two boxes
+// (tools/env_probe.py, profiles/r01/v10_env_probe.txt). MVTV_F3D_IH=8 selects the 8-row image.
+int f3d::rows() {   // read per launch set-up (tools/env_probe.py varies it inside one process)
+    const char* e = std::getenv("MVTV_F3D_IH");
+    return (e && std::atoi(e) == 8) ? 8 : 16;
 }
 
 namespace {
@@ -672,10 +672,8 @@ Fused3dArgs f3d_args(const Geom& g) {
     a.zlo = int(g.ibeg / (g.m[0] * g.m[1]));
     a.zhi = int(g.iend / (g.m[0] * g.m[1]));
     const int TY = f3d::rows() - 1, m0 = int(g.m[0]), r0 = m0 % f3d::TX;
-    static const bool strip_on = [] {
-        const char* e = std::getenv("MVTV_F3D_STRIP");
-        return !e || std::atoi(e) != 0;
-    }();
+    const char* se = std::getenv("MVTV_F3D_STRIP");   // read per launch set-up (tools/env_probe.py)
+    const bool strip_on = !se || std::atoi(se) != 0;
     a.tiles_y = int((int(g.m[1]) + TY - 1) / TY);
     a.strip = strip_on && m0 >= f3d::TX && r0 >= 1 && r0 <= f3d::SW - 1;
     if (a.strip) {
