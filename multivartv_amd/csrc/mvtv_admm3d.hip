@@ -405,6 +405,7 @@ struct Fused3dArgs {
     const AdmmCtl* ctl;
     int tiles_x, tiles_y, zchunk, nblocks, zlo, zhi;
     int strip, tpz;   // k_admm3d: ragged-edge strip tiles on / tiles per z chunk
+    int xcd;          // k_admm3d: contiguous tile runs per XCD (MVTV_F3D_XCD=0: blockIdx order)
 };
 
 // partials: |r|^2, |D theta|^2, |alpha|^2, max dtheta, |g_u|^2, |s_B|^2, |s_A|^2 (max slot 3)
@@ -610,7 +611,7 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
     }
     __shared__ double szr[2 * NB * NT];
     double red[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const int bid = a.xcd ? int((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)) : int(blockIdx.x);
     const bool valid = bid < a.nblocks;
     if (valid) {
         const int tz = bid / a.tpz, rem = bid - tz * a.tpz;
@@ -672,6 +673,8 @@ Fused3dArgs f3d_args(const Geom& g) {
     a.zlo = int(g.ibeg / (g.m[0] * g.m[1]));
     a.zhi = int(g.iend / (g.m[0] * g.m[1]));
     const int TY = f3d::rows() - 1, m0 = int(g.m[0]), r0 = m0 % f3d::TX;
+    const char* xe = std::getenv("MVTV_F3D_XCD");     // read per launch set-up (tools/env_probe.py)
+    a.xcd = !xe || std::atoi(xe) != 0;
     const char* se = std::getenv("MVTV_F3D_STRIP");   // read per launch set-up (tools/env_probe.py)
     const bool strip_on = !se || std::atoi(se) != 0;
     a.tiles_y = int((int(g.m[1]) + TY - 1) / TY);

@@ -10,7 +10,7 @@ import numpy as np  # noqa: E402
 import multivartv_amd as mv  # noqa: E402
 from multivartv_amd.synth import towers  # noqa: E402
 
-KNOBS = ("MVTV_F3D_IH", "MVTV_F3D_STRIP", "MVTV_F3D_WG")
+KNOBS = ("MVTV_F3D_IH", "MVTV_F3D_STRIP", "MVTV_F3D_WG", "MVTV_F3D_XCD")
 m = [512] * 3
 y = towers(m)
 P = mv.Problem(m, y, deltas=[(1.0 + 2e-4) / v for v in m], order=mv.ORDER_CPP, device=0)
