@@ -849,6 +849,18 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         if (rot3_env > 0 || fits) MVTV_TRY(alloc(&P->edges3, ne));
     }
     const int nbuf = (fused && P->edges3) ? 3 : 2;
+    // MVTV_ZFLIP (probe only, tools/zflip_probe.py): move z to the other edge buffer before this run,
+    // so the g_u ping-pong meets the z ping-pong in the other pairing of physical buffers
+    if (fused && nbuf == 2 && std::getenv("MVTV_ZFLIP")) {
+        HIP_TRY(hipMemcpyAsync(P->edges2, P->edges, size_t(P->g.nb) * P->g.N * sizeof(double),
+                               hipMemcpyDeviceToDevice, P->stream));
+        std::swap(P->edges, P->edges2);
+    }
+    if (fused && std::getenv("MVTV_GFLIP")) {   // probe only: the same for the g_u ping-pong
+        HIP_TRY(hipMemcpyAsync(P->gu, P->guprev, size_t(P->g.N) * sizeof(double), hipMemcpyDeviceToDevice,
+                               P->stream));
+        std::swap(P->gu, P->guprev);
+    }
     double dtheta = 0.0;
     if (track_theta) {
         if (!P->thold) MVTV_TRY(alloc(&P->thold, P->g.N));
