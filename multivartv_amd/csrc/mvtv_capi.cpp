@@ -82,6 +82,7 @@ struct mvtv_problem {
     bool e3d = false;             // z-marching 3-D edge kernels
     bool f3d = false;             // fused 3-D edge update + gather (needs the second edge buffer)
     double* edges2 = nullptr;     // ping-pong partner of edges for the fused kernel
+    bool zpicked = false;         // the z ping-pong pair was chosen by timed probes (pick_zpair)
     double* edges3 = nullptr;     // third z buffer of the spectral loop (MVTV_EBUF3=1). On boxes where the fused
                                   // launches alternate fast / slow, the slow ones are those writing into
                                   // `edges` (measured 4.60 / 4.97 ms alternating -> 4.60 / 4.53 / 5.00);
@@ -189,6 +190,73 @@ struct DeviceGuard {
 
 mvtv_status alloc(double** ptr, size_t n) {
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(ptr), std::max<size_t>(n, 1) * sizeof(double)));
+    return MVTV_OK;
+}
+
+// Placement-aware z ping-pong: the fused 3-D kernel's time depends on WHICH physical
+// edge buffer it reads z from and writes to (profiles/r01/v12_zflip_probe.txt: up to 4.70 against
+// 4.15 ms for the two directions of one pair). Once per problem, for meshes of >= 2^24 nodes, time
+// every ordered pair of four candidate buffers with side-effect-free launches (zeroed inputs, no
+// control block, scratch outputs), keep the pair with the lowest round-trip cost, move z into it and
+// free the rest. MVTV_ZPICK=0 keeps the allocation order.
+mvtv_status pick_zpair(mvtv_problem* P, int umode) {
+    P->zpicked = true;
+    const char* env = std::getenv("MVTV_ZPICK");
+    if ((env && std::atoi(env) == 0) || P->g.N < (size_t(1) << 24) || !P->edges2) return MVTV_OK;
+    const size_t ne = size_t(P->g.nb) * P->g.N, bytes = ne * sizeof(double);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < 3 * bytes + (size_t(16) << 30)) return MVTV_OK;
+    constexpr int K = 4, R = 3;
+    double* cand[K] = {P->edges2, nullptr, nullptr, nullptr};
+    for (int i = 1; i < K; ++i)
+        if (alloc(&cand[i], ne) != MVTV_OK) {
+            for (int j = 1; j < i; ++j) (void)hipFree(cand[j]);
+            return MVTV_OK;
+        }
+    double* gtmp[2] = {nullptr, nullptr};   // the probes' g_alpha / g_u outputs (P->ga is state)
+    for (int i = 0; i < 2; ++i)
+        if (alloc(&gtmp[i], P->g.N) != MVTV_OK) {
+            for (int j = 0; j < 2; ++j) (void)hipFree(gtmp[j]);
+            for (int j = 1; j < K; ++j) (void)hipFree(cand[j]);
+            return MVTV_OK;
+        }
+    for (int i = 0; i < K; ++i) HIP_TRY(hipMemsetAsync(cand[i], 0, bytes, P->stream));
+    hipEvent_t ev[2];
+    HIP_TRY(hipEventCreate(&ev[0]));
+    HIP_TRY(hipEventCreate(&ev[1]));
+    double cost[K][K] = {};
+    for (int rep = 0; rep <= R; ++rep)   // rep 0 warms up
+        for (int i = 0; i < K; ++i)
+            for (int j = 0; j < K; ++j) {
+                if (i == j) continue;
+                int np = 0;
+                HIP_TRY(hipEventRecord(ev[0], P->stream));
+                HIP_TRY(launch_admm3d(P->g, P->order, umode, P->stream, P->theta, cand[i], cand[j], 0.0, 1.0, 0.0, 1.0,
+                                      nullptr, gtmp[0], gtmp[1], P->guprev, P->partials, &np, nullptr));
+                HIP_TRY(hipEventRecord(ev[1], P->stream));
+                HIP_TRY(hipEventSynchronize(ev[1]));
+                float ms = 0.f;
+                HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+                if (rep > 0) cost[i][j] += ms;
+            }
+    (void)hipEventDestroy(ev[0]);
+    (void)hipEventDestroy(ev[1]);
+    int a = 0, b = 1;
+    for (int i = 0; i < K; ++i)
+        for (int j = i + 1; j < K; ++j)
+            if (cost[i][j] + cost[j][i] < cost[a][b] + cost[b][a]) a = i, b = j;
+    // the probes wrote only the candidates, gtmp and the partials (scratch until the next reduction)
+    HIP_TRY(hipMemcpyAsync(cand[a], P->edges, bytes, hipMemcpyDeviceToDevice, P->stream));
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    for (int i = 0; i < 2; ++i) (void)hipFree(gtmp[i]);
+    (void)hipFree(P->edges);
+    for (int i = 0; i < K; ++i)
+        if (i != a && i != b) (void)hipFree(cand[i]);
+    P->edges = cand[a];
+    P->edges2 = cand[b];
+    if (std::getenv("MVTV_ZPICK_LOG"))
+        std::fprintf(stderr, "[mvtv] z pair %d,%d: %.3f / %.3f ms (pair 0,1: %.3f / %.3f)\n", a, b, cost[a][b] / R,
+                     cost[b][a] / R, cost[0][1] / R, cost[1][0] / R);
     return MVTV_OK;
 }
 
@@ -861,6 +929,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
                                P->stream));
         std::swap(P->gu, P->guprev);
     }
+    if (fused && spectral && nbuf == 2 && !P->zpicked) MVTV_TRY(pick_zpair(P, mode));
     double dtheta = 0.0;
     if (track_theta) {
         if (!P->thold) MVTV_TRY(alloc(&P->thold, P->g.N));
