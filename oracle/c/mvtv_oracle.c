@@ -160,19 +160,36 @@ static void apply_Dt(const geom_t* g, const double* v, double* out) {
 }
 
 static inline double stencil(const geom_t* g, const double* x, int64_t i, const int64_t* c) {
-    int nt = 1;
-    for (int j = 0; j < g->p; ++j) nt *= 3;
+    /* clamped neighbour offsets per dim (o = 0: -1, 1: 0, 2: +1), then the 3^p terms in t order
+       (dim 0 fastest), the same summation order as the generic index walk */
+    int64_t off[4][3];
+    for (int j = 0; j < 4; ++j) {
+        off[j][0] = (j < g->p && c[j] > 0) ? -g->stride[j] : 0;
+        off[j][1] = 0;
+        off[j][2] = (j < g->p && c[j] + 1 < g->m[j]) ? g->stride[j] : 0;
+    }
     double acc = 0.0;
-    for (int t = 0; t < nt; ++t) {
-        int64_t idx = i;
-        int tt = t;
-        for (int j = 0; j < g->p; ++j) {
-            const int o = tt % 3;
-            tt /= 3;
-            if (o == 0 && c[j] > 0) idx -= g->stride[j];
-            if (o == 2 && c[j] + 1 < g->m[j]) idx += g->stride[j];
-        }
-        acc += g->K[t] * x[idx];
+    const double* K = g->K;
+    const double* xi = x + i;
+    switch (g->p) {
+        case 1:
+            for (int a = 0; a < 3; ++a) acc += K[a] * xi[off[0][a]];
+            break;
+        case 2:
+            for (int b = 0; b < 3; ++b)
+                for (int a = 0; a < 3; ++a) acc += K[a + 3 * b] * xi[off[0][a] + off[1][b]];
+            break;
+        case 3:
+            for (int d = 0; d < 3; ++d)
+                for (int b = 0; b < 3; ++b)
+                    for (int a = 0; a < 3; ++a) acc += K[a + 3 * b + 9 * d] * xi[off[0][a] + off[1][b] + off[2][d]];
+            break;
+        default:
+            for (int e = 0; e < 3; ++e)
+                for (int d = 0; d < 3; ++d)
+                    for (int b = 0; b < 3; ++b)
+                        for (int a = 0; a < 3; ++a)
+                            acc += K[a + 3 * b + 9 * d + 27 * e] * xi[off[0][a] + off[1][b] + off[2][d] + off[3][e]];
     }
     return acc;
 }
@@ -193,13 +210,16 @@ static int pcg(const geom_t* g, const double* W, double sigma, const double* b, 
                double* q, double rtol, int maxit, int fixed, double* relres) {
     const int64_t N = g->N;
     double bb = 0.0, rz = 0.0, rr = 0.0;
+    double* dinv = (double*)malloc(sizeof(double) * N);   /* 1 / Jacobi diagonal, once per solve */
+    if (!dinv) return -1;
 #pragma omp parallel for schedule(static) reduction(+ : bb, rz, rr)
     for (int64_t i = 0; i < N; ++i) {
         int64_t c[4];
         decode(g, i, c);
+        dinv[i] = 1.0 / jdiag(g, W, sigma, i, c);
         const double ax = (W ? W[i] : 1.0) * x[i] + sigma * stencil(g, x, i, c);
         const double ri = b[i] - ax;
-        const double zi = ri / jdiag(g, W, sigma, i, c);
+        const double zi = ri * dinv[i];
         r[i] = ri;
         p[i] = zi;
         bb += b[i] * b[i];
@@ -223,25 +243,20 @@ static int pcg(const geom_t* g, const double* W, double sigma, const double* b, 
         rr = 0.0;
 #pragma omp parallel for schedule(static) reduction(+ : rz2, rr)
         for (int64_t i = 0; i < N; ++i) {
-            int64_t c[4];
-            decode(g, i, c);
             x[i] += alpha * p[i];
             const double ri = r[i] - alpha * q[i];
             r[i] = ri;
-            const double zi = ri / jdiag(g, W, sigma, i, c);
+            const double zi = ri * dinv[i];
             rz2 += ri * zi;
             rr += ri * ri;
         }
         const double beta = rz2 / rz;
         rz = rz2;
 #pragma omp parallel for schedule(static)
-        for (int64_t i = 0; i < N; ++i) {
-            int64_t c[4];
-            decode(g, i, c);
-            p[i] = r[i] / jdiag(g, W, sigma, i, c) + beta * p[i];
-        }
+        for (int64_t i = 0; i < N; ++i) p[i] = r[i] * dinv[i] + beta * p[i];
         ++it;
     }
+    free(dinv);
     *relres = bb > 0 ? sqrt(rr / bb) : 0.0;
     return it;
 }

@@ -35,20 +35,3 @@ def test_spectral_and_pcg_trajectories_agree(m, iters):
     assert ss["r_norm"] == pytest.approx(sp["r_norm"], rel=1e-8)
     assert ss["s_norm"] == pytest.approx(sp["s_norm"], rel=1e-8)
 
-
-def test_path_warm_start_2d_2048_lambda_chunk():
-    """Config 4's per-GPU work item: 4 lambdas of a 2048^2 path, warm-started, to convergence
-    (first lambda capped); iteration counts stay positive and rho stays a power-of-two multiple."""
-    m = [2048, 2048]
-    y = towers(m)
-    deltas = [(1.0 + 2e-4) / v for v in m]
-    from multivartv_amd import cv
-    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
-        lmax, it = P.lambda_max()
-        lams = np.exp(np.linspace(np.log(lmax * 1e-4), np.log(lmax), 32))[::-1][8:12]
-        thetas, stats = cv.mbs_path(P, lams, float(y.mean()))
-    assert len(thetas) == 4 and all(s["iters"] > 0 for s in stats)
-    r0 = lams[0] / 5
-    for s in stats:
-        k = np.log2(s["rho"] / r0)
-        assert abs(k - round(k)) < 1e-12          # adapt_step multiplies rho by 2 or 1/2 (tau = 2)

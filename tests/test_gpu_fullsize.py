@@ -1,0 +1,83 @@
+"""BASELINE.json configs at their real shapes, anchored to the CPU oracle where it finishes in seconds.
+
+* metric config, 3-D 512^3: the spectral solve and the Jacobi-PCG (rtol 1e-13) follow the same
+  variant-B trajectory (rcpp-code/MultivarTV/src/solvers.cpp:110-133) for 3 fixed iterations;
+* config 5, 4-D 128^4 on one GPU: the same agreement for 2 iterations (one process holds the whole
+  128^4 mesh: 15 edge blocks, 32 GB of edge state);
+* config 4's work item, 2-D 2048^2 with a 0/1 CV-fold mask W (rcpp…/solvers.cpp:340-353): a
+  warm-started lambda chunk (4 lambdas x 3 fixed iterations, theta / u / rho carried,
+  rcpp…/solvers.cpp:212-220) against oracle/c/mvtv_oracle.c run on the same inputs, which follows
+  the same warm-start chain on the host.
+
+Tolerances: with identical adapt_step decisions theta differs only by the theta-solve's accuracy
+(PCG rtol 1e-13 on both sides): |dtheta| <= 1e-9 max|theta|; rho exactly; r and s norms 1e-8 rel.
+"""
+import numpy as np
+import pytest
+
+mv = pytest.importorskip("multivartv_amd")
+from multivartv_amd import cv  # noqa: E402
+from multivartv_amd.synth import towers  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _two_solvers(m, iters):
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    out = {}
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        assert P.spectral_ok()
+        th0 = np.full(y.size, y.mean())
+        del y
+        for solver in (mv.SOLVER_SPECTRAL, mv.SOLVER_PCG):
+            P.state_set(th0, None, 0.2)
+            st = P.run(1.0, fixed_iters=iters, pcg_rtol=1e-13, theta_solver=solver)
+            th, _, rho = P.state_get(want_u=False)
+            out[solver] = (th, rho, st)
+    (ts, rs, ss), (tp, rp, sp) = out[mv.SOLVER_SPECTRAL], out[mv.SOLVER_PCG]
+    assert ss["theta_solver"] == mv.SOLVER_SPECTRAL and sp["theta_solver"] == mv.SOLVER_PCG
+    assert ss["iters"] == sp["iters"] == iters
+    assert rs == rp
+    assert np.max(np.abs(ts - tp)) <= 1e-9 * np.max(np.abs(tp))
+    assert ss["r_norm"] == pytest.approx(sp["r_norm"], rel=1e-8)
+    assert ss["s_norm"] == pytest.approx(sp["s_norm"], rel=1e-8)
+    return ss, sp
+
+
+def test_metric_config_512_cubed():
+    ss, sp = _two_solvers([512, 512, 512], 3)
+    assert sp["pcg_unconverged"] == 0
+
+
+def test_config5_4d_128_single_gpu():
+    ss, sp = _two_solvers([128, 128, 128, 128], 2)
+    assert sp["pcg_unconverged"] == 0
+
+
+def test_config4_fold_path_2048_vs_c_oracle():
+    from oracle import c_oracle
+    m = [2048, 2048]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    fold = cv.kfoldinds(y.size, 5, seed=0)
+    W = (fold != 0).astype(np.float64)          # training rows of fold 0: O^T O on the lattice
+    oty = W * y                                  # O^T y
+    ymean = float(y[W > 0].mean())
+    lams = np.array([1.6, 1.2, 0.9, 0.7])
+    iters = 3
+    with mv.Problem(m, oty, wdiag=W, deltas=deltas, order=mv.ORDER_CPP) as P:
+        assert not P.spectral_ok()
+        thetas, rhos, stats = P.path(lams, np.full(y.size, ymean), lams[0] / 5.0, fixed_iters=iters,
+                                     pcg_rtol=1e-13)
+    th = np.full(y.size, ymean)
+    u = np.zeros(c_oracle.num_edges(m))
+    rho = lams[0] / 5.0
+    for k, lam in enumerate(lams):
+        st = c_oracle.admm_rcpp(m, oty, lam, th, u, rho, deltas, W=W, fixed_iters=iters, pcg_rtol=1e-13)
+        rho = st["rho"]
+        assert stats[k]["iters"] == iters and stats[k]["theta_solver"] == mv.SOLVER_PCG
+        assert rhos[k] == rho
+        assert np.max(np.abs(thetas[k] - th)) <= 1e-9 * np.max(np.abs(th)), k
+        assert stats[k]["r_norm"] == pytest.approx(st["r_norm"], rel=1e-8)
+        assert stats[k]["s_norm"] == pytest.approx(st["s_norm"], rel=1e-8)

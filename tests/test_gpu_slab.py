@@ -103,3 +103,31 @@ def test_rccl_transport_single_rank(fixed):
     assert p.exitcode == 0
     assert r[1] == st["iters"] and r[2] == rho
     assert _rel(r[3], th) <= 1e-11
+
+
+def test_slab_4d_16_four_ranks_vs_c_oracle():
+    """Config 5's decomposition (4-D, dim 3 split, 4 planes per rank) against the C oracle rather
+    than the one-GPU HIP path: 20 fixed iterations of variant B from theta0 = mean y, u0 = 0."""
+    import torch.multiprocessing as mp
+    from oracle import c_oracle
+    m, lam, world, fixed = [16, 16, 16, 16], 1.0, 4, 20
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    th = np.full(y.size, y.mean())
+    u = np.zeros(c_oracle.num_edges(m))
+    ref = c_oracle.admm_rcpp(m, y, lam, th, u, lam / 5.0, deltas, fixed_iters=fixed, pcg_rtol=1e-13)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, m, lam, fixed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=100) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in res:
+        assert r[1] == fixed and r[2] == ref["rho"]
+    assert _rel(np.concatenate([r[3] for r in res]), th) <= 1e-9
