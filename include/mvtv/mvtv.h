@@ -185,6 +185,10 @@ mvtv_status mvtv_solve(mvtv_problem* prob, double sigma, const double* b, double
  * 5 ||D x||_inf with x from the reference's CG on D^T D x = O^T y (relative stop 1e-4, at most
  * min(N, 2000) iterations), its recurrences reproduced step by step on the GPU. */
 mvtv_status mvtv_lambda_max(mvtv_problem* prob, double* out, int32_t* iters);
+/* lam_max_pinv of variant A (cpp-code/utils.cpp:354-404, called by create_lambdas cpp-code/solvers.cpp:
+ * 179-192): ||D x||_inf with x from cg(D^T D, O^T y): x0 = mean(O^T y), absolute stop ||r|| < 0.01, at most
+ * 500 iterations (N < 400) or 100 */
+mvtv_status mvtv_lambda_max_cpp(mvtv_problem* prob, double* out, int32_t* iters);
 /* direct theta-solve (I + sigma D^T D) x = b by cosine transforms (MVTV_SOLVER_SPECTRAL) */
 mvtv_status mvtv_solve_spectral(mvtv_problem* prob, double sigma, const double* b, double* x_out);
 

@@ -46,6 +46,8 @@ struct mbs_cache {
     std::vector<int64_t> oidx;      // O as nearest-mesh indices
     vec oty, w;
     int64_t ntheta = 0, rowsD = 0;
+    vec deltas;                     // block weights of D (empty: every weight 1, cpp-code mbs_one without cache)
+    double sp_sigma = 0.0;          // variant A: sp_crosses = crossO + sp_sigma * crossD (cpp-code/solvers.hpp:26)
     mbs_cache() = default;
     mbs_cache(const mbs_cache&) = delete;
     mbs_cache& operator=(const mbs_cache&) = delete;
@@ -65,7 +67,8 @@ struct admm_out {
 // B: rcpp…/solvers.hpp:100 (y is unused by the loop, kept for signature parity)
 void admm_update(const vec& y, mbs_cache& inits, vec& theta_init, double lambda, bool verbose, vec& u_init,
                  double& rho_init, admm_out& out);
-// A: cpp-code/solvers.hpp:85 — throws std::invalid_argument("Failed to converge!") past 2000 iterations
+// A: cpp-code/solvers.hpp:85 — throws std::invalid_argument("Failed to converge!") past 2000 iterations;
+// the solve matrix is crossO + lambda crossD (mbs_one's, :144). See also the variant-A overload below.
 vec admm_update_cpp(const vec& y, mbs_cache& inits, const vec* theta_init, double lambda);
 
 struct mbs_one_object {   // rcpp…/solvers.hpp:52-61
@@ -121,5 +124,58 @@ struct mbs_impl_result {
 mbs_impl_result mbs_impl(const mat& data, const vec& y, const vec& m, const mat* mesh, int n_lambda,
                          const vec* ftrue, const vec* lambdas, int folds, bool verbose = false, uint64_t seed = 0,
                          int device = 0);
+
+// ---- variant A: the research code's API, cpp-code/solvers.hpp ------------------------------------
+// Its own setup constants: EPS = 0.01 (cpp-code/solvers.hpp:13, utils.hpp), TOL = 1e-3.
+// create_deltas (cpp-code/utils.cpp:300-307): (max - min + 2 EPS) / m_j
+vec create_deltas_cpp(const mat& data, const vec& m);
+// create_mesh (cpp-code/utils.cpp:271-298): axis j = linspace(min + EPS, max + EPS, m_j) (both ends shifted
+// up), stored in a float matrix (typedef fmat MAT): every mesh value is rounded to float
+mat create_mesh_cpp(const mat& data, const vec& m);
+// create_cache_objects (cpp-code/solvers.cpp:31-41): O, D (weights from `deltas`; empty: all 1), O^T O, O^T y
+void create_cache_objects_cpp(const mat& data, const vec& y, const mat& mesh, const vec& m, const vec& deltas,
+                              mbs_cache& cache, int device = 0);
+// create_lambdas (cpp-code/solvers.cpp:179-192): flipud(exp(linspace(log(1e-5 lmax), log(lmax), n))) with
+// lmax = lam_max_pinv (cpp-code/utils.cpp:354-404, GPU: mvtv_lambda_max_cpp)
+vec create_lambdas_cpp(int n_lambda, mbs_cache& inits, const vec* lambdas, double* lambda_max = nullptr);
+// admm_update (cpp-code/solvers.hpp:85) on inits.sp_sigma's matrix; y gives mean(y) for theta_old
+vec admm_update(const vec& y, mbs_cache& inits, const vec* theta_init, double lambda);
+// mbs_one (cpp-code/solvers.hpp:89, solvers.cpp:134-152). cache == nullptr: O and D are built here with EMPTY
+// deltas, so every block weight is 1, and the matrix is crossO + lambda crossD; otherwise the
+// cache's D and its sp_sigma matrix are used. Throws std::invalid_argument("Failed to converge!") past 2000
+// iterations (:122-124).
+void mbs_one(const mat& data, const vec& y, const vec& m, mbs_one_object& output, const mat& mesh,
+             const vec* theta_init = nullptr, double lambda = 1.0, mbs_cache* cache = nullptr, int device = 0);
+
+// mbs (cpp-code/solvers.hpp:129, solvers.cpp:277-310): k-fold CV over a lambda path, refit at the best lambda.
+// The reference's CV differs from a textbook CV in three ways, all reproduced when reference_cv is set
+// (the default, so results match the reference's code):
+//   1. the cache (O, O^T y, O^T O) is built once on the FULL data and never rebuilt per fold (:288-301): each
+//      fold's path fits all n points and differs from the others only through mean(y_train) (theta_0 and
+//      theta_old, :199, :103);
+//   2. the path object accumulates models over folds and test_mse reads models[0 .. n_lambda-1] (:264-273),
+//      so every fold's test MSE is computed with fold 0's path;
+//   3. the refit (:248-260) starts from fold 0's model at the best lambda and solves with the matrix the
+//      last path left in the cache, crossO + lambdas[n_lambda-1] crossD (:209).
+// reference_cv = false: each fold's path runs on its own training cache, test MSEs use that fold's models,
+// and the refit solves with crossO + best_lambda crossD from mean(y).
+// kfold (cpp-code/utils.cpp:417-436) shuffles rows with Armadillo's RNG, which cannot be reproduced outside
+// that build; here the row order is the seeded permutation kfold_perm(n, seed), then fold i tests rows
+// [i n/k, (i+1) n/k) of it and trains on the others in permuted order, as the reference.
+struct mbs_cpp_options {
+    uint64_t seed = 0;
+    bool reference_cv = true;
+    int device = 0;
+};
+struct mbs_cpp_report {        // what mbs computed on the way (the reference keeps these local)
+    vec lambdas;
+    double lambda_max = 0.0;
+    mat mse_mat;               // n_lambda x folds (:296, :303)
+    int64_t best = 0;          // 0-based row of the smallest row mean (:249-251)
+};
+std::vector<int64_t> kfold_perm(int64_t n, uint64_t seed);
+void mbs(const mat& data, const vec& y, const vec& m, mbs_one_object& output, const mat* mesh = nullptr,
+         int n_lambda = 100, const vec* ftrue = nullptr, const vec* lambdas = nullptr, int folds = 5,
+         const mbs_cpp_options& opts = mbs_cpp_options(), mbs_cpp_report* report = nullptr);
 
 }  // namespace mvtv

@@ -94,6 +94,7 @@ SIGNATURES = {
     "mvtv_solve": (C.c_int, [C.c_void_p, C.c_double, _dp, _dp, C.c_double, C.c_int32, C.POINTER(C.c_int32), _dp]),
     "mvtv_solve_spectral": (C.c_int, [C.c_void_p, C.c_double, _dp, _dp]),
     "mvtv_lambda_max": (C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int32)]),
+    "mvtv_lambda_max_cpp": (C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_int32)]),
     "mvtv_timing_enable": (C.c_int, [C.c_void_p, C.c_int32]),
     "mvtv_timing_get": (C.c_int, [C.c_void_p, C.c_int32, _dp, C.POINTER(C.c_int64), _dp]),
     "mvtv_kernel_name": (C.c_char_p, [C.c_int32]),
@@ -351,6 +352,12 @@ class Problem:
         """lam_max_pinv of the released package on the GPU: (lambda_max, CG iterations)."""
         v, it = C.c_double(), C.c_int32()
         _check(lib().mvtv_lambda_max(self._h, C.byref(v), C.byref(it)))
+        return v.value, it.value
+
+    def lambda_max_cpp(self):
+        """lam_max_pinv of the research code (cpp-code/utils.cpp:354-404) on the GPU: (lambda_max, CG iterations)."""
+        v, it = C.c_double(), C.c_int32()
+        _check(lib().mvtv_lambda_max_cpp(self._h, C.byref(v), C.byref(it)))
         return v.value, it.value
 
     def spectral_ok(self) -> bool:

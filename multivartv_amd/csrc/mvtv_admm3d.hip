@@ -231,7 +231,7 @@ __global__ __launch_bounds__(NT) void k_gather3d(const Edge3dArgs a) {
 namespace {
 int e3d_rows() {
     static const int ty = [] {
-        const char* e = std::getenv("MVTV_E3D_TY");
+        const char* e = probe_env("MVTV_E3D_TY");
         const int v = e ? std::atoi(e) : 4;
         return v == 8 ? 8 : 4;
     }();
@@ -249,7 +249,7 @@ Edge3dArgs e3d_args(const Geom& g) {
     // dim-2 chunks: enough workgroups to fill 256 CUs several times over, long enough marches
     // that the carried plane (gather) and the extra theta plane (edge) are amortised
     static const int want = [] {
-        const char* e = std::getenv("MVTV_E3D_WG");
+        const char* e = probe_env("MVTV_E3D_WG");
         return e ? std::atoi(e) : 8192;
     }();
     const int nzp = std::max(1, a.zhi - a.zlo);
@@ -276,7 +276,7 @@ hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, co
 
 bool edge3d_ok(const Geom& g) {
     if (g.p == 4) return edge4d_ok(g);
-    if (g.p != 3 || std::getenv("MVTV_E3D_OFF")) return false;
+    if (g.p != 3 || probe_env("MVTV_E3D_OFF")) return false;
     const Edge3dArgs a = e3d_args(g);
     return (a.nblocks + 7) / 8 * 8 <= kMaxCgBlocks;
 }
@@ -331,7 +331,7 @@ hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, c
                                   scratch4);
         // 4-D: the marching gather (k_gather4d) reads ~65 neighbour words per cell through L1/L2 and
         // measured slower at 128^4 (20.8 vs 18.4 ms) than the grid-stride kernel; opt-in only
-        static const bool marching = std::getenv("MVTV_G4D") != nullptr;
+        static const bool marching = probe_env("MVTV_G4D") != nullptr;
         if (marching)
             return launch_gather4d(g, order, umode, s, edges, t, g_alpha, g_u, g_uprev, c_prev, partials, nparts, ctl);
         const int grid = int(std::min<uint64_t>((uint64_t(g.N) + kThreads - 1) / kThreads, kMaxGrid));
@@ -662,7 +662,7 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
 // 512-thread workgroups per CU) with every setting timed inside one process on two boxes
 // (tools/env_probe.py, profiles/r01/v10_env_probe.txt). MVTV_F3D_IH=8 selects the 8-row image.
 int f3d::rows() {   // read per launch set-up (tools/env_probe.py varies it inside one process)
-    const char* e = std::getenv("MVTV_F3D_IH");
+    const char* e = probe_env("MVTV_F3D_IH");
     return (e && std::atoi(e) == 8) ? 8 : 16;
 }
 
@@ -673,9 +673,9 @@ Fused3dArgs f3d_args(const Geom& g) {
     a.zlo = int(g.ibeg / (g.m[0] * g.m[1]));
     a.zhi = int(g.iend / (g.m[0] * g.m[1]));
     const int TY = f3d::rows() - 1, m0 = int(g.m[0]), r0 = m0 % f3d::TX;
-    const char* xe = std::getenv("MVTV_F3D_XCD");     // read per launch set-up (tools/env_probe.py)
+    const char* xe = probe_env("MVTV_F3D_XCD");     // read per launch set-up (tools/env_probe.py)
     a.xcd = !xe || std::atoi(xe) != 0;
-    const char* se = std::getenv("MVTV_F3D_STRIP");   // read per launch set-up (tools/env_probe.py)
+    const char* se = probe_env("MVTV_F3D_STRIP");   // read per launch set-up (tools/env_probe.py)
     const bool strip_on = !se || std::atoi(se) != 0;
     a.tiles_y = int((int(g.m[1]) + TY - 1) / TY);
     a.strip = strip_on && m0 >= f3d::TX && r0 >= 1 && r0 <= f3d::SW - 1;
@@ -691,7 +691,7 @@ Fused3dArgs f3d_args(const Geom& g) {
     // dim-2 chunks: ~4096 workgroups, or up to ~8192 while a chunk keeps >= 32 planes (each chunk
     // recomputes one plane). 512^3: 6 -> 13 chunks, fused kernel -2 % on two boxes, each setting
     // timed in one process (tools/zchunk_probe.py, profiles/r01/v10_zchunk_probe.txt)
-    const char* wge = std::getenv("MVTV_F3D_WG");   // read per launch set-up: the probe varies it
+    const char* wge = probe_env("MVTV_F3D_WG");   // read per launch set-up: the probe varies it
     const int nzp = std::max(1, a.zhi - a.zlo);
     int nz;
     if (wge) {
@@ -717,7 +717,7 @@ hipError_t launch_admm2d(const Geom& g, int order, int umode, hipStream_t s, con
 
 bool fused3d_ok(const Geom& g) {
     if (g.p == 2) return fused2d_ok(g);
-    if (g.p != 3 || std::getenv("MVTV_F3D_OFF")) return false;
+    if (g.p != 3 || probe_env("MVTV_F3D_OFF")) return false;
     const Fused3dArgs a = f3d_args(g);
     return ((a.nblocks + 7) / 8 * 8) * 7 <= kMaxCgBlocks * kMaxRed;
 }
@@ -991,7 +991,7 @@ Edge4dArgs e4d_args(const Geom& g) {
 }  // namespace
 
 bool edge4d_ok(const Geom& g) {
-    if (g.p != 4 || std::getenv("MVTV_E3D_OFF")) return false;
+    if (g.p != 4 || probe_env("MVTV_E3D_OFF")) return false;
     const Edge4dArgs a = e4d_args(g);
     return (a.nblocks + 7) / 8 * 8 <= kMaxCgBlocks;
 }
@@ -1240,7 +1240,7 @@ __global__ __launch_bounds__(g4::NTB) void k_gather4b(const Gather4Args a) {
 }
 
 bool gather4_ok(const Geom& g) {
-    if (g.p != 4 || std::getenv("MVTV_G4D") || std::getenv("MVTV_G4_OFF")) return false;
+    if (g.p != 4 || probe_env("MVTV_G4D") || probe_env("MVTV_G4_OFF")) return false;
     const uint32_t pl = g.m[0] * g.m[1] * g.m[2];
     const int nwp = int(g.iend / pl) - int(g.ibeg / pl);
     const int per = int((pl + g4::NTB - 1) / g4::NTB);
@@ -1499,7 +1499,7 @@ Fused3dArgs f2d_args(const Geom& g) {
     a.g = g;
     a.tiles_x = int((g.m[0] + f2d::TX - 1) / f2d::TX);
     static const int want = [] {
-        const char* e = std::getenv("MVTV_F2D_WAVES");
+        const char* e = probe_env("MVTV_F2D_WAVES");
         return e ? std::atoi(e) : 2048;   // 2048^2: 2048 waves 75.8 us, 4096 81.8, 8192 81.0
     }();
     const int m1 = int(g.m[1]);
@@ -1514,7 +1514,7 @@ Fused3dArgs f2d_args(const Geom& g) {
 }  // namespace
 
 bool fused2d_ok(const Geom& g) {
-    if (g.p != 2 || std::getenv("MVTV_F2D_OFF") || g.ibeg != 0 || g.iend != g.N) return false;
+    if (g.p != 2 || probe_env("MVTV_F2D_OFF") || g.ibeg != 0 || g.iend != g.N) return false;
     const Fused3dArgs a = f2d_args(g);
     const int wg = (a.nblocks + f2d::NT / 64 - 1) / (f2d::NT / 64);
     return ((wg + 7) / 8 * 8) * 7 <= kMaxCgBlocks * kMaxRed;

@@ -195,68 +195,82 @@ mvtv_status alloc(double** ptr, size_t n) {
 
 // Placement-aware z ping-pong: the fused 3-D kernel's time depends on WHICH physical
 // edge buffer it reads z from and writes to (profiles/r01/v12_zflip_probe.txt: up to 4.70 against
-// 4.15 ms for the two directions of one pair). Once per problem, for meshes of >= 2^24 nodes, time
-// every ordered pair of four candidate buffers with side-effect-free launches (zeroed inputs, no
-// control block, scratch outputs), keep the pair with the lowest round-trip cost, move z into it and
-// free the rest. MVTV_ZPICK=0 keeps the allocation order.
-mvtv_status pick_zpair(mvtv_problem* P, int umode) {
+// 4.15 ms for the two directions of one pair). Once per problem, for 3-D meshes of >= 2^24 nodes, time
+// every ordered pair of four candidate buffers (candidate 0 = edges2, 1..3 = new allocations; `edges`
+// holds the state and is not a candidate) with side-effect-free launches of the steady-state kernel
+// (zeroed z, scratch outputs, no control block), keep the pair with the lowest round-trip cost, move z into
+// it and free the rest. Best effort: any failure (allocation, launch) leaves the allocation-order pair in
+// place, frees everything the probe allocated and clears HIP's error state. MVTV_ZPICK=0 turns it off
+// (MVTV_ZPICK=fail: allocate, then take the failure path; tests/test_gpu_zpick.py).
+mvtv_status pick_zpair(mvtv_problem* P, bool track_theta) {
     P->zpicked = true;
     const char* env = std::getenv("MVTV_ZPICK");
-    if ((env && std::atoi(env) == 0) || P->g.N < (size_t(1) << 24) || !P->edges2) return MVTV_OK;
+    if ((env && std::atoi(env) == 0) || P->g.p != 3 || P->g.N < (size_t(1) << 24) || !P->edges2) return MVTV_OK;
     const size_t ne = size_t(P->g.nb) * P->g.N, bytes = ne * sizeof(double);
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < 3 * bytes + (size_t(16) << 30)) return MVTV_OK;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < 3 * bytes + (size_t(16) << 30)) {
+        (void)hipGetLastError();
+        return MVTV_OK;
+    }
     constexpr int K = 4, R = 3;
     double* cand[K] = {P->edges2, nullptr, nullptr, nullptr};
-    for (int i = 1; i < K; ++i)
-        if (alloc(&cand[i], ne) != MVTV_OK) {
-            for (int j = 1; j < i; ++j) (void)hipFree(cand[j]);
-            return MVTV_OK;
-        }
-    double* gtmp[2] = {nullptr, nullptr};   // the probes' g_alpha / g_u outputs (P->ga is state)
-    for (int i = 0; i < 2; ++i)
-        if (alloc(&gtmp[i], P->g.N) != MVTV_OK) {
-            for (int j = 0; j < 2; ++j) (void)hipFree(gtmp[j]);
-            for (int j = 1; j < K; ++j) (void)hipFree(cand[j]);
-            return MVTV_OK;
-        }
-    for (int i = 0; i < K; ++i) HIP_TRY(hipMemsetAsync(cand[i], 0, bytes, P->stream));
-    hipEvent_t ev[2];
-    HIP_TRY(hipEventCreate(&ev[0]));
-    HIP_TRY(hipEventCreate(&ev[1]));
+    double* tmp[3] = {nullptr, nullptr, nullptr};   // the probes' g_alpha / g_u outputs and theta_old input
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool ok = true;
+    auto hip = [&](hipError_t e) {
+        if (e != hipSuccess) ok = false;
+        return ok;
+    };
+    for (int i = 1; i < K && ok; ++i) hip(hipMalloc(reinterpret_cast<void**>(&cand[i]), bytes));
+    for (int i = 0; i < 3 && ok; ++i) hip(hipMalloc(reinterpret_cast<void**>(&tmp[i]), size_t(P->g.N) * sizeof(double)));
+    for (int i = 0; i < K && ok; ++i) hip(hipMemsetAsync(cand[i], 0, bytes, P->stream));
+    if (ok) hip(hipMemsetAsync(tmp[2], 0, size_t(P->g.N) * sizeof(double), P->stream));
+    if (ok) hip(hipEventCreate(&ev[0]));
+    if (ok) hip(hipEventCreate(&ev[1]));
+    if (env && std::strcmp(env, "fail") == 0) ok = false;   // test hook: take the failure path after allocating
     double cost[K][K] = {};
-    for (int rep = 0; rep <= R; ++rep)   // rep 0 warms up
-        for (int i = 0; i < K; ++i)
-            for (int j = 0; j < K; ++j) {
+    for (int rep = 0; rep <= R && ok; ++rep)   // rep 0 warms up
+        for (int i = 0; i < K && ok; ++i)
+            for (int j = 0; j < K && ok; ++j) {
                 if (i == j) continue;
                 int np = 0;
-                HIP_TRY(hipEventRecord(ev[0], P->stream));
-                HIP_TRY(launch_admm3d(P->g, P->order, umode, P->stream, P->theta, cand[i], cand[j], 0.0, 1.0, 0.0, 1.0,
-                                      nullptr, gtmp[0], gtmp[1], P->guprev, P->partials, &np, nullptr));
-                HIP_TRY(hipEventRecord(ev[1], P->stream));
-                HIP_TRY(hipEventSynchronize(ev[1]));
                 float ms = 0.f;
-                HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
-                if (rep > 0) cost[i][j] += ms;
+                if (hip(hipEventRecord(ev[0], P->stream)) &&
+                    hip(launch_admm3d(P->g, P->order, U_FROM_Z, P->stream, P->theta, cand[i], cand[j], 0.0, 1.0, 0.0,
+                                      1.0, track_theta ? tmp[2] : nullptr, tmp[0], tmp[1], P->guprev, P->partials,
+                                      &np, nullptr)) &&
+                    hip(hipEventRecord(ev[1], P->stream)) && hip(hipEventSynchronize(ev[1])) &&
+                    hip(hipEventElapsedTime(&ms, ev[0], ev[1])) && rep > 0)
+                    cost[i][j] += ms;
             }
-    (void)hipEventDestroy(ev[0]);
-    (void)hipEventDestroy(ev[1]);
     int a = 0, b = 1;
-    for (int i = 0; i < K; ++i)
-        for (int j = i + 1; j < K; ++j)
-            if (cost[i][j] + cost[j][i] < cost[a][b] + cost[b][a]) a = i, b = j;
-    // the probes wrote only the candidates, gtmp and the partials (scratch until the next reduction)
-    HIP_TRY(hipMemcpyAsync(cand[a], P->edges, bytes, hipMemcpyDeviceToDevice, P->stream));
-    HIP_TRY(hipStreamSynchronize(P->stream));
-    for (int i = 0; i < 2; ++i) (void)hipFree(gtmp[i]);
+    if (ok) {
+        for (int i = 0; i < K; ++i)
+            for (int j = i + 1; j < K; ++j)
+                if (cost[i][j] + cost[j][i] < cost[a][b] + cost[b][a]) a = i, b = j;
+        // the probes wrote only the candidates, tmp and the partials (scratch until the next reduction)
+        ok = hip(hipMemcpyAsync(cand[a], P->edges, bytes, hipMemcpyDeviceToDevice, P->stream)) &&
+             hip(hipStreamSynchronize(P->stream));
+    }
+    (void)hipStreamSynchronize(P->stream);
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto t : tmp)
+        if (t) (void)hipFree(t);
+    if (!ok) {   // keep (edges, edges2); the candidates' contents were never used
+        for (int i = 1; i < K; ++i)
+            if (cand[i]) (void)hipFree(cand[i]);
+        (void)hipGetLastError();
+        return MVTV_OK;
+    }
     (void)hipFree(P->edges);
     for (int i = 0; i < K; ++i)
         if (i != a && i != b) (void)hipFree(cand[i]);
     P->edges = cand[a];
     P->edges2 = cand[b];
-    if (std::getenv("MVTV_ZPICK_LOG"))
-        std::fprintf(stderr, "[mvtv] z pair %d,%d: %.3f / %.3f ms (pair 0,1: %.3f / %.3f)\n", a, b, cost[a][b] / R,
-                     cost[b][a] / R, cost[0][1] / R, cost[1][0] / R);
+    if (probe_env("MVTV_ZPICK_LOG"))
+        std::fprintf(stderr, "[mvtv] z pair %d,%d: %.3f / %.3f ms (candidate 0 = edges2, 1-3 new; pair 0,1: %.3f / %.3f)\n",
+                     a, b, cost[a][b] / R, cost[b][a] / R, cost[0][1] / R, cost[1][0] / R);
     return MVTV_OK;
 }
 
@@ -456,7 +470,7 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
     // back; the MID dimension defaults to p-1 (MVTV_DCT_MID selects another one for experiments)
     const int p = P->g.p;
     static const int mid_env = [] {
-        const char* e = std::getenv("MVTV_DCT_MID");
+        const char* e = probe_env("MVTV_DCT_MID");
         return e ? std::atoi(e) : -1;
     }();
     const int mid = (mid_env >= 1 && mid_env < p) ? mid_env : p - 1;
@@ -735,7 +749,7 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
     P->f3d = !sl && fused3d_ok(g);
     {   // chunked edge layout for the 3-D fused path (MVTV_EAOS=0 keeps block-major): the fused kernel's
         // launches 2-4 % shorter at 512^3 on the same box (4.21 -> 4.13 ms, 5.2-5.36 -> 5.13 ms)
-        const char* e = std::getenv("MVTV_EAOS");
+        const char* e = probe_env("MVTV_EAOS");
         const bool want = e ? std::atoi(e) != 0 : true;
         g.eaos = (want && P->f3d && g.p == 3 && g.N % 64 == 0) ? 1u : 0u;
     }
@@ -907,7 +921,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     // MVTV_EBUF3=1: z rotates over three buffers (when the third fits with 16 GiB to spare). Opt-in:
     // over five boxes it is as often slower as faster than two (profiles/r01/v8_ebuf3_ab.txt)
     static const int rot3_env = [] {
-        const char* e = std::getenv("MVTV_EBUF3");
+        const char* e = probe_env("MVTV_EBUF3");
         return e ? std::atoi(e) : 0;
     }();
     if (fused && spectral && rot3_env != 0 && !P->edges3) {
@@ -919,17 +933,17 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     const int nbuf = (fused && P->edges3) ? 3 : 2;
     // MVTV_ZFLIP (probe only, tools/zflip_probe.py): move z to the other edge buffer before this run,
     // so the g_u ping-pong meets the z ping-pong in the other pairing of physical buffers
-    if (fused && nbuf == 2 && std::getenv("MVTV_ZFLIP")) {
+    if (fused && nbuf == 2 && probe_env("MVTV_ZFLIP")) {
         HIP_TRY(hipMemcpyAsync(P->edges2, P->edges, size_t(P->g.nb) * P->g.N * sizeof(double),
                                hipMemcpyDeviceToDevice, P->stream));
         std::swap(P->edges, P->edges2);
     }
-    if (fused && std::getenv("MVTV_GFLIP")) {   // probe only: the same for the g_u ping-pong
+    if (fused && probe_env("MVTV_GFLIP")) {   // probe only: the same for the g_u ping-pong
         HIP_TRY(hipMemcpyAsync(P->gu, P->guprev, size_t(P->g.N) * sizeof(double), hipMemcpyDeviceToDevice,
                                P->stream));
         std::swap(P->gu, P->guprev);
     }
-    if (fused && spectral && nbuf == 2 && !P->zpicked) MVTV_TRY(pick_zpair(P, mode));
+    if (fused && spectral && nbuf == 2 && !P->zpicked) MVTV_TRY(pick_zpair(P, track_theta));
     double dtheta = 0.0;
     if (track_theta) {
         if (!P->thold) MVTV_TRY(alloc(&P->thold, P->g.N));
@@ -1530,6 +1544,62 @@ mvtv_status mvtv_lambda_max(mvtv_problem* P, double* out, int32_t* iters) {
     HIP_TRY(hipMemcpyAsync(P->host_red, P->red, sizeof(double), hipMemcpyDeviceToHost, P->stream));
     HIP_TRY(hipStreamSynchronize(P->stream));
     *out = 5.0 * P->host_red[0];
+    if (iters) *iters = iter;
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_lambda_max_cpp(mvtv_problem* P, double* out, int32_t* iters) {
+    if (!P || !out) return fail(MVTV_BAD_ARG, "null argument");
+    DeviceGuard dg(P->device);
+    const Launch L = P->L();
+    const size_t n = P->g.N, bytes = n * sizeof(double);
+    if (!P->p2) MVTV_TRY(alloc(&P->p2, n));
+    if (!P->thold) MVTV_TRY(alloc(&P->thold, n));
+    double *x = P->thold, *r = P->r, *p = P->p, *ap = P->p2;
+    auto reduce1 = [&](double* res) -> mvtv_status {   // the one partial sum in P->partials
+        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 0, 0, P->red, P->st));
+        HIP_TRY(hipMemcpyAsync(P->host_red, P->red, sizeof(double), hipMemcpyDeviceToHost, P->stream));
+        HIP_TRY(hipStreamSynchronize(P->stream));
+        *res = P->host_red[0];
+        return MVTV_OK;
+    };
+    // cg(ata, Oty) of cpp-code/utils.cpp:354-386: x = mean(b), r = b - A x, p = r, absolute stop
+    // ||r|| < 0.01, at most 500 iterations when N < 400 and 100 otherwise
+    std::vector<double> hb(n);
+    HIP_TRY(hipMemcpyAsync(hb.data(), P->oty, bytes, hipMemcpyDeviceToHost, P->stream));
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    double sum = 0.0;
+    for (double v : hb) sum += v;
+    HIP_TRY(launch_fill(P->stream, x, sum / double(n), n));
+    HIP_TRY(launch_apply_A(P->g, L, 1.0, W_NONE, nullptr, x, ap, nullptr, nullptr));   // A x
+    HIP_TRY(hipMemcpyAsync(r, P->oty, bytes, hipMemcpyDeviceToDevice, P->stream));
+    HIP_TRY(launch_cg_vec(P->g, L, 3, 1.0, nullptr, r, nullptr, ap, nullptr));          // r = b - A x
+    HIP_TRY(hipMemcpyAsync(p, r, bytes, hipMemcpyDeviceToDevice, P->stream));
+    double rsold = 0.0;
+    HIP_TRY(launch_cg_vec(P->g, L, 0, 0.0, r, nullptr, nullptr, nullptr, P->partials));
+    MVTV_TRY(reduce1(&rsold));
+    double rsnew = rsold + 1.0;
+    const int MAXIT = n < 400 ? 500 : 100;
+    int iter = 0;
+    while (std::sqrt(rsnew) >= 0.01) {
+        double pap = 0.0;   // Ap = A p, p.Ap
+        HIP_TRY(launch_apply_A(P->g, L, 1.0, W_NONE, nullptr, p, ap, P->partials, nullptr));
+        MVTV_TRY(reduce1(&pap));
+        const double alpha = rsold / pap;
+        HIP_TRY(launch_cg_vec(P->g, L, 1, alpha, x, r, p, ap, nullptr));                // x += a p, r -= a Ap
+        HIP_TRY(launch_cg_vec(P->g, L, 0, 0.0, r, nullptr, nullptr, nullptr, P->partials));
+        MVTV_TRY(reduce1(&rsnew));
+        iter += 1;
+        if (iter == MAXIT) break;
+        HIP_TRY(launch_cg_vec(P->g, L, 2, rsnew / rsold, p, nullptr, r, nullptr, nullptr));   // p = r + beta p
+        rsold = rsnew;
+    }
+    // lam_max_pinv (:399-404): max |D x|, no factor
+    HIP_TRY(launch_dmaxabs(P->g, P->order, L, x, P->partials));
+    HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 1, 0, P->red, P->st));
+    HIP_TRY(hipMemcpyAsync(P->host_red, P->red, sizeof(double), hipMemcpyDeviceToHost, P->stream));
+    HIP_TRY(hipStreamSynchronize(P->stream));
+    *out = P->host_red[0];
     if (iters) *iters = iter;
     return MVTV_OK;
 }

@@ -343,7 +343,7 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
         return 2 * std::max(1, cus);
     }();
     static const int nz_env = [] {
-        const char* e = getenv("MVTV_CG3D_NZ");
+        const char* e = probe_env("MVTV_CG3D_NZ");
         return e ? atoi(e) : 0;
     }();
     int nz = 1;

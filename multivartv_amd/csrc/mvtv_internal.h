@@ -13,7 +13,22 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 namespace mvtv {
+
+// Experiment knobs (tile shapes, buffer placement probes, alternative kernels) are read from the
+// environment only in a probe build (`make PROBES=1`, -DMVTV_PROBES); the release library always
+// takes the defaults. The run-time options a user may set are MVTV_ZPICK=0 (keep the allocation-order
+// z buffer pair), MVTV_ADMM_SYNC=1 (host-synchronous ADMM loop) and MVTV_PCG=classic (3-kernel PCG).
+inline const char* probe_env(const char* name) {
+#ifdef MVTV_PROBES
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 
 // Unsigned 32-bit division by an invariant divisor (Granlund-Montgomery):
 // q = (umulhi(n, mul) + n) >> shift, evaluated with a 64-bit add so it holds for every n < 2^32.
@@ -185,7 +200,7 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
                        const double* gb, double cb, const PcgState* st, double* partials, int* nblocks_out);
 hipError_t launch_maxabsdiff(const Geom& g, const Launch& L, const double* a, const double* b, double* partials);
 hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n);
-// CG vector steps of lam_max_pinv (op 0 |x|^2 into partials, 1 x += c p & y -= c t, 2 x = p + c x)
+// CG vector steps of lam_max_pinv (op 0 |x|^2 into partials, 1 x += c p & y -= c t, 2 x = p + c x, 3 y -= c t)
 hipError_t launch_cg_vec(const Geom& g, const Launch& L, int op, double coef, double* x, double* y, const double* p,
                          const double* t, double* partials);
 // vector steps of PCG with the spectral preconditioner (mvtv_kernels.hip k_pcgs_vec): op 0 b and

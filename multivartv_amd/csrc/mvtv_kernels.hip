@@ -421,7 +421,7 @@ __global__ void k_fill(double* __restrict__ x, double v, uint64_t n) {
 
 // --------------------------------------------------------------------- lam_max_pinv support
 // CG on (D^T D) with the reference's recurrences (rcpp-code/MultivarTV/src/utils.cpp:306-355):
-// op 0: sum x*x;  op 1: x += alpha p, d -= alpha t;  op 2: p = r + beta p
+// op 0: sum x*x;  op 1: x += alpha p, d -= alpha t;  op 2: p = r + beta p;  op 3: y -= coef t
 __global__ __launch_bounds__(kThreads) void k_cg_vec(int op, uint32_t n, double coef, double* __restrict__ x,
                                                      double* __restrict__ y, const double* __restrict__ p,
                                                      const double* __restrict__ t, double* __restrict__ partials) {
@@ -432,8 +432,10 @@ __global__ __launch_bounds__(kThreads) void k_cg_vec(int op, uint32_t n, double 
         } else if (op == 1) {
             x[i] = fma(coef, p[i], x[i]);
             y[i] = fma(-coef, t[i], y[i]);
-        } else {
+        } else if (op == 2) {
             x[i] = fma(coef, x[i], p[i]);   // x = p (the new r) + beta x
+        } else {
+            y[i] = fma(-coef, t[i], y[i]);
         }
     }
     if (op == 0) block_reduce_store<1, 0>(red, partials);
@@ -697,7 +699,7 @@ hipError_t launch_apply_A(const Geom& g, const Launch& L, double sigma, int wmod
                           const double* x, double* q, double* partials, const PcgState* st) {
     // plain operator application on a whole 3-D mesh: the z-marching kernel (MVTV_APPLY3D=0: generic)
     static const bool a3d = [] {
-        const char* e = std::getenv("MVTV_APPLY3D");
+        const char* e = probe_env("MVTV_APPLY3D");
         return !e || std::atoi(e) != 0;
     }();
     if (a3d && g.p == 3 && !partials && g.ibeg == 0 && g.iend == g.N)

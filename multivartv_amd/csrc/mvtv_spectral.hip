@@ -710,7 +710,7 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
     using S = spec8::Shape<L>;
     if constexpr (wide_tq<L>() > 0) {
         static const bool wide = [] {
-            const char* e = std::getenv("MVTV_DCT_WIDE");
+            const char* e = probe_env("MVTV_DCT_WIDE");
             return !e || std::atoi(e) != 0;
         }();
         if (wide && !d0 && a.tq == S::TQ && uint32_t(wide_tq<L>()) <= a.stride) {
@@ -784,7 +784,7 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     while ((1u << a.L) < m) ++a.L;
     if ((1u << a.L) != m || m > 4096) return hipErrorInvalidValue;
     const bool formb = ga != nullptr;
-    if (a.L >= 3 && !std::getenv("MVTV_DCT_LDS")) {
+    if (a.L >= 3 && !probe_env("MVTV_DCT_LDS")) {
         static constexpr int tq8[13] = {0, 0, 0, 16, 16, 16, 16, 16, 16, 16, 8, 4, 2};
         int tq = tq8[a.L];
         if (d > 0) tq = std::min<int>(tq, int(g.stride[d]));

@@ -171,8 +171,11 @@ vec softthresh(const vec& z, double lam) {
     return out;
 }
 
-void create_cache_objects(const mat& data, const vec& y, const mat& mesh, const vec& m, const vec& deltas,
-                          mbs_cache& cache, int device) {
+namespace {
+// create_cache_objects of either variant: O as nearest-mesh indices, D's weights from `deltas` (empty: all 1,
+// variant A's mbs_one without cache), W = O^T O and O^T y installed on the (re-used when possible) problem
+void build_cache(const mat& data, const vec& y, const mat& mesh, const vec& m, const vec& deltas, mbs_cache& cache,
+                 int device) {
     const auto dims = mesh_dims(m);
     if (dims.empty() || dims.size() > MVTV_MAX_DIMS) throw std::invalid_argument("mesh must have 1..4 dimensions");
     int64_t N = 1;
@@ -180,8 +183,10 @@ void create_cache_objects(const mat& data, const vec& y, const mat& mesh, const 
     if (mesh.n_rows != N) throw std::invalid_argument("mesh rows != prod(m)");
     if (data.n_cols != int64_t(dims.size()) || int64_t(y.size()) != data.n_rows)
         throw std::invalid_argument("data must be n x p and y of length n");
+    if (!deltas.empty() && deltas.size() != dims.size()) throw std::invalid_argument("deltas must have p values");
     const auto axes = tensor_axes(mesh, dims);
-    const bool reuse = cache.prob && cache.ntheta == N;   // the same mesh (CV fold): new data only
+    // the same mesh and D (CV folds): new data only
+    const bool reuse = cache.prob && cache.ntheta == N && cache.deltas == deltas;
     if (!reuse) {
         if (cache.prob) mvtv_problem_destroy(cache.prob);
         cache.prob = nullptr;
@@ -189,16 +194,17 @@ void create_cache_objects(const mat& data, const vec& y, const mat& mesh, const 
         d.p = int32_t(dims.size());
         for (size_t j = 0; j < dims.size(); ++j) {
             d.m[j] = dims[j];
-            d.deltas[j] = deltas[j];
+            d.deltas[j] = deltas.empty() ? 1.0 : deltas[j];
         }
         d.block_order = MVTV_ORDER_CPP;
-        d.weighted = 1;
+        d.weighted = deltas.empty() ? 0 : 1;
         const vec zeros(size_t(N), 0.0);
         d.oty = zeros.data();
         d.device = device;
         check(mvtv_problem_create(&d, &cache.prob));
         cache.ntheta = N;
         cache.rowsD = mvtv_problem_edges(cache.prob);
+        cache.deltas = deltas;
     }
     cache.oidx.assign(size_t(data.n_rows), 0);
     if (!axes.empty()) {
@@ -219,6 +225,13 @@ void create_cache_objects(const mat& data, const vec& y, const mat& mesh, const 
         cache.w[size_t(cache.oidx[i])] += 1.0;
     }
     check(mvtv_problem_set_data(cache.prob, cache.oty.data(), cache.w.data()));
+}
+}  // namespace
+
+void create_cache_objects(const mat& data, const vec& y, const mat& mesh, const vec& m, const vec& deltas,
+                          mbs_cache& cache, int device) {
+    if (deltas.empty()) throw std::invalid_argument("deltas must have p values");
+    build_cache(data, y, mesh, m, deltas, cache, device);
 }
 
 void admm_update(const vec& /*y*/, mbs_cache& inits, vec& theta_init, double lambda, bool verbose, vec& u_init,
@@ -437,6 +450,183 @@ mbs_impl_result mbs_impl(const mat& data, const vec& y, const vec& m, const mat*
     R.residuals.resize(y.size());
     for (size_t i = 0; i < y.size(); ++i) R.residuals[i] = y[i] - R.best.fitted[i];
     return R;
+}
+
+// =============================================================================== variant A (cpp-code)
+vec create_deltas_cpp(const mat& data, const vec& m) { return create_deltas(data, m, 0.01); }
+
+mat create_mesh_cpp(const mat& data, const vec& m) {
+    const auto dims = mesh_dims(m);
+    const int p = int(data.n_cols);
+    int64_t N = 1;
+    for (auto v : dims) N *= v;
+    std::vector<vec> axes(static_cast<size_t>(p));
+    for (int j = 0; j < p; ++j) {
+        double lo = std::numeric_limits<double>::infinity(), hi = -lo;
+        for (int64_t i = 0; i < data.n_rows; ++i) {
+            lo = std::min(lo, data(i, j));
+            hi = std::max(hi, data(i, j));
+        }
+        axes[size_t(j)] = linspace(lo + 0.01, hi + 0.01, dims[size_t(j)]);   // EPS added to both ends (:281)
+        for (double& v : axes[size_t(j)]) v = double(float(v));               // MAT = fmat (solvers.hpp:12)
+    }
+    mat mesh(N, p);
+    for (int64_t i = 0; i < N; ++i) {
+        int64_t r = i;
+        for (int j = 0; j < p; ++j) {
+            mesh(i, j) = axes[size_t(j)][size_t(r % dims[size_t(j)])];
+            r /= dims[size_t(j)];
+        }
+    }
+    return mesh;
+}
+
+void create_cache_objects_cpp(const mat& data, const vec& y, const mat& mesh, const vec& m, const vec& deltas,
+                              mbs_cache& cache, int device) {
+    build_cache(data, y, mesh, m, deltas, cache, device);
+}
+
+vec create_lambdas_cpp(int n_lambda, mbs_cache& inits, const vec* lambdas, double* lambda_max) {
+    if (lambdas) return *lambdas;
+    double lmax = 0.0;
+    int32_t it = 0;
+    check(mvtv_lambda_max_cpp(inits.prob, &lmax, &it));
+    if (lambda_max) *lambda_max = lmax;
+    const vec grid = linspace(std::log(lmax * 0.00001), std::log(lmax), n_lambda);
+    vec out(grid.size());
+    for (size_t i = 0; i < grid.size(); ++i) out[grid.size() - 1 - i] = std::exp(grid[i]);   // flipud
+    return out;
+}
+
+vec admm_update(const vec& y, mbs_cache& inits, const vec* theta_init, double lambda) {
+    mvtv_admm_opts o;
+    mvtv_default_opts(&o, MVTV_VARIANT_CPP);
+    o.ymean = mean(y);
+    o.sigma = inits.sp_sigma;
+    vec theta = theta_init ? *theta_init : vec(size_t(inits.ntheta), o.ymean);
+    double rho = lambda;
+    mvtv_admm_stats st;
+    const int s = mvtv_admm(inits.prob, &o, lambda, theta.data(), nullptr, &rho, &st);
+    if (s == MVTV_MAXITER) throw std::invalid_argument("Failed to converge!");
+    check(s);
+    return theta;
+}
+
+namespace {
+// fill_output_mbs_one (cpp-code/solvers.cpp:64-68): fitted = O theta with the O the solve used
+void fill_output_cpp(mbs_one_object& out, const mat& data, const vec& y, const mat& mesh, const vec& theta,
+                     const mbs_cache& inits, const vec& m) {
+    out.mesh = mesh;
+    out.theta_hat = theta;
+    out.fitted.resize(inits.oidx.size());
+    for (size_t i = 0; i < inits.oidx.size(); ++i) out.fitted[i] = theta[size_t(inits.oidx[i])];
+    out.data = data;
+    out.y = y;
+    out.m = m;
+}
+}  // namespace
+
+void mbs_one(const mat& data, const vec& y, const vec& m, mbs_one_object& output, const mat& mesh,
+             const vec* theta_init, double lambda, mbs_cache* cache, int device) {
+    if (!cache) {   // :141-145: create_cache_objects with inits.deltas never set -> unit weights
+        mbs_cache local;
+        create_cache_objects_cpp(data, y, mesh, m, vec{}, local, device);
+        local.sp_sigma = lambda;
+        const vec theta = admm_update(y, local, theta_init, lambda);
+        fill_output_cpp(output, data, y, mesh, theta, local, m);
+        return;
+    }
+    const vec theta = admm_update(y, *cache, theta_init, lambda);
+    fill_output_cpp(output, data, y, mesh, theta, *cache, m);
+}
+
+std::vector<int64_t> kfold_perm(int64_t n, uint64_t seed) {
+    std::vector<uint64_t> key(size_t(std::max<int64_t>(n, 0)));
+    for (int64_t i = 0; i < n; ++i) {
+        uint64_t z = seed * 0xD1B54A32D192ED03ull + uint64_t(i) + 0x9E3779B97F4A7C15ull;   // splitmix64
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        key[size_t(i)] = z ^ (z >> 31);
+    }
+    std::vector<int64_t> perm(key.size());
+    for (size_t i = 0; i < perm.size(); ++i) perm[i] = int64_t(i);
+    std::stable_sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return key[size_t(a)] < key[size_t(b)]; });
+    return perm;
+}
+
+void mbs(const mat& data, const vec& y, const vec& m, mbs_one_object& output, const mat* mesh, int n_lambda,
+         const vec* ftrue, const vec* lambdas, int folds, const mbs_cpp_options& opts, mbs_cpp_report* report) {
+    if (folds < 1) throw std::invalid_argument("folds must be >= 1");
+    const vec deltas = create_deltas_cpp(data, m);                  // :281
+    const mat MESH = mesh ? *mesh : create_mesh_cpp(data, m);       // :282
+    mbs_cache cache;                                                // :286-289, full data
+    create_cache_objects_cpp(data, y, MESH, m, deltas, cache, opts.device);
+    double lmax = 0.0;
+    const vec LAMBDAS = create_lambdas_cpp(n_lambda, cache, lambdas, &lmax);   // :292
+    const int nl = int(LAMBDAS.size());
+    (void)ftrue;   // FTRUE (:293) only feeds the path models' own MSEs, which mbs never reads
+    // kfold (cpp-code/utils.cpp:417-436) over the permuted rows
+    const int64_t n = data.n_rows, ntest = n / folds, p = data.n_cols;
+    const auto perm = kfold_perm(n, opts.seed);
+    mat mse_mat(nl, folds);
+    std::vector<vec> path0;   // fold 0's path models (what test_mse and the refit read in reference mode)
+    for (int f = 0; f < folds; ++f) {
+        const int64_t first = int64_t(f) * ntest, last = first + ntest;   // test rows [first, last)
+        mat trx(n - ntest, p), tex(ntest, p);
+        vec tr_y, te_y;
+        for (int64_t r = 0, a = 0, b = 0; r < n; ++r) {
+            const int64_t i = perm[size_t(r)];
+            const bool test = r >= first && r < last;
+            for (int64_t j = 0; j < p; ++j) (test ? tex(b, j) : trx(a, j)) = data(i, j);
+            (test ? te_y : tr_y).push_back(y[size_t(i)]);
+            test ? ++b : ++a;
+        }
+        // mbs_path (:196-217): warm-started theta, rho = lambda, matrix crossO + lambda crossD
+        mbs_cache fold_cache;
+        mbs_cache& pc = opts.reference_cv ? cache : fold_cache;
+        if (!opts.reference_cv) create_cache_objects_cpp(trx, tr_y, MESH, m, deltas, fold_cache, opts.device);
+        vec theta(size_t(cache.ntheta), mean(tr_y));
+        std::vector<vec> models;
+        for (int i = 0; i < nl; ++i) {
+            pc.sp_sigma = LAMBDAS[size_t(i)];
+            theta = admm_update(tr_y, pc, &theta, LAMBDAS[size_t(i)]);
+            models.push_back(theta);
+        }
+        if (f == 0) path0 = models;
+        // test_mse (:264-273): reference mode reads the first n_lambda models of the accumulated path = fold 0's
+        const std::vector<vec>& use = opts.reference_cv ? path0 : models;
+        const auto idx = nearest_index(tex, MESH);
+        for (int i = 0; i < nl; ++i) {
+            vec fits(idx.size());
+            for (size_t k = 0; k < idx.size(); ++k) fits[k] = use[size_t(i)][size_t(idx[k])];
+            mse_mat(i, f) = mse(fits, te_y);
+        }
+        if (opts.reference_cv) cache.sp_sigma = LAMBDAS[size_t(nl - 1)];   // what the last path leaves (:209)
+    }
+    // mbs_fit_optimal (:248-260): rowmean, first minimum
+    int64_t best = 0;
+    double bestv = std::numeric_limits<double>::infinity();
+    for (int i = 0; i < nl; ++i) {
+        double s = 0.0;
+        for (int f = 0; f < folds; ++f) s += mse_mat(i, f);
+        s /= double(folds);
+        if (s < bestv) {
+            bestv = s;
+            best = i;
+        }
+    }
+    if (opts.reference_cv) {
+        mbs_one(data, y, m, output, MESH, &path0[size_t(best)], LAMBDAS[size_t(best)], &cache);
+    } else {
+        cache.sp_sigma = LAMBDAS[size_t(best)];
+        mbs_one(data, y, m, output, MESH, nullptr, LAMBDAS[size_t(best)], &cache);
+    }
+    if (report) {
+        report->lambdas = LAMBDAS;
+        report->lambda_max = lmax;
+        report->mse_mat = mse_mat;
+        report->best = best;
+    }
 }
 
 }  // namespace mvtv

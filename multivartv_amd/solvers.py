@@ -10,13 +10,10 @@ is no CPU fallback.
 matrices (code/solvers.py:42-51). Here it is an :class:`MbsCache` (GPU-resident
 problem + nearest-mesh index), built by :func:`make_cache` or by ``mbs``.
 
-lambda_max: the reference computes it with SuperLU on the singular matrix D^T D
-(code/utils.py:198-209), whose result depends on SuperLU's pivoting on a zero
-pivot (e.g. 320.0 against the pseudo-inverse value 53.57 on the fixture
-tests/golden/py_2d_mbs_one_nocache.npz). No other solver reproduces that value;
-:func:`lam_max` returns the pseudo-inverse value ||D (D^T D)^+ O^T y||_inf computed
-on the GPU, and callers that need the reference's exact grid pass ``tune`` /
-``tuners`` explicitly.
+lambda_max: the reference computes it on the host with SuperLU on the singular matrix
+D^T D (code/utils.py:198-209); :func:`lam_max` builds the same sparse D (utils.create_D) and
+calls the same library (scipy's SuperLU), so the no-cache ``mbs_one`` and ``mbs`` without
+``tuners`` use the reference's own tuning values (setup, not the hot path).
 """
 from __future__ import annotations
 
@@ -25,7 +22,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from .utils import interp_weights, mesh_coords, nearest_index
+from .utils import create_D, interp_weights, lam_max_pinv, mesh_coords, nearest_index
 
 
 def softthresh(z, lam):
@@ -68,22 +65,11 @@ def make_cache(data, y, m, mesh=None, deltas=None, sigma=1.0, weighted=None, dev
     return MbsCache(P, idx, np.asarray(mesh), N, float(sigma))
 
 
-def lam_max(cache: MbsCache, rtol=1e-12):
-    """||D (D^T D)^+ O^T y||_inf on the GPU (see module docstring).
-
-    D^T D is singular with the constants as its null space (every single-dimension difference
-    block is in D), so the mean-free right-hand side is consistent and PCG from 0 converges to
-    the minimum-norm solution. The solve runs on an auxiliary problem with W = 0.
-    """
-    P = cache.problem
-    b = P._oty - P._oty.mean()
-    aux = _lib.Problem(P.m, b, wdiag=np.zeros(P.N), deltas=P.deltas, order=P.order, weighted=P.weighted,
-                       device=P.device)
-    try:
-        x, _, _ = aux.solve(1.0, b, rtol=rtol)
-        return float(np.max(np.abs(aux.apply_D(x))))
-    finally:
-        aux.close()
+def lam_max(cache: MbsCache, deltas=None):
+    """code/utils.py:206-209 (lam_max_pinv) for the cache's mesh and data: max |D splu(D^T D).solve(O^T y)|
+    with D = create_D(m, deltas) built on the host exactly as the reference builds it."""
+    m = cache.problem.m
+    return lam_max_pinv(create_D(m, deltas), cache.problem._oty)
 
 
 def mbs_one(data, y, m, theta_init=None, mesh=None, tune=1.0, eps=0.01, tol=0.001, cache=None):
@@ -93,8 +79,13 @@ def mbs_one(data, y, m, theta_init=None, mesh=None, tune=1.0, eps=0.01, tol=0.00
         if mesh is not None:
             # the reference leaves `deltas` unbound on this path (code/solvers.py:24-31)
             raise NameError("name 'deltas' is not defined")
+        data = np.asarray(data, dtype=np.float64)
+        data = data.reshape(-1, 1) if data.ndim == 1 else data
+        deltas = mesh_coords(data, m)["deltas"]
+        if len(np.atleast_1d(m)) == 1:
+            raise ValueError("blocks must be 2-D")   # create_D(m, deltas) at p = 1 (code/utils.py:145-148)
         cache = make_cache(data, y, m, sigma=tune)
-        tune = lam_max(cache)
+        tune = lam_max(cache, deltas)
         cache.sigma = tune
     ntheta = cache.ntheta
     ym = float(np.mean(y))
@@ -135,7 +126,7 @@ def mbs(data, y, m, ftrue=None, mesh=None, ntune=100, tuners=None, eps=0.01):
     mesh_, deltas = mo["mesh"], mo["deltas"]
     cache = make_cache(data, y, m, mesh=mesh_ if mesh is None else mesh, deltas=deltas)
     if tuners is None:
-        lmax = lam_max(cache) * float(np.prod(deltas))
+        lmax = lam_max(cache, deltas) * float(np.prod(deltas))
         tuners = np.exp(np.linspace(np.log(lmax * 1e-4), np.log(lmax), ntune))[::-1]
         rho = lmax
     else:

@@ -56,6 +56,24 @@ def test_mbs_path_with_reference_tuners():
     np.testing.assert_allclose(out["minmse.fits"]["theta.hat"].ravel(), g["theta"], rtol=1e-8, atol=1e-10)
 
 
+def test_mbs_one_nocache_reference_lambda_max():
+    """code/solvers.py:23-40 without a cache: tune := lam_max_pinv (SuperLU on the singular D^T D),
+    reproduced by utils.lam_max_pinv; theta against the reference's own output."""
+    meta, g = load_golden("py_2d_mbs_one_nocache")
+    out = solvers.mbs_one(g["data"], g["y"], np.array(meta["m"]))
+    np.testing.assert_allclose(out["theta.hat"].ravel(), g["theta"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(out["fitted"].ravel(), g["fitted"], rtol=1e-9, atol=1e-12)
+
+
+def test_mbs_path_auto_grid():
+    """code/solvers.py:mbs with ntune only: the lambda grid from lam_max_pinv * prod(deltas) (:115-117)."""
+    meta, g = load_golden("py_2d_mbs_path")
+    out = solvers.mbs(g["data"], g["y"], np.array(meta["m"]), ftrue=g["ftrue"], ntune=meta["ntune"])
+    assert out["minmse.lam"] == pytest.approx(float(g["minlam"]), rel=1e-12)
+    assert out["minmse"] == pytest.approx(float(g["minmse"]), rel=1e-8)
+    np.testing.assert_allclose(out["minmse.fits"]["theta.hat"].ravel(), g["theta"], rtol=1e-8, atol=1e-10)
+
+
 def test_cpp_host_api(tmp_path):
     """include/mvtv/solvers.hpp: create_cache_objects + mbs_path (warm start) on a 2D scattered fit."""
     exe = tmp_path / "cpp_api"

@@ -74,3 +74,26 @@ def test_slab_desc_layout_matches_header():
     from multivartv_amd import slab
     assert ctypes.sizeof(slab.SlabDesc) == 32          # int64 x3 + int32 x2 (include/mvtv/mvtv.h)
     assert [f[0] for f in slab.SlabDesc._fields_] == ["m_global", "z_begin", "z_end", "ghost_lo", "ghost_hi"]
+
+
+def test_create_D_and_lam_max_pinv_match_reference_fixtures():
+    """utils.create_D is the Python reference's D (bit-identical to the oracle's, itself pinned to
+    the reference) and utils.lam_max_pinv gives the reference's SuperLU value on the no-cache
+    fixture (320.0, tests/golden/py_2d_mbs_one_nocache.npz)."""
+    from multivartv_amd import utils as U
+    from oracle import mvtv_oracle as O
+    for m in ([8, 8], [3, 3, 3, 3], [4, 4, 4], [7]):
+        for dl in (None, [0.1, 0.2, 0.3, 0.4][:len(m)]):
+            if len(m) == 1 and dl is not None:
+                with pytest.raises(ValueError):
+                    U.create_D(m, dl)
+                continue
+            D1, D2 = U.create_D(m, dl), O.build_D(m, O.block_table(len(m), dl, "py"))
+            assert D1.shape == D2.shape and (D1 != D2).nnz == 0
+    with pytest.raises(ValueError):
+        U.create_D([4, 5, 3])
+    meta, g = load_golden("py_2d_mbs_one_nocache")
+    mesh, deltas = U.mesh_coords(g["data"], meta["m"])["mesh"], U.mesh_coords(g["data"], meta["m"])["deltas"]
+    idx = U.nearest_index(g["data"], mesh)
+    _, oty = U.interp_weights(idx, 64, g["y"])
+    assert U.lam_max_pinv(U.create_D(meta["m"], deltas), oty) == 320.0
