@@ -12,7 +12,9 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmvtv.so")
+# MVTV_LIB_PATH: load another build of the same library (e.g. a probe build, `make PROBES=1 OUT=...`)
+LIB_PATH = os.environ.get("MVTV_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                           "libmvtv.so")
 
 MVTV_OK, MVTV_MAXITER, MVTV_BAD_ARG, MVTV_DIM_MISMATCH = 0, 1, 2, 3
 MVTV_HIP_ERROR, MVTV_NO_DEVICE, MVTV_OUT_OF_MEMORY, MVTV_PCG_NOT_CONVERGED = 4, 5, 6, 7

@@ -375,22 +375,12 @@ hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, c
 }
 
 // =============================================================================================
-// k_admm3d: edge update and D^T gather in ONE pass (the z state is read once and written once).
-//
-// The gather at (x,y,e) needs z_new at the in-plane backward neighbours (x-1, y), (x, y-1),
-// (x-1, y-1) of plane e, which other threads produce in the same step, so a workgroup stages
-// z_new of one plane in LDS. Its image is 64 x 16 cells with lane 0 on x = X0-1 and row 0 on
-// y = Y0-1: those halo cells recompute the neighbour tile's z_new (never stored) so the gather
-// of the 63 x 15 interior is complete. z_new goes to a second edge buffer (ping-pong), so a
-// halo or a chunk-start recompute always reads the previous iterate, never a value another
-// workgroup has already overwritten. The dim-2 backward corners come from the carried
-// in-plane sums of the previous plane (as in k_gather3d), so no plane is ever re-read.
-namespace f3d {
-constexpr int IW = 64, TX = IW - 1;
-constexpr int SW = 16;   // strip image width: the last m0 % 63 (1..15) columns of dim 0
-int rows();   // image rows per workgroup (16, or 8 with MVTV_F3D_IH=8)
-}
-
+// Fused 3-D pass (k_admm3a below): edge update and D^T gather in ONE pass over the edge state (z read
+// once, written once to the ping-pong partner buffer). The gather at (x,y,e) needs z_new at the
+// in-plane backward neighbours (x-1, y), (x, y-1), (x-1, y-1) of plane e, which other threads produce
+// in the same step, so a workgroup stages z_new of one plane in LDS; halo cells recompute the
+// neighbouring tiles' z_new from the previous iterate (never stored), and the dim-2 backward corners
+// come from in-plane sums carried from the previous plane, so no plane is ever re-read.
 struct Fused3dArgs {
     Geom g;
     const double* theta;
@@ -404,203 +394,232 @@ struct Fused3dArgs {
     double t_old, c_old, t_new, c_prev;
     const AdmmCtl* ctl;
     int tiles_x, tiles_y, zchunk, nblocks, zlo, zhi;
-    int strip, tpz;   // k_admm3d: ragged-edge strip tiles on / tiles per z chunk
-    int xcd;          // k_admm3d: contiguous tile runs per XCD (MVTV_F3D_XCD=0: blockIdx order)
+    int tpz;          // tiles per z chunk
+    int xcd;          // contiguous tile runs per XCD (MVTV_F3D_XCD=0 in a probe build: blockIdx order)
 };
 
-// partials: |r|^2, |D theta|^2, |alpha|^2, max dtheta, |g_u|^2, |s_B|^2, |s_A|^2 (max slot 3)
-// (IH = 10 at 5 waves per SIMD was tried: 96 VGPRs only with 96 B/lane of spills, 2.1x slower)
-template <int ORD, int UM, bool DTH, int NB, int IW, int IH>
-__device__ __forceinline__ void admm3d_tile(const Fused3dArgs& a, double* __restrict__ szr, double (&red)[7], int xh,
-                                            int yh, int rows_used, int z0, int z1, double t_old, double c_old,
-                                            double t_new, double c_prev) {
-    constexpr int P = 3, NC = 8;
-    const Geom& g = a.g;
-    {
-        const int lane = int(threadIdx.x) % IW, row = int(threadIdx.x) / IW;
-        const int x = xh + lane, y = yh + row;
-        const int m0 = int(g.m[0]), m1 = int(g.m[1]), m2 = int(g.m[2]);
-        const bool cell = row < rows_used && x >= 0 && y >= 0 && x < m0 && y < m1;     // computes z_new here
-        const bool inner = cell && lane > 0 && row > 0;              // owns outputs here
-        const uint32_t pl = uint32_t(m0) * uint32_t(m1);
-        const int xc = min(max(x, 0), m0 - 1), yc = min(max(y, 0), m1 - 1);
-        const uint32_t xo[2] = {uint32_t(xc), uint32_t(min(xc + 1, m0 - 1))};
-        const uint32_t yo[2] = {uint32_t(yc) * uint32_t(m0), uint32_t(min(yc + 1, m1 - 1)) * uint32_t(m0)};
-        const uint32_t ixy = yo[0] + xo[0];
-        const bool okx = x > 0, oky = y > 0;
+// ---------------------------------------------------------------------------------------------
+// k_admm3a: tiles aligned to the 64-node chunks of the edge layout (Geom.eaos) and of every N-vector
+// row: a tile owns x in [64 t, 64 t + 63], so each wave's z_new, g_alpha and g_u stores are whole
+// 512-B runs (four full 128-B lines). (The round-1 kernel owned 63 columns with lane 0 as the x - 1
+// halo: its 63-word stores straddled two chunks, 10.3 GB written per launch at 512^3 against 9.66
+// here, 3.90 -> 3.49 ms on one box, profiles/r02/v3_*.) The x - 1 column the gather of lane 0 needs is computed by a 16th wave (lanes
+// 0..14 = image rows) that recomputes z_new at x = 64 t - 1 (never stored); waves 0..14 hold image
+// rows 0..14, row 0 being the y - 1 halo (recomputed, never stored) and rows 1..14 the owned rows.
+// The LDS image is 65 columns wide (column 0 = the halo column) and holds only the blocks whose
+// difference set has dim 0 or dim 1 (the block with S' = {2} is read by its own cell only, from a
+// register).
+namespace f3a {
+constexpr int IW = 65, IH = 15, TY = IH - 1, NT = 1024;
+}
 
-        // loads of one step: theta at plane e+1, z_old and g_uprev at plane e (issued a step ahead)
-        auto load_theta = [&](double (&th)[4], int e) {
-            const uint32_t zo = uint32_t(e) * pl;
+template <int NB, int ORD>
+__host__ __device__ constexpr int f3a_nimg() {
+    int n = 0;
+    for (int k = 0; k < NB; ++k)
+        if ((sprime_mask(block_code(k, 3, ORD), 3) & 3) != 0) ++n;
+    return n;
+}
+template <int NB, int ORD>
+__host__ __device__ constexpr int f3a_slot(int k) {   // image slot of block k (-1: not in the image)
+    int n = 0;
+    for (int j = 0; j < k; ++j)
+        if ((sprime_mask(block_code(j, 3, ORD), 3) & 3) != 0) ++n;
+    return (sprime_mask(block_code(k, 3, ORD), 3) & 3) != 0 ? n : -1;
+}
+
+template <int ORD, int UM, bool DTH, int NB>
+__device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __restrict__ szr, double (&red)[7], int X0,
+                                            int Yh, int z0, int z1, double t_old, double c_old, double t_new,
+                                            double c_prev) {
+    constexpr int P = 3, NC = 8, IW = f3a::IW, IH = f3a::IH, NI = f3a_nimg<NB, ORD>();
+    const Geom& g = a.g;
+    const int wv = int(threadIdx.x) >> 6, ln = int(threadIdx.x) & 63;
+    const bool hcol = wv == IH;                 // the halo-column wave
+    const int row = hcol ? ln : wv;
+    const int col = hcol ? 0 : ln + 1;
+    const int x = hcol ? X0 - 1 : X0 + ln, y = Yh + row;
+    const int m0 = int(g.m[0]), m1 = int(g.m[1]), m2 = int(g.m[2]);
+    const bool active = row < IH;               // holds an image cell
+    const bool cell = active && x >= 0 && y >= 0 && x < m0 && y < m1;   // computes z_new here
+    const bool inner = cell && !hcol && row > 0;                       // owns outputs here
+    const uint32_t pl = uint32_t(m0) * uint32_t(m1);
+    const int xc = min(max(x, 0), m0 - 1), yc = min(max(y, 0), m1 - 1);
+    const uint32_t xo[2] = {uint32_t(xc), uint32_t(min(xc + 1, m0 - 1))};
+    const uint32_t yo[2] = {uint32_t(yc) * uint32_t(m0), uint32_t(min(yc + 1, m1 - 1)) * uint32_t(m0)};
+    const uint32_t ixy = yo[0] + xo[0];
+    const bool okx = x > 0, oky = y > 0;
+    const bool hrow = row == 0;
+    auto sidx = [&](int buf, int slot, int r, int c) { return ((buf * NI + slot) * IH + r) * IW + c; };
+
+    auto load_theta = [&](double (&th)[4], int e) {
+        const uint32_t zo = uint32_t(e) * pl;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) th[q] = cell ? a.theta[zo + yo[q >> 1] + xo[q & 1]] : 0.0;
-        };
-        // A halo cell's z_new is read only through the neighbour offsets of the blocks whose
-        // difference set contains that offset: row 0 serves (x, y-1) and (x-1, y-1) (S has dim 1),
-        // lane 0 serves (x-1, y) and (x-1, y-1) (S has dim 0), the corner only (x-1, y-1). Other
-        // blocks of halo cells are never loaded.
-        const bool hrow = row == 0, hlane = lane == 0;
-        // (cached loads: the halo cells of the neighbouring tiles read the same lines. Loading the
-        // words no halo re-reads nontemporal did not lower FETCH_SIZE and cost 2-8 %.)
-        auto load_z = [&](double (&zo)[NB], int e) {
-            const uint32_t i = uint32_t(e) * pl + ixy;
-            static_for<0, NB>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                const bool need = cell && (!hrow || (S & 2)) && (!hlane || (S & 1));
-                const double* src = a.z_old + eix(g, k, i);
-                zo[k] = need ? *src : 0.0;
-            });
-        };
-        // z_new of this cell at plane e from theta planes e (th0), e+1 (th1) and the old z
-        auto edge_cell = [&](int e, const double (&th0)[4], const double (&th1)[4], const double (&zo)[NB],
-                             double (&zn)[NB], bool own) {
-            const uint32_t i = uint32_t(e) * pl + ixy;
-            double v[NC];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                v[q] = th0[q];
-                v[q | 4] = th1[q];
-            }
-            if constexpr (DTH)
-                if (own) red[3] = fmax(red[3], fabs(v[0] - a.theta_old[i]));
-#pragma unroll
-            for (int j = 0; j < P; ++j)
-#pragma unroll
-                for (int q = 0; q < NC; ++q)
-                    if (!((q >> j) & 1)) v[q | (1 << j)] = v[q] - v[q | (1 << j)];
-            static_for<0, NB>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                const double d = g.w[k] * v[S];
-                const double uo = (UM == U_EXPLICIT) ? zo[k] : -c_old * clampd(zo[k], t_old);
-                const double z = cell ? d - uo : 0.0;
-                zn[k] = z;
-                if (own) {
-                    const double al = z - clampd(z, t_new);
-                    const double r = al - d;
-                    __builtin_nontemporal_store(z, a.z_new + eix(g, k, i));
-                    red[0] = fma(r, r, red[0]);
-                    red[1] = fma(d, d, red[1]);
-                    red[2] = fma(al, al, red[2]);
-                }
-            });
-        };
-        // in-plane backward sums Q_k of this (interior) cell from the LDS image of plane e
-        auto plane_q = [&](auto kc, int buf, double& qa, double& qu) {
+        for (int q = 0; q < 4; ++q) th[q] = cell ? a.theta[zo + yo[q >> 1] + xo[q & 1]] : 0.0;
+    };
+    // halo cells load only the blocks their neighbours read: row 0 those with dim 1 in S', the halo
+    // column those with dim 0, the corner both
+    auto load_z = [&](double (&zo)[NB], int e) {
+        const uint32_t i = uint32_t(e) * pl + ixy;
+        static_for<0, NB>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-            constexpr int SI = S & 3;
-            qa = 0.0;
-            qu = 0.0;
+            const bool need = cell && (!hrow || (S & 2)) && (!hcol || (S & 1));
+            zo[k] = need ? a.z_old[eix(g, k, i)] : 0.0;
+        });
+    };
+    auto edge_cell = [&](int e, const double (&th0)[4], const double (&th1)[4], const double (&zo)[NB],
+                         double (&zn)[NB], bool own) {
+        const uint32_t i = uint32_t(e) * pl + ixy;
+        double v[NC];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if ((q & ~SI) != 0) continue;
-                const bool ok = (!(q & 1) || okx) && (!(q & 2) || oky);
-                const double v = ok ? szr[((buf * NB + k) * IH + row - ((q >> 1) & 1)) * IW + lane - (q & 1)] : 0.0;
-                const bool neg = __builtin_popcount(q) & 1;
-                const double cl = clampd(v, t_new);
-                const double al = v - cl;
-                qa = neg ? qa - al : qa + al;
-                qu = neg ? qu + cl : qu - cl;   // u = -clamp
-            }
-        };
-        // the dim-2 difference is carried as two weighted sums (alpha, u) over the blocks with dim 2
-        // in S', not per block
-        double qa_prev = 0.0, qu_prev = 0.0;
-
-        double th0[4], th1[4], zo[NB], zn[NB];
-        if (z0 > 0) {   // carried sums of plane z0 - 1: recompute its z_new from the old state
-            load_theta(th0, z0 - 1);
-            load_theta(th1, z0);
-            load_z(zo, z0 - 1);
-            edge_cell(z0 - 1, th0, th1, zo, zn, false);
-#pragma unroll
-            for (int k = 0; k < NB; ++k) szr[((NB + k) * IH + row) * IW + lane] = zn[k];
-            lds_barrier();
-            if (inner) {
-                static_for<0, NB>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                    if constexpr ((S & 4) != 0) {
-                        double qa, qu;
-                        plane_q(kc, 1, qa, qu);
-                        qa_prev = fma(g.w[k], qa, qa_prev);
-                        qu_prev = fma(g.w[k], qu, qu_prev);
-                    }
-                });
-            }
-            lds_barrier();
+        for (int q = 0; q < 4; ++q) {
+            v[q] = th0[q];
+            v[q | 4] = th1[q];
         }
-        load_theta(th0, z0);
-        load_theta(th1, min(z0 + 1, m2 - 1));
-        load_z(zo, z0);
-        double gp = inner ? __builtin_nontemporal_load(a.g_uprev + uint32_t(z0) * pl + ixy) : 0.0;
-        for (int e = z0; e < z1; ++e) {
-            const int buf = (e - z0) & 1;
-            edge_cell(e, th0, th1, zo, zn, inner);
+        if constexpr (DTH)
+            if (own) red[3] = fmax(red[3], fabs(v[0] - a.theta_old[i]));
 #pragma unroll
-            for (int k = 0; k < NB; ++k) szr[((buf * NB + k) * IH + row) * IW + lane] = zn[k];
-            // prefetch step e+1 while this step's gather runs
-            double nth[4], nzo[NB], ngp = 0.0;
-            if (e + 1 < z1) {
-                load_theta(nth, min(e + 2, m2 - 1));
-                load_z(nzo, e + 1);
-                ngp = inner ? __builtin_nontemporal_load(a.g_uprev + uint32_t(e + 1) * pl + ixy) : 0.0;
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int q = 0; q < NC; ++q)
+                if (!((q >> j) & 1)) v[q | (1 << j)] = v[q] - v[q | (1 << j)];
+        static_for<0, NB>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+            const double d = g.w[k] * v[S];
+            const double uo = (UM == U_EXPLICIT) ? zo[k] : -c_old * clampd(zo[k], t_old);
+            const double z = cell ? d - uo : 0.0;
+            zn[k] = z;
+            if (own) {
+                const double al = z - clampd(z, t_new);
+                const double r = al - d;
+                __builtin_nontemporal_store(z, a.z_new + eix(g, k, i));
+                red[0] = fma(r, r, red[0]);
+                red[1] = fma(d, d, red[1]);
+                red[2] = fma(al, al, red[2]);
+            }
+        });
+    };
+    auto to_image = [&](int buf, const double (&zn)[NB]) {
+        if (!active) return;
+        static_for<0, NB>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int sl = f3a_slot<NB, ORD>(k);
+            if constexpr (sl >= 0) szr[sidx(buf, sl, row, col)] = zn[k];
+        });
+    };
+    // in-plane backward sums Q_k of an owned cell: its own value from the register, the neighbours
+    // (x-1, y), (x, y-1), (x-1, y-1) from the image
+    auto plane_q = [&](auto kc, int buf, double own_z, double& qa, double& qu) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+        constexpr int SI = S & 3;
+        constexpr int sl = f3a_slot<NB, ORD>(k);
+        qa = 0.0;
+        qu = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if ((q & ~SI) != 0) continue;
+            double v;
+            if (q == 0) {
+                v = own_z;
             } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) nth[q] = 0.0;
-#pragma unroll
-                for (int k = 0; k < NB; ++k) nzo[k] = 0.0;
+                const bool ok = (!(q & 1) || okx) && (!(q & 2) || oky);
+                if constexpr (sl >= 0) v = ok ? szr[sidx(buf, sl, row - ((q >> 1) & 1), col - (q & 1))] : 0.0;
+                else v = 0.0;
             }
-            lds_barrier();
-            if (inner) {
-                double ga = 0.0, gu = 0.0, na = 0.0, nu = 0.0;
-                static_for<0, NB>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                    double qa, qu;
-                    plane_q(kc, buf, qa, qu);
-                    ga = fma(g.w[k], qa, ga);
-                    gu = fma(g.w[k], qu, gu);
-                    if constexpr ((S & 4) != 0) {
-                        na = fma(g.w[k], qa, na);
-                        nu = fma(g.w[k], qu, nu);
-                    }
-                });
-                ga -= qa_prev;
-                gu -= qu_prev;
-                qa_prev = na;
-                qu_prev = nu;
-                const uint32_t i = uint32_t(e) * pl + ixy;
-                __builtin_nontemporal_store(ga, a.g_alpha + i);
-                __builtin_nontemporal_store(gu, a.g_u + i);
-                const double gpc = c_prev * gp;
-                const double db = gu - gpc, da = ga + gpc;
-                red[4] = fma(gu, gu, red[4]);
-                red[5] = fma(db, db, red[5]);
-                red[6] = fma(da, da, red[6]);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                th0[q] = th1[q];
-                th1[q] = nth[q];
-            }
-#pragma unroll
-            for (int k = 0; k < NB; ++k) zo[k] = nzo[k];
-            gp = ngp;
-            // the buffer written next step is the other one; the one after waits for this barrier
+            const bool neg = __builtin_popcount(q) & 1;
+            const double cl = clampd(v, t_new);
+            const double al = v - cl;
+            qa = neg ? qa - al : qa + al;
+            qu = neg ? qu + cl : qu - cl;   // u = -clamp
         }
+    };
+    double qa_prev = 0.0, qu_prev = 0.0;
+    double th0[4], th1[4], zo[NB], zn[NB];
+    if (z0 > 0) {   // carried sums of plane z0 - 1: recompute its z_new from the old state
+        load_theta(th0, z0 - 1);
+        load_theta(th1, z0);
+        load_z(zo, z0 - 1);
+        edge_cell(z0 - 1, th0, th1, zo, zn, false);
+        to_image(1, zn);
+        lds_barrier();
+        if (inner) {
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                if constexpr ((S & 4) != 0) {
+                    double qa, qu;
+                    plane_q(kc, 1, zn[k], qa, qu);
+                    qa_prev = fma(g.w[k], qa, qa_prev);
+                    qu_prev = fma(g.w[k], qu, qu_prev);
+                }
+            });
+        }
+        lds_barrier();
+    }
+    load_theta(th0, z0);
+    load_theta(th1, min(z0 + 1, m2 - 1));
+    load_z(zo, z0);
+    double gp = inner ? __builtin_nontemporal_load(a.g_uprev + uint32_t(z0) * pl + ixy) : 0.0;
+    for (int e = z0; e < z1; ++e) {
+        const int buf = (e - z0) & 1;
+        edge_cell(e, th0, th1, zo, zn, inner);
+        to_image(buf, zn);
+        double nth[4], nzo[NB], ngp = 0.0;   // prefetch step e+1 while this step's gather runs
+        if (e + 1 < z1) {
+            load_theta(nth, min(e + 2, m2 - 1));
+            load_z(nzo, e + 1);
+            ngp = inner ? __builtin_nontemporal_load(a.g_uprev + uint32_t(e + 1) * pl + ixy) : 0.0;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) nth[q] = 0.0;
+#pragma unroll
+            for (int k = 0; k < NB; ++k) nzo[k] = 0.0;
+        }
+        lds_barrier();
+        if (inner) {
+            double ga = 0.0, gu = 0.0, na = 0.0, nu = 0.0;
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                double qa, qu;
+                plane_q(kc, buf, zn[k], qa, qu);
+                ga = fma(g.w[k], qa, ga);
+                gu = fma(g.w[k], qu, gu);
+                if constexpr ((S & 4) != 0) {
+                    na = fma(g.w[k], qa, na);
+                    nu = fma(g.w[k], qu, nu);
+                }
+            });
+            ga -= qa_prev;
+            gu -= qu_prev;
+            qa_prev = na;
+            qu_prev = nu;
+            const uint32_t i = uint32_t(e) * pl + ixy;
+            __builtin_nontemporal_store(ga, a.g_alpha + i);
+            __builtin_nontemporal_store(gu, a.g_u + i);
+            const double gpc = c_prev * gp;
+            const double db = gu - gpc, da = ga + gpc;
+            red[4] = fma(gu, gu, red[4]);
+            red[5] = fma(db, db, red[5]);
+            red[6] = fma(da, da, red[6]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            th0[q] = th1[q];
+            th1[q] = nth[q];
+        }
+#pragma unroll
+        for (int k = 0; k < NB; ++k) zo[k] = nzo[k];
+        gp = ngp;
     }
 }
 
-// m0 = 63 q + r with 1 <= r <= 15 (512 = 8 * 63 + 8): instead of a (q+1)-th 64-lane tile that
-// computes r + 1 columns with 64 lanes, a 16 x (NT/16) strip image covers those columns for G
-// consecutive main y-tiles (tile order per group: G rows of main tiles, then the strip). The
-// per-cell arithmetic and its order are the same in either image, so the fields are unchanged.
-template <int ORD, int UM, bool DTH, int NB, int IH>
-__global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
-    constexpr int IW = f3d::IW, TX = f3d::TX, TY = IH - 1, NT = IW * IH;
+template <int ORD, int UM, bool DTH, int NB>
+__global__ __launch_bounds__(f3a::NT) void k_admm3a(const Fused3dArgs a) {
+    constexpr int NT = f3a::NT, NI = f3a_nimg<NB, ORD>();
     double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new, c_prev = a.c_prev;
     if (a.ctl) {
         if (a.ctl->done) return;
@@ -609,33 +628,16 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
         t_new = a.ctl->t_next;
         c_prev = a.ctl->c_prev;
     }
-    __shared__ double szr[2 * NB * NT];
+    __shared__ double szr[2 * NI * f3a::IH * f3a::IW];
     double red[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     const int bid = a.xcd ? int((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)) : int(blockIdx.x);
     const bool valid = bid < a.nblocks;
     if (valid) {
         const int tz = bid / a.tpz, rem = bid - tz * a.tpz;
         const int z0 = a.zlo + tz * a.zchunk, z1 = min(a.zhi, z0 + a.zchunk);
-        if (a.strip) {
-            constexpr int SH = NT / f3d::SW, G = (SH - 1) / TY;
-            const int per = G * a.tiles_x + 1;
-            const int grp = rem / per, o = rem - grp * per;
-            if (o == G * a.tiles_x) {
-                admm3d_tile<ORD, UM, DTH, NB, f3d::SW, SH>(a, szr, red, a.tiles_x * TX - 1, grp * G * TY - 1,
-                                                           G * TY + 1, z0, z1, t_old, c_old, t_new, c_prev);
-            } else {
-                const int tyi = grp * G + o / a.tiles_x, txi = o - (o / a.tiles_x) * a.tiles_x;
-                if (tyi < a.tiles_y)
-                    admm3d_tile<ORD, UM, DTH, NB, IW, IH>(a, szr, red, txi * TX - 1, tyi * TY - 1, IH, z0, z1, t_old,
-                                                          c_old, t_new, c_prev);
-            }
-        } else {
-            const int tyi = rem / a.tiles_x, txi = rem - tyi * a.tiles_x;
-            admm3d_tile<ORD, UM, DTH, NB, IW, IH>(a, szr, red, txi * TX - 1, tyi * TY - 1, IH, z0, z1, t_old, c_old,
-                                                  t_new, c_prev);
-        }
+        const int tyi = rem / a.tiles_x, txi = rem - tyi * a.tiles_x;
+        admm3a_tile<ORD, UM, DTH, NB>(a, szr, red, txi * 64, tyi * f3a::TY - 1, z0, z1, t_old, c_old, t_new, c_prev);
     }
-    // block reduction (max in slot 3)
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
@@ -658,35 +660,17 @@ __global__ __launch_bounds__(f3d::IW * IH) void k_admm3d(const Fused3dArgs a) {
     }
 }
 
-// 16 image rows (one 1024-thread workgroup per CU) by default: 2.6-5 % faster than 8 rows (two
-// 512-thread workgroups per CU) with every setting timed inside one process on two boxes
-// (tools/env_probe.py, profiles/r01/v10_env_probe.txt). MVTV_F3D_IH=8 selects the 8-row image.
-int f3d::rows() {   // read per launch set-up (tools/env_probe.py varies it inside one process)
-    const char* e = probe_env("MVTV_F3D_IH");
-    return (e && std::atoi(e) == 8) ? 8 : 16;
-}
-
 namespace {
 Fused3dArgs f3d_args(const Geom& g) {
     Fused3dArgs a{};
     a.g = g;
     a.zlo = int(g.ibeg / (g.m[0] * g.m[1]));
     a.zhi = int(g.iend / (g.m[0] * g.m[1]));
-    const int TY = f3d::rows() - 1, m0 = int(g.m[0]), r0 = m0 % f3d::TX;
-    const char* xe = probe_env("MVTV_F3D_XCD");     // read per launch set-up (tools/env_probe.py)
+    const char* xe = probe_env("MVTV_F3D_XCD");
     a.xcd = !xe || std::atoi(xe) != 0;
-    const char* se = probe_env("MVTV_F3D_STRIP");   // read per launch set-up (tools/env_probe.py)
-    const bool strip_on = !se || std::atoi(se) != 0;
-    a.tiles_y = int((int(g.m[1]) + TY - 1) / TY);
-    a.strip = strip_on && m0 >= f3d::TX && r0 >= 1 && r0 <= f3d::SW - 1;
-    if (a.strip) {
-        const int G = (f3d::IW * (TY + 1) / f3d::SW - 1) / TY;   // main y-tiles per strip tile
-        a.tiles_x = m0 / f3d::TX;
-        a.tpz = (a.tiles_y + G - 1) / G * (G * a.tiles_x + 1);
-    } else {
-        a.tiles_x = (m0 + f3d::TX - 1) / f3d::TX;
-        a.tpz = a.tiles_x * a.tiles_y;
-    }
+    a.tiles_x = int((g.m[0] + 63) / 64);
+    a.tiles_y = int((int(g.m[1]) + f3a::TY - 1) / f3a::TY);
+    a.tpz = a.tiles_x * a.tiles_y;
     const int tiles = a.tpz;
     // dim-2 chunks: ~4096 workgroups, or up to ~8192 while a chunk keeps >= 32 planes (each chunk
     // recomputes one plane). 512^3: 6 -> 13 chunks, fused kernel -2 % on two boxes, each setting
@@ -746,28 +730,23 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
     const int grid = (a.nblocks + 7) / 8 * 8;
     *nparts = grid;
     const bool dth = theta_old != nullptr;
-    auto pick = [&](auto ihc) {
-        constexpr int IH = decltype(ihc)::value;
-        auto go = [&](auto kern) {
-            klaunch(kern, dim3(grid), dim3(f3d::IW * IH), 0, s, a);
-            return hipGetLastError();
-        };
-        if (order == 0) {
-            if (umode == U_EXPLICIT)
-                return dth ? go(k_admm3d<0, U_EXPLICIT, true, 7, IH>) : go(k_admm3d<0, U_EXPLICIT, false, 7, IH>);
-            return dth ? go(k_admm3d<0, U_FROM_Z, true, 7, IH>) : go(k_admm3d<0, U_FROM_Z, false, 7, IH>);
-        }
-        if (g.nb == 6) {
-            if (umode == U_EXPLICIT)
-                return dth ? go(k_admm3d<1, U_EXPLICIT, true, 6, IH>) : go(k_admm3d<1, U_EXPLICIT, false, 6, IH>);
-            return dth ? go(k_admm3d<1, U_FROM_Z, true, 6, IH>) : go(k_admm3d<1, U_FROM_Z, false, 6, IH>);
-        }
-        if (umode == U_EXPLICIT)
-            return dth ? go(k_admm3d<1, U_EXPLICIT, true, 7, IH>) : go(k_admm3d<1, U_EXPLICIT, false, 7, IH>);
-        return dth ? go(k_admm3d<1, U_FROM_Z, true, 7, IH>) : go(k_admm3d<1, U_FROM_Z, false, 7, IH>);
+    auto go = [&](auto kern) {
+        klaunch(kern, dim3(grid), dim3(f3a::NT), 0, s, a);
+        return hipGetLastError();
     };
-    if (f3d::rows() == 8) return pick(std::integral_constant<int, 8>{});
-    return pick(std::integral_constant<int, 16>{});
+    if (order == 0) {
+        if (umode == U_EXPLICIT)
+            return dth ? go(k_admm3a<0, U_EXPLICIT, true, 7>) : go(k_admm3a<0, U_EXPLICIT, false, 7>);
+        return dth ? go(k_admm3a<0, U_FROM_Z, true, 7>) : go(k_admm3a<0, U_FROM_Z, false, 7>);
+    }
+    if (g.nb == 6) {
+        if (umode == U_EXPLICIT)
+            return dth ? go(k_admm3a<1, U_EXPLICIT, true, 6>) : go(k_admm3a<1, U_EXPLICIT, false, 6>);
+        return dth ? go(k_admm3a<1, U_FROM_Z, true, 6>) : go(k_admm3a<1, U_FROM_Z, false, 6>);
+    }
+    if (umode == U_EXPLICIT)
+        return dth ? go(k_admm3a<1, U_EXPLICIT, true, 7>) : go(k_admm3a<1, U_EXPLICIT, false, 7>);
+    return dth ? go(k_admm3a<1, U_FROM_Z, true, 7>) : go(k_admm3a<1, U_FROM_Z, false, 7>);
 }
 
 // =============================================================================================

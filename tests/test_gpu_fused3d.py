@@ -1,5 +1,6 @@
-"""Fused 3-D edge kernel (k_admm3d) on meshes whose dim 0 leaves a ragged last column block
-(m0 = 63 q + r): r in 1..15 runs the 16-wide strip tiles, r >= 16 the 64-lane tiles. Each run is
+"""Fused 3-D edge kernel (k_admm3a: 64-column tiles aligned to the edge chunks, 14 owned rows per
+tile) on meshes whose dims 0 and 1 leave ragged last tiles (m0 % 64 != 0, m1 % 14 != 0) and on exact
+multiples; m2 sets the dim-2 chunking (non-power-of-two meshes take the Jacobi-PCG solve). Each run is
 checked against the C oracle (oracle/c/mvtv_oracle.c, variant B of rcpp…/solvers.cpp:96-136,
 pinned to the golden fixtures in test_oracle_c.py) over fixed ADMM iterations: rho exactly, theta
 and u to 1e-9 of their max (both sides solve to PCG rtol 1e-13, or exactly by DCT on the GPU)."""
@@ -13,10 +14,9 @@ from multivartv_amd.synth import towers  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n,iters", [(64, 8), (72, 6), (80, 6), (128, 4)],
-                         ids=["r1_strip", "r9_strip", "r17_tiles", "r2_strip"])
-def test_fused_ragged_dim0_matches_oracle(n, iters):
-    m = [n, n, n]
+@pytest.mark.parametrize("m,iters", [([64, 64, 64], 8), ([72, 72, 20], 6), ([100, 100, 30], 5), ([128, 128, 128], 4)],
+                         ids=["aligned", "r8", "r36_pcg", "aligned_128"])
+def test_fused_ragged_dim0_matches_oracle(m, iters):
     y = towers(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     lam = 1.0
