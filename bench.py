@@ -7,6 +7,10 @@ rho0 = lambda/5, u0 = 0, theta0 = mean(y), fixed-iteration mode (the stopping
 test is evaluated but not acted on), PCG theta-solves warm-started at
 rtol 1e-10. Inputs are resident in HBM before timing starts.
 
+Other BASELINE configs: ``--dims 2 --size 1024`` (config 2), ``--dims 3 --size 256`` (config 3),
+``--dims 4 --size 128`` (config 5 on one GPU) and ``--mode cv`` (config 4's work item: a CV fold's
+warm-started lambda chunk on 2048^2 with a 0/1 fold mask W, so the theta-solve is Jacobi-PCG).
+
 Multi-GPU (torchrun, one process per GPU): every rank fits its own independent
 512^3 mesh (noise seed + rank) — the embarrassingly parallel "independent mesh
 fits" sharding of the north star — so value = total iterations/s of all ranks
@@ -50,12 +54,13 @@ def parse():
                     help="theta-solve: auto = spectral (exact DCT solve) where it applies, else Jacobi-PCG")
     ap.add_argument("--pcg-steps", type=int, default=10,
                     help="steps of the secondary Jacobi-PCG leg reported beside the main one (0 = skip)")
-    ap.add_argument("--mode", choices=["independent", "slab"], default="independent",
+    ap.add_argument("--mode", choices=["independent", "slab", "cv"], default="independent",
                     help="N > 1: independent fits per GPU (weak scaling, default) or one mesh slab-decomposed "
                          "over the GPUs (strong scaling; RCCL halo exchange + all-to-all transposes)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-planes", type=int, default=0,
-                    help="cpu_baseline sample: slowest-dim planes of the mesh (0 = auto)")
+                    help="cpu_baseline sample: slowest-dim planes of the mesh (0 = a quarter of them)")
+    ap.add_argument("--cpu-full", action="store_true", help="cpu_baseline on the whole mesh (no extrapolation)")
     return ap.parse_args()
 
 
@@ -94,35 +99,72 @@ class Dist:
 
 
 def load_pmc(name):
+    """Per-launch HBM bytes of kernel `name` from the last committed rocprofv3 PMC pass of this code
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py): (bytes, source label) or (None, None)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         d = json.load(open(path))
-        return d.get(name)
+        meta = d.get("_source", {})
+        label = f"profiles/pmc_traffic.json ({meta.get('pass', 'rocprofv3 FETCH_SIZE + WRITE_SIZE')}, {meta.get('date', '?')})"
+        return d.get(name), label
     except Exception:
-        return None
+        return None, None
 
 
-def cpu_baseline(m, lam, pcg_iters, planes):
-    """Oracle (C, OpenMP) on a bounded slab of the same workload, scaled to full-mesh iterations/s."""
+def cpu_baseline(m, lam, pcg_iters, planes, full=False):
+    """The CPU oracle on the host cores, one ADMM iteration (variant B) of the same towers problem:
+      * spectral (the headline's like-for-like): oracle/c/mvtv_oracle.c's loop with the exact theta-solve
+        by scipy.fft.dctn / idctn, all cores; this is `value`;
+      * pcg: the same loop with Jacobi-PCG at the GPU PCG leg's mean iteration count, all cores and 1 thread.
+    On a slab of `planes` of the last dimension (the per-iteration work is linear in the node count, so the
+    rate is scaled by N_full / N_slab and labelled as such), or on the whole mesh with full=True."""
     from oracle import c_oracle
-    sub = list(m[:-1]) + [planes]
+    ncores = c_oracle.threads()
+    sub = list(m) if full else list(m[:-1]) + [planes]
     y = towers(sub)
     N = y.size
     E = c_oracle.num_edges(sub)
-    th = np.full(N, y.mean())
-    u = np.zeros(E)
     deltas = [(1.0 + 2e-4) / v for v in m]
-    t0 = time.perf_counter()
-    st = c_oracle.admm_rcpp(sub, y, lam, th, u, lam / 5.0, deltas, fixed_iters=1, pcg_fixed=int(pcg_iters))
-    dt = time.perf_counter() - t0
     scale = float(np.prod(m)) / float(N)
-    return dict(value=1.0 / (dt * scale), unit="iters/s", cores=c_oracle.threads(), kind="port",
-                sample=(f"1 ADMM iteration (variant B, {int(pcg_iters)} PCG iterations = GPU mean) on a "
-                        f"{'x'.join(map(str, sub))} slab of the same towers problem ({dt:.1f} s), "
-                        f"scaled by N_full/N_slab = {scale:.0f}; oracle/c/mvtv_oracle.c, OpenMP"),
-                seconds=dt, pcg_iters=st["pcg_iters"])
+
+    def timed(fn, **kw):
+        th = np.full(N, y.mean())
+        u = np.zeros(E)
+        t0 = time.perf_counter()
+        fn(sub, y, lam, th, u, lam / 5.0, deltas, fixed_iters=1, **kw)
+        return time.perf_counter() - t0
+
+    c_oracle.set_threads(ncores)
+    import scipy.fft
+    sym = c_oracle.dtd_symbol(sub, deltas)                                    # setup, outside the timing
+    scipy.fft.dctn(np.zeros([8] * len(sub)), type=2, norm="ortho", workers=ncores)   # thread-pool warm-up
+    t_spec = timed(c_oracle.admm_rcpp_spectral, workers=ncores, sym=sym)
+    t_pcg = timed(c_oracle.admm_rcpp, pcg_fixed=int(pcg_iters))
+    # 1 thread on a quarter of the sample (bounded run time), scaled the same way
+    sub1 = sub[:-1] + [max(1, sub[-1] // 4)]
+    y1 = towers(sub1)
+    c_oracle.set_threads(1)
+    th1, u1 = np.full(y1.size, y1.mean()), np.zeros(c_oracle.num_edges(sub1))
+    t0 = time.perf_counter()
+    c_oracle.admm_rcpp(sub1, y1, lam, th1, u1, lam / 5.0, deltas, fixed_iters=1, pcg_fixed=int(pcg_iters))
+    t_1 = time.perf_counter() - t0
+    c_oracle.set_threads(ncores)
+    scale1 = float(np.prod(m)) / float(y1.size)
+    where = "the whole mesh" if full else (f"a {'x'.join(map(str, sub))} slab, rate scaled by N_full/N_slab = "
+                                           f"{scale:.0f}")
+    best_spec = t_spec <= t_pcg
+    return dict(value=1.0 / (min(t_spec, t_pcg) * scale), unit="iters/s", cores=ncores, kind="port",
+                algorithm="spectral" if best_spec else f"Jacobi-PCG x {int(pcg_iters)}",
+                sample=(f"1 ADMM iteration (variant B) of the same towers problem on {where}, "
+                        f"{ncores} threads: oracle/c/mvtv_oracle.c loop with the faster of its two theta-solves "
+                        f"(scipy.fft DCT: {t_spec:.2f} s; Jacobi-PCG at the GPU leg's iteration count: {t_pcg:.2f} s)"),
+                spectral_all_cores=1.0 / (t_spec * scale),
+                pcg_all_cores=1.0 / (t_pcg * scale), pcg_iters=int(pcg_iters), pcg_seconds=round(t_pcg, 2),
+                pcg_1thread=1.0 / (t_1 * scale1),
+                pcg_1thread_sample=f"{'x'.join(map(str, sub1))} slab, {t_1:.1f} s, scaled by {scale1:.0f}",
+                spectral_seconds=round(t_spec, 2))
 
 
 def slab_main(a):
@@ -175,8 +217,76 @@ def slab_main(a):
     D.close()
 
 
+def cv_main(a):
+    """Config 4's work item (BASELINE.json: 2D 2048^2, 32-lambda CV path batched over 8 GPUs): on each rank
+    one CV fold's warm-started lambda chunk (rcpp…/solvers.cpp:340-353 -> mbs_path :204-222). Fold
+    (rank % 5) of kfoldinds drops 1/5 of the lattice points, so W = O^T O is a 0/1 mask and the theta-solve
+    is the Jacobi-PCG (rtol 1e-10, warm-started). The 32-lambda grid is create_lambdas' (lam_max_pinv on the
+    GPU, 1e-4 lambda_max .. lambda_max); rank r takes lambdas [4r, 4r+4) (mod 32) and runs steps/4 fixed ADMM
+    iterations at each, theta / u / rho carried (one mvtv_path call). value = ADMM iterations/s of all ranks."""
+    from multivartv_amd import cv as mcv
+    D = Dist(os.environ.get("MVTV_DIST_BACKEND", "nccl"))
+    m = [a.size] * a.dims
+    y = towers(m)
+    fold = mcv.kfoldinds(y.size, 5, seed=0)
+    W = (fold != D.rank % 5).astype(np.float64)
+    oty = W * y
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    P = mv.Problem(m, oty, wdiag=W, deltas=deltas, order=mv.ORDER_CPP, device=D.local % max(1, mv.device_count()))
+    ymean = float(y[W > 0].mean())
+    del y, fold
+    lmax, _ = P.lambda_max()
+    grid = np.exp(np.linspace(np.log(lmax * 1e-4), np.log(lmax), 32))[::-1]
+    chunk = grid[(4 * D.rank + np.arange(4)) % 32]
+    per = max(1, a.steps // 4)
+    steps = 4 * per
+    opts = dict(pcg_rtol=a.pcg_rtol)
+    if a.warmup > 0:
+        P.path(chunk[:1], np.full(P.N, ymean), chunk[0] / 5.0, want_thetas=False, fixed_iters=a.warmup, **opts)
+    D.barrier()
+    P.timing(True)
+    t0 = time.perf_counter()
+    _, rhos, stats = P.path(chunk, np.full(P.N, ymean), chunk[0] / 5.0, want_thetas=False, fixed_iters=per, **opts)
+    t1 = time.perf_counter()
+    D.barrier()
+    tim = P.timings()
+    P.timing(False)
+    g_elapsed, = D.allreduce([t1 - t0], "max")
+    kbar = sum(st["pcg_iters"] for st in stats) / steps
+    dom = max((k for k in tim if tim[k]["bytes_per_launch"] > 0 and tim[k]["launches"]), key=lambda k: tim[k]["ms"])
+    d_avg = tim[dom]["ms"] / tim[dom]["launches"]
+    achieved = tim[dom]["bytes_per_launch"] / (d_avg * 1e-3) / 1e9
+    kern = {k: dict(avg_ms=round(v["ms"] / v["launches"], 4), launches=v["launches"],
+                    share=round(v["ms"] / ((t1 - t0) * 1e3), 4)) for k, v in tim.items() if v["launches"]}
+    N = P.N
+    P.close()
+    if D.rank == 0:
+        print(json.dumps({
+            "metric": "ADMM iters/sec on 512^3 fp64 mesh; achieved HBM GB/s vs peak at 1/2/4/8 GPUs",
+            "value": round(D.world * steps / g_elapsed, 4), "unit": "iters/s", "n_gpus": D.world, "steps": steps,
+            "warmup": a.warmup, "ms_per_step": round(g_elapsed / steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: 2D towers + 0.5 N(0,1) on the lattice, CV fold mask W (kfoldinds seed 0), O = I on the "
+                    "training rows",
+            "config": {"workload": f"config 4 work item: {a.dims}D {a.size}^{a.dims} CV fold (rank % 5) lambda chunk, "
+                                   f"4 lambdas x {per} fixed iterations, warm-started, variant B",
+                       "mesh": m, "nodes": N, "lambdas": [float(v) for v in chunk], "theta_solver": "pcg",
+                       "pcg_rtol": a.pcg_rtol, "pcg_iters_mean": round(kbar, 2), "rho_out": [float(r) for r in rhos],
+                       "parallelism": f"fold / lambda-chunk work items, one per GPU (x{D.world})"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "bytes_per_launch": tim[dom]["bytes_per_launch"], "avg_launch_ms": round(d_avg, 4),
+                         "mall_resident": 8 * N * 7 < 256 * 2 ** 20},
+            "kernels": kern, "cpu_baseline": None}), flush=True)
+    D.close()
+
+
 def main():
     a = parse()
+    if a.mode == "cv":
+        if a.size == 512 and a.dims == 3:   # config 4's shape unless given
+            a.dims, a.size = 2, 2048
+        return cv_main(a)
     if a.mode == "slab" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
         return slab_main(a)
     # the independent fits share nothing but the barrier, the max time and the final residual
@@ -250,14 +360,18 @@ def main():
     achieved = tim[dom]["bytes_per_launch"] / (d_avg_ms * 1e-3) / 1e9
     N, E = P.N, P.E
     iter_gbps = moved * a.steps / elapsed / 1e9                  # algorithmic bytes of every kernel launched
-    pmc = load_pmc(dom)
+    pmc, pmc_src = load_pmc(dom) if (a.dims, a.size) == (3, 512) else (None, None)
 
     cpu = None
     if D.world == 1 and not a.no_cpu:
-        planes = a.cpu_planes or max(4, m[-1] // 8)
+        planes = a.cpu_planes or max(4, m[-1] // 4)
         try:
-            k_cpu = pcg_leg["pcg_iters_mean"] if pcg_leg else kbar   # the oracle's theta-solve is PCG
-            cpu = cpu_baseline(m, lam, max(1, round(k_cpu)), planes)
+            k_cpu = pcg_leg["pcg_iters_mean"] if pcg_leg else kbar   # the oracle's PCG leg runs the GPU's mean count
+            cpu = cpu_baseline(m, lam, max(1, round(k_cpu)), planes, full=a.cpu_full)
+            # like for like: spectral GPU value / spectral CPU; Jacobi-PCG leg / the same PCG on the CPU
+            cpu["gpu_over_cpu_spectral"] = round(D.world * a.steps / g_elapsed / cpu["spectral_all_cores"], 1)
+            if pcg_leg:
+                cpu["gpu_pcg_leg_over_cpu_pcg"] = round(pcg_leg["value"] / cpu["pcg_all_cores"], 1)
         except Exception as e:  # the baseline is reported, never required
             log(f"cpu_baseline failed: {e}")
     P.close()
@@ -285,8 +399,11 @@ def main():
                                        f"barrier / max-time / residual all-reduce)") if D.world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": pmc, "bytes_per_launch": tim[dom]["bytes_per_launch"],
-                         "avg_launch_ms": round(d_avg_ms, 4)},
+                         "traffic": pmc, "traffic_source": pmc_src, "bytes_per_launch": tim[dom]["bytes_per_launch"],
+                         "avg_launch_ms": round(d_avg_ms, 4),
+                         # a mesh whose working set fits the 256 MiB Infinity Cache is served partly on-die:
+                         # its "HBM" fraction is an upper bound, not an HBM measurement (SURVEY §7 hard part 7)
+                         "mall_resident": 8 * N * 6 < 256 * 2 ** 20},
             "iteration_hbm": {"bytes_per_iter": moved, "GBps": round(iter_gbps, 1),
                               "frac": round(iter_gbps / HBM_PEAK_GBPS, 4),
                               "survey_bytes_per_iter": 8.0 * (5 * E + 8 * N + 10 * kbar * N)},

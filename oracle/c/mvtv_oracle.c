@@ -269,6 +269,15 @@ int mvtv_oracle_threads(void) {
 #endif
 }
 
+/* OpenMP threads of the following calls (CPU-baseline legs time 1 thread and all threads) */
+void mvtv_oracle_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
 int64_t mvtv_oracle_edges(int p, const int64_t* m, int order, int weighted) {
     geom_t g;
     double d[4] = {1, 1, 1, 1};
@@ -277,10 +286,52 @@ int64_t mvtv_oracle_edges(int p, const int64_t* m, int order, int weighted) {
 }
 
 /* stats[0] iters, [1] r_norm, [2] s_norm, [3] eps_pri, [4] eps_dual, [5] pcg iters total, [6] max pcg relres */
+/* theta-solve callback: x = (I + sigma D^T D)^-1 b (the caller's direct solver, e.g. cosine transforms) */
+typedef int (*theta_solve_fn)(double sigma, const double* b, double* x, void* ctx);
+
+static int admm_rcpp_impl(int p, const int64_t* m, int order, int weighted, const double* deltas, const double* oty,
+                          const double* W, double lambda, double* theta, double* u, double* rho_io, int fixed_iters,
+                          double tol, int max_counter, double pcg_rtol, int pcg_fixed, int pcg_maxit, double* stats,
+                          theta_solve_fn solve, void* ctx);
+
 int mvtv_oracle_admm_rcpp(int p, const int64_t* m, int order, int weighted, const double* deltas,
                           const double* oty, const double* W, double lambda, double* theta, double* u, double* rho_io,
                           int fixed_iters, double tol, int max_counter, double pcg_rtol, int pcg_fixed,
                           int pcg_maxit, double* stats) {
+    return admm_rcpp_impl(p, m, order, weighted, deltas, oty, W, lambda, theta, u, rho_io, fixed_iters, tol,
+                          max_counter, pcg_rtol, pcg_fixed, pcg_maxit, stats, NULL, NULL);
+}
+
+/* the same loop with the theta-solve done by `solve` (W must be NULL: the direct solvers are for W = I) */
+int mvtv_oracle_admm_rcpp_cb(int p, const int64_t* m, int order, int weighted, const double* deltas,
+                             const double* oty, double lambda, double* theta, double* u, double* rho_io,
+                             int fixed_iters, double tol, int max_counter, double* stats, theta_solve_fn solve,
+                             void* ctx) {
+    if (!solve) return -3;
+    return admm_rcpp_impl(p, m, order, weighted, deltas, oty, NULL, lambda, theta, u, rho_io, fixed_iters, tol,
+                          max_counter, 0.0, 0, 0, stats, solve, ctx);
+}
+
+/* d = D theta and out = D^T v on the compact edge layout (operator checks, CPU baselines) */
+int mvtv_oracle_apply_D(int p, const int64_t* m, int order, int weighted, const double* deltas, const double* theta,
+                        double* d) {
+    geom_t g;
+    if (geom_init(&g, p, m, order, weighted, deltas)) return -1;
+    apply_D(&g, theta, d);
+    return 0;
+}
+int mvtv_oracle_apply_Dt(int p, const int64_t* m, int order, int weighted, const double* deltas, const double* v,
+                         double* out) {
+    geom_t g;
+    if (geom_init(&g, p, m, order, weighted, deltas)) return -1;
+    apply_Dt(&g, v, out);
+    return 0;
+}
+
+static int admm_rcpp_impl(int p, const int64_t* m, int order, int weighted, const double* deltas, const double* oty,
+                          const double* W, double lambda, double* theta, double* u, double* rho_io, int fixed_iters,
+                          double tol, int max_counter, double pcg_rtol, int pcg_fixed, int pcg_maxit, double* stats,
+                          theta_solve_fn solve, void* ctx) {
     geom_t g;
     if (geom_init(&g, p, m, order, weighted, deltas)) return -1;
     const int64_t N = g.N, E = g.E;
@@ -310,7 +361,11 @@ int mvtv_oracle_admm_rcpp(int p, const int64_t* m, int order, int weighted, cons
 #pragma omp parallel for schedule(static)
         for (int64_t i = 0; i < N; ++i) b[i] = oty[i] + rho * tmp[i];
         double rel = 0.0;
-        pcg_total += pcg(&g, W, rho, b, theta, r, pv, q, pcg_rtol, pcg_maxit, pcg_fixed, &rel);
+        if (solve) {
+            if (solve(rho, b, theta, ctx) != 0) return -4;
+        } else {
+            pcg_total += pcg(&g, W, rho, b, theta, r, pv, q, pcg_rtol, pcg_maxit, pcg_fixed, &rel);
+        }
         if (rel > relmax) relmax = rel;
         apply_D(&g, theta, dth);
         const double t = lambda / rho;

@@ -66,7 +66,16 @@ def main(out_dir: str, dest: str | None):
     w8 = known / (cw["copy8"] * 1024) if cw.get("copy8") else None
     f16 = known / (cf["copy16"] * 1024) if cf.get("copy16") else None
     w16 = known / (cw["copy16"] * 1024) if cw.get("copy16") else None
-    out = {"calibration": {"fetch_factor_8B": f8, "write_factor_8B": w8, "fetch_factor_16B": f16,
+    import datetime
+    import subprocess
+    try:
+        head = subprocess.check_output(["git", "rev-parse", "--short", "HEAD"], text=True,
+                                       cwd=os.path.dirname(os.path.abspath(__file__))).strip()
+    except Exception:
+        head = "?"
+    out = {"_source": {"pass": f"rocprofv3 FETCH_SIZE + WRITE_SIZE passes of {out_dir} (tree {head})",
+                       "date": datetime.date.today().isoformat()},
+           "calibration": {"fetch_factor_8B": f8, "write_factor_8B": w8, "fetch_factor_16B": f16,
                            "write_factor_16B": w16},
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
