@@ -51,7 +51,9 @@ def parse():
     ap.add_argument("--lam", type=float, default=1.0)
     ap.add_argument("--pcg-rtol", type=float, default=1e-10)
     ap.add_argument("--solver", choices=["auto", "pcg", "spectral"], default="auto",
-                    help="theta-solve: auto = spectral (exact DCT solve) where it applies, else Jacobi-PCG")
+                    help="theta-solve: auto = spectral (exact DCT solve) where it applies, else the spectrally "
+                         "preconditioned PCG (power-of-two meshes), else Jacobi-PCG; pcg = Jacobi-PCG; "
+                         "spectral = the exact solve (--mode cv: the spectrally preconditioned PCG)")
     ap.add_argument("--pcg-steps", type=int, default=10,
                     help="steps of the secondary Jacobi-PCG leg reported beside the main one (0 = skip)")
     ap.add_argument("--mode", choices=["independent", "slab", "cv"], default="independent",
@@ -240,7 +242,8 @@ def cv_main(a):
     chunk = grid[(4 * D.rank + np.arange(4)) % 32]
     per = max(1, a.steps // 4)
     steps = 4 * per
-    opts = dict(pcg_rtol=a.pcg_rtol)
+    solver = {"auto": mv.SOLVER_AUTO, "pcg": mv.SOLVER_PCG, "spectral": mv.SOLVER_PCG_SPECTRAL}[a.solver]
+    opts = dict(pcg_rtol=a.pcg_rtol, theta_solver=solver)
     if a.warmup > 0:
         P.path(chunk[:1], np.full(P.N, ymean), chunk[0] / 5.0, want_thetas=False, fixed_iters=a.warmup, **opts)
     D.barrier()
@@ -270,7 +273,9 @@ def cv_main(a):
                     "training rows",
             "config": {"workload": f"config 4 work item: {a.dims}D {a.size}^{a.dims} CV fold (rank % 5) lambda chunk, "
                                    f"4 lambdas x {per} fixed iterations, warm-started, variant B",
-                       "mesh": m, "nodes": N, "lambdas": [float(v) for v in chunk], "theta_solver": "pcg",
+                       "mesh": m, "nodes": N, "lambdas": [float(v) for v in chunk],
+                       "theta_solver": {mv.SOLVER_PCG: "jacobi_pcg", mv.SOLVER_PCG_SPECTRAL: "pcg_spectral"}.get(
+                           stats[0]["theta_solver"], "?"),
                        "pcg_rtol": a.pcg_rtol, "pcg_iters_mean": round(kbar, 2), "rho_out": [float(r) for r in rhos],
                        "parallelism": f"fold / lambda-chunk work items, one per GPU (x{D.world})"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,

@@ -85,12 +85,14 @@ typedef struct mvtv_admm_opts {
 /* theta-solve of (W + sigma D^T D) theta = b. The reference factorises with SuperLU every
  * iteration (rcpp…/solvers.cpp:113, cpp-code/solvers.cpp:116, code/solvers.py:72). */
 typedef enum mvtv_theta_solver {
-    MVTV_SOLVER_AUTO = 0,      /* SPECTRAL where it is exact, else PCG */
+    MVTV_SOLVER_AUTO = 0,      /* SPECTRAL where it is exact; else PCG_SPECTRAL on power-of-two meshes <= 4096; else PCG */
     MVTV_SOLVER_PCG = 1,       /* Jacobi-PCG on the 3^p-point stencil, warm-started, pcg_rtol */
     MVTV_SOLVER_SPECTRAL = 2,  /* direct: cosine transforms + diagonal divide. Exact for W = I (mesh == data)
                                   with every m_j a power of two <= 4096; MVTV_BAD_ARG otherwise */
-    MVTV_SOLVER_PCG_SPECTRAL = 3 /* PCG preconditioned by the exact inverse of mean(W) I + sigma D^T D (cosine
-                                  transforms): for W != I (scattered data, CV folds) on power-of-two meshes */
+    MVTV_SOLVER_PCG_SPECTRAL = 3 /* PCG preconditioned by S (mean(W) I + sigma D^T D) S, its middle factor inverted
+                                  exactly by cosine transforms, S = I or a Jacobi-like diagonal scaling when W varies
+                                  strongly against sigma D^T D's diagonal: for W != I (scattered data, CV folds) on
+                                  power-of-two meshes */
 } mvtv_theta_solver;
 
 typedef struct mvtv_admm_stats {

@@ -90,6 +90,9 @@ struct mvtv_problem {
     double* pcg_b = nullptr;      // right-hand side of the spectrally preconditioned PCG
     double* g4 = nullptr;         // 4 N-arrays: the two-pass 4-D gather's partial sums
     double wmean = 1.0;           // mean(W): the preconditioner's identity weight
+    double wstd = 0.0;            // std(W): chooses the diagonally scaled spectral preconditioner
+    double* pcg_s = nullptr;      // 1/s of the scaled spectral preconditioner
+    double* pcg_t = nullptr;      // r / s, the preconditioner's input
     AdmmCtl* ctl = nullptr;       // device control block of the asynchronous ADMM loop
     AdmmCtl* host_ctl = nullptr;  // pinned mirror
     int admm_hint = 0;            // ADMM iterations of the last converged run (enqueue-ahead depth)
@@ -277,7 +280,7 @@ mvtv_status pick_zpair(mvtv_problem* P, bool track_theta) {
 void free_all(mvtv_problem* P) {
     double** bufs[] = {&P->oty, &P->wdiag, &P->theta, &P->edges, &P->ga, &P->gu, &P->guprev, &P->r,
                        &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->scratch,
-                       &P->edges2, &P->pcg_b, &P->g4, &P->edges3};
+                       &P->edges2, &P->pcg_b, &P->g4, &P->edges3, &P->pcg_s, &P->pcg_t};
     for (double** b : bufs)
         if (*b) {
             (void)hipFree(*b);
@@ -500,9 +503,13 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
     return MVTV_OK;
 }
 
-// (W + sigma D^T D) x = oty + ca*ga + cb*gb by PCG with M = mean(W) I + sigma D^T D, applied exactly by
-// the spectral solve. Scalars stay on the device (PcgState, k_finalize ops 1-3); iterations enqueued
-// after convergence return at once (st->done), the host polls like pcg_solve.
+// (W + sigma D^T D) x = oty + ca*ga + cb*gb by PCG with the spectral preconditioner M = S A0 S,
+// A0 = mean(W) I + sigma D^T D applied exactly by the cosine-transform solve. S = I when W is nearly
+// constant against sigma D^T D's diagonal d (std(W) < 0.1 mean(d)); otherwise S = diag(sqrt(d / mean d)),
+// which turns M into the Jacobi preconditioner as sigma -> 0 and into A0 as sigma grows (PCG counts to
+// rtol 1e-10 from zero, 128^2 / 256^2: CV-fold mask at sigma = 6: Jacobi 187-192, M 19; scattered counts
+// at sigma = 0.04: Jacobi 115, scaled M 95, unscaled 297). Scalars stay on the device
+// (PcgState, k_finalize ops 1-3); iterations enqueued after convergence return at once (st->done).
 mvtv_status pcgs_solve(mvtv_problem* P, double sigma, const double* oty, const double* ga, double ca,
                        const double* gb, double cb, double* x, double rtol, int maxit, int* iters, double* relres) {
     const Launch L = P->L();
@@ -510,12 +517,32 @@ mvtv_status pcgs_solve(mvtv_problem* P, double sigma, const double* oty, const d
     if (!P->pcg_b) MVTV_TRY(alloc(&P->pcg_b, P->g.N));
     double *r = P->r, *z = P->q, *p = P->p, *q = P->p2, *b = P->pcg_b;
     const double w0 = P->wmean > 0.0 ? P->wmean : 1.0;
+    // mean over the mesh of D^T D's diagonal: sum_S cS[S] prod_{j in S} mean(l_j), l_j = 1 at the ends, 2 inside
+    double cmean = 0.0;
+    for (int S = 1; S < (1 << P->g.p); ++S) {
+        double prod = P->g.cS[S];
+        for (int j = 0; j < P->g.p; ++j)
+            if ((S >> j) & 1) prod *= 2.0 * double(P->g.m[j] - 1) / double(P->g.m[j]);
+        cmean += prod;
+    }
+    const double dbar = w0 + sigma * cmean;
+    const bool scaled = P->wmode == W_DIAG && P->wstd >= 0.1 * dbar;
+    double *sinv = nullptr, *t = nullptr;
+    if (scaled) {
+        if (!P->pcg_s) MVTV_TRY(alloc(&P->pcg_s, P->g.N));
+        if (!P->pcg_t) MVTV_TRY(alloc(&P->pcg_t, P->g.N));
+        sinv = P->pcg_s;
+        t = P->pcg_t;
+        HIP_TRY(launch_pcgs_sinv(P->g, L, sigma, P->wmode, P->wdiag, dbar, sinv));
+    }
+    const double* rin = scaled ? t : r;
     int h = P->tstart(MVTV_K_PCG_INIT);
     HIP_TRY(launch_apply_A(P->g, L, sigma, P->wmode, P->wdiag, x, q, nullptr, nullptr));
     P->tstop(h);
-    HIP_TRY(launch_pcgs_vec(P->g, L, 0, oty, ga, ca, gb, cb, x, r, p, q, nullptr, b, P->st, nullptr, 0));
-    MVTV_TRY(spectral_solve(P, sigma, r, nullptr, 0.0, nullptr, 0.0, z, nullptr, w0, nullptr));
-    HIP_TRY(launch_pcgs_vec(P->g, L, 2, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, z, b, P->st, P->partials, 1));
+    HIP_TRY(launch_pcgs_vec(P->g, L, 0, oty, ga, ca, gb, cb, x, r, p, q, nullptr, b, sinv, t, P->st, nullptr, 0));
+    MVTV_TRY(spectral_solve(P, sigma, rin, nullptr, 0.0, nullptr, 0.0, z, nullptr, w0, nullptr));
+    HIP_TRY(launch_pcgs_vec(P->g, L, 2, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, z, b, sinv, nullptr, P->st,
+                            P->partials, 1));
     HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 3, 0, 1, nullptr, P->st, rtol * rtol, maxit));
     HIP_TRY(hipMemcpyAsync(p, z, size_t(P->g.N) * sizeof(double), hipMemcpyDeviceToDevice, P->stream));
     const int32_t* skip = &P->st->done;
@@ -525,15 +552,16 @@ mvtv_status pcgs_solve(mvtv_problem* P, double sigma, const double* oty, const d
         P->tstop(hh);
         HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 0, 2, nullptr, P->st));         // alpha
         hh = P->tstart(MVTV_K_PCG_UPDATE);
-        HIP_TRY(launch_pcgs_vec(P->g, L, 1, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, nullptr, b, P->st,
-                                nullptr, 0));
+        HIP_TRY(launch_pcgs_vec(P->g, L, 1, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, nullptr, b, sinv, t,
+                                P->st, nullptr, 0));
         P->tstop(hh);
-        MVTV_TRY(spectral_solve(P, sigma, r, nullptr, 0.0, nullptr, 0.0, z, nullptr, w0, skip));   // z = M^-1 r
-        HIP_TRY(launch_pcgs_vec(P->g, L, 2, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, z, b, P->st,
-                                P->partials, 0));
+        MVTV_TRY(spectral_solve(P, sigma, rin, nullptr, 0.0, nullptr, 0.0, z, nullptr, w0, skip));   // z = M^-1 r
+        HIP_TRY(launch_pcgs_vec(P->g, L, 2, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, z, b, sinv, nullptr,
+                                P->st, P->partials, 0));
         HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 3, 0, 3, nullptr, P->st));         // beta, done
         hh = P->tstart(MVTV_K_PCG_DIRECTION);
-        HIP_TRY(launch_pcgs_vec(P->g, L, 3, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, z, b, P->st, nullptr, 0));
+        HIP_TRY(launch_pcgs_vec(P->g, L, 3, nullptr, nullptr, 0.0, nullptr, 0.0, x, r, p, q, z, b, nullptr, nullptr,
+                                P->st, nullptr, 0));
         P->tstop(hh);
         return MVTV_OK;
     };
@@ -805,11 +833,15 @@ mvtv_status mvtv_problem_set_data(mvtv_problem* P, const double* oty, const doub
         if (!P->wdiag) MVTV_TRY(alloc(&P->wdiag, P->g.N));
         HIP_TRY(hipMemcpyAsync(P->wdiag, wdiag, bytes, hipMemcpyHostToDevice, P->stream));
         P->wmode = W_DIAG;
-        double acc = 0.0;
+        double acc = 0.0, acc2 = 0.0;
         for (uint32_t i = 0; i < P->g.N; ++i) acc += wdiag[i];
         P->wmean = acc / double(P->g.N);
+        for (uint32_t i = 0; i < P->g.N; ++i) acc2 += (wdiag[i] - P->wmean) * (wdiag[i] - P->wmean);
+        P->wstd = std::sqrt(acc2 / double(P->g.N));
     } else {
         P->wmode = W_IDENTITY;
+        P->wmean = 1.0;
+        P->wstd = 0.0;
     }
     HIP_TRY(hipStreamSynchronize(P->stream));
     return MVTV_OK;
@@ -873,7 +905,11 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         return fail(MVTV_BAD_ARG, "spectral preconditioner needs power-of-two m_j <= 4096");
     const bool spectral = o.theta_solver == MVTV_SOLVER_SPECTRAL ||
                           (o.theta_solver == MVTV_SOLVER_AUTO && spectral_ok(P));
-    const bool pcg_spec = o.theta_solver == MVTV_SOLVER_PCG_SPECTRAL;
+    // AUTO with W != I on a power-of-two mesh: PCG with the spectral preconditioner (K an order of magnitude
+    // below Jacobi's once sigma D^T D dominates); other meshes: Jacobi-PCG
+    const bool pcg_spec = o.theta_solver == MVTV_SOLVER_PCG_SPECTRAL ||
+                          (o.theta_solver == MVTV_SOLVER_AUTO && !spectral && P->spec_mesh && P->wmode != W_NONE &&
+                           !P->slab);
 
     // ---- initial state: u explicit in the edge buffer, alpha_0 = D theta_0 ------------------
     double rho;
@@ -1388,9 +1424,15 @@ mvtv_status mvtv_problem_set_scattered(mvtv_problem* P, const double* axes, cons
     if (uint64_t(n) == uint64_t(P->g.N) && hit == uint64_t(P->g.N)) {
         P->wmode = W_IDENTITY;
         P->wmean = 1.0;
+        P->wstd = 0.0;
     } else {
         P->wmode = W_DIAG;
         P->wmean = double(n) / double(P->g.N);
+        std::vector<double> w(P->g.N);   // std(W) for the preconditioner choice (setup path)
+        HIP_TRY(hipMemcpy(w.data(), P->wdiag, size_t(P->g.N) * sizeof(double), hipMemcpyDeviceToHost));
+        double acc2 = 0.0;
+        for (double v : w) acc2 += (v - P->wmean) * (v - P->wmean);
+        P->wstd = std::sqrt(acc2 / double(P->g.N));
     }
     return MVTV_OK;
 }

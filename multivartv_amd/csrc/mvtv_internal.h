@@ -203,11 +203,16 @@ hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n);
 // CG vector steps of lam_max_pinv (op 0 |x|^2 into partials, 1 x += c p & y -= c t, 2 x = p + c x, 3 y -= c t)
 hipError_t launch_cg_vec(const Geom& g, const Launch& L, int op, double coef, double* x, double* y, const double* p,
                          const double* t, double* partials);
-// vector steps of PCG with the spectral preconditioner (mvtv_kernels.hip k_pcgs_vec): op 0 b and
-// r = b - q with |b|^2; 1 x, r update; 2 (r.z, |r|^2 [, |b|^2]) in PR layout; 3 p = z + beta p
+// vector steps of PCG with the (optionally diagonally scaled) spectral preconditioner (mvtv_kernels.hip
+// k_pcgs_vec): op 0 b and r = b - q with t = r sinv; 1 x, r update with t = r sinv; 2 z *= sinv and
+// (r.z, |r|^2 [, |b|^2]) in PR layout; 3 p = z + beta p. sinv / t may be nullptr (no scaling)
 hipError_t launch_pcgs_vec(const Geom& g, const Launch& L, int op, const double* oty, const double* ga, double ca,
-                           const double* gb, double cb, double* x, double* r, double* p, const double* q,
-                           const double* z, double* b, const PcgState* st, double* partials, int with_b2);
+                           const double* gb, double cb, double* x, double* r, double* p, const double* q, double* z,
+                           double* b, const double* sinv, double* t, const PcgState* st, double* partials,
+                           int with_b2);
+// sinv = sqrt(dbar / jacobi_diag) of W + sigma D^T D
+hipError_t launch_pcgs_sinv(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag, double dbar,
+                            double* sinv);
 // per-workgroup max |D x| (one max-partial per workgroup, L.grid rows)
 hipError_t launch_dmaxabs(const Geom& g, int order, const Launch& L, const double* x, double* partials);
 // compact <-> padded edge layouts for one block segment [e0, e0+cnt) of block k

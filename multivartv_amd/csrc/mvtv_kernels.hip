@@ -474,18 +474,21 @@ __global__ __launch_bounds__(kThreads) void k_dmaxabs(Geom g, const double* __re
 }
 
 // --------------------------------------------------------------------- PCG with the spectral preconditioner
-// M = wbar I + sigma D^T D (exact inverse by cosine transforms, mvtv_spectral.hip) for A = W + sigma D^T D.
-// op 0: b = oty + ca ga + cb gb, r = b - q (q = A x)
-// op 1: x += alpha p, r -= alpha q (alpha from the PCG state)
-// op 2: partials, 3 per workgroup: (|b|^2, r.z, |r|^2) = k_finalize op 1's layout when with_b2,
-//       else (r.z, |r|^2, 0) = op 3's
+// A = W + sigma D^T D, preconditioner M = S A0 S with A0 = w0 I + sigma D^T D (exact inverse by cosine
+// transforms, mvtv_spectral.hip) and S = diag(s) (sinv = 1/s; sinv == nullptr: S = I, plain spectral).
+// op 0: b = oty + ca ga + cb gb, r = b - q (q = A x); t = r sinv
+// op 1: x += alpha p, r -= alpha q (alpha from the PCG state); t = r sinv
+// op 2: z *= sinv (the solve's output, in place); partials, 3 per workgroup: (|b|^2, r.z, |r|^2) = k_finalize
+//       op 1's layout when with_b2, else (r.z, |r|^2, 0) = op 3's
 // op 3: p = z + beta p
+// (t == nullptr: no scaled copy; the solve reads r itself)
 __global__ __launch_bounds__(kThreads) void k_pcgs_vec(int op, uint32_t n, const double* __restrict__ oty,
                                                        const double* __restrict__ ga, double ca,
                                                        const double* __restrict__ gb, double cb,
                                                        double* __restrict__ x, double* __restrict__ r,
                                                        double* __restrict__ p, const double* __restrict__ q,
-                                                       const double* __restrict__ z, double* __restrict__ b,
+                                                       double* __restrict__ z, double* __restrict__ b,
+                                                       const double* __restrict__ sinv, double* __restrict__ t,
                                                        const PcgState* __restrict__ st, double* __restrict__ partials,
                                                        int with_b2) {
     // op 0 and the init reduction (with_b2) run before k_finalize op 1 resets st->done
@@ -496,18 +499,27 @@ __global__ __launch_bounds__(kThreads) void k_pcgs_vec(int op, uint32_t n, const
         if (op == 0) {
             const double bi = fma(cb, gb[i], fma(ca, ga[i], oty[i]));
             b[i] = bi;
-            r[i] = bi - q[i];
+            const double ri = bi - q[i];
+            r[i] = ri;
+            if (t) t[i] = ri * sinv[i];
         } else if (op == 1) {
             x[i] = fma(alpha, p[i], x[i]);
-            r[i] = fma(-alpha, q[i], r[i]);
+            const double ri = fma(-alpha, q[i], r[i]);
+            r[i] = ri;
+            if (t) t[i] = ri * sinv[i];
         } else if (op == 2) {
             const double ri = r[i];
+            double zi = z[i];
+            if (sinv) {
+                zi *= sinv[i];
+                z[i] = zi;
+            }
             if (with_b2) {
                 red[PR_B2] = fma(b[i], b[i], red[PR_B2]);
-                red[PR_RZ] = fma(ri, z[i], red[PR_RZ]);
+                red[PR_RZ] = fma(ri, zi, red[PR_RZ]);
                 red[PR_R2] = fma(ri, ri, red[PR_R2]);
             } else {
-                red[0] = fma(ri, z[i], red[0]);
+                red[0] = fma(ri, zi, red[0]);
                 red[1] = fma(ri, ri, red[1]);
             }
         } else {
@@ -515,6 +527,18 @@ __global__ __launch_bounds__(kThreads) void k_pcgs_vec(int op, uint32_t n, const
         }
     }
     if (op == 2) block_reduce_store<3, 0>(red, partials);
+}
+
+// sinv = sqrt(dbar / d) with d the Jacobi diagonal of W + sigma D^T D: the diagonal scaling of the spectral
+// preconditioner when W varies a lot against sigma D^T D's diagonal (M -> Jacobi as sigma -> 0)
+template <int P, int WM>
+__global__ __launch_bounds__(kThreads) void k_pcgs_sinv(Geom g, double sigma, const double* __restrict__ wdiag,
+                                                        double dbar, double* __restrict__ sinv) {
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < g.N; i += gridDim.x * kThreads) {
+        uint32_t c[kMaxDims];
+        decode<P>(g, i, c);
+        sinv[i] = sqrt(dbar / jacobi_diag<P, WM>(g, sigma, wdiag, i, c));
+    }
 }
 
 struct RedDims {
@@ -874,11 +898,24 @@ hipError_t launch_dmaxabs(const Geom& g, int order, const Launch& L, const doubl
 }
 
 hipError_t launch_pcgs_vec(const Geom& g, const Launch& L, int op, const double* oty, const double* ga, double ca,
-                           const double* gb, double cb, double* x, double* r, double* p, const double* q,
-                           const double* z, double* b, const PcgState* st, double* partials, int with_b2) {
-    klaunch(k_pcgs_vec, dim3(L.grid), dim3(kThreads), 0, L.stream, op, g.N, oty, ga, ca, gb, cb, x, r, p, q, z, b, st,
-            partials, with_b2);
+                           const double* gb, double cb, double* x, double* r, double* p, const double* q, double* z,
+                           double* b, const double* sinv, double* t, const PcgState* st, double* partials,
+                           int with_b2) {
+    klaunch(k_pcgs_vec, dim3(L.grid), dim3(kThreads), 0, L.stream, op, g.N, oty, ga, ca, gb, cb, x, r, p, q, z, b,
+            sinv, t, st, partials, with_b2);
     return hipGetLastError();
+}
+
+hipError_t launch_pcgs_sinv(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag, double dbar,
+                            double* sinv) {
+    return dispatch_p(g.p, [&](auto pc) {
+        constexpr int P = decltype(pc)::value;
+        return dispatch_w(wmode, [&](auto wc) {
+            constexpr int WM = decltype(wc)::value;
+            klaunch((k_pcgs_sinv<P, WM>), dim3(L.grid), dim3(kThreads), 0, L.stream, g, sigma, wdiag, dbar, sinv);
+            return hipGetLastError();
+        });
+    });
 }
 
 hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n) {

@@ -55,7 +55,8 @@ def test_config5_4d_128_single_gpu():
     assert sp["pcg_unconverged"] == 0
 
 
-def test_config4_fold_path_2048_vs_c_oracle():
+@pytest.mark.parametrize("solver", [mv.SOLVER_AUTO, mv.SOLVER_PCG], ids=["auto_pcg_spectral", "jacobi_pcg"])
+def test_config4_fold_path_2048_vs_c_oracle(solver):
     from oracle import c_oracle
     m = [2048, 2048]
     y = towers(m)
@@ -69,14 +70,15 @@ def test_config4_fold_path_2048_vs_c_oracle():
     with mv.Problem(m, oty, wdiag=W, deltas=deltas, order=mv.ORDER_CPP) as P:
         assert not P.spectral_ok()
         thetas, rhos, stats = P.path(lams, np.full(y.size, ymean), lams[0] / 5.0, fixed_iters=iters,
-                                     pcg_rtol=1e-13)
+                                     pcg_rtol=1e-13, theta_solver=solver)
     th = np.full(y.size, ymean)
     u = np.zeros(c_oracle.num_edges(m))
     rho = lams[0] / 5.0
     for k, lam in enumerate(lams):
         st = c_oracle.admm_rcpp(m, oty, lam, th, u, rho, deltas, W=W, fixed_iters=iters, pcg_rtol=1e-13)
         rho = st["rho"]
-        assert stats[k]["iters"] == iters and stats[k]["theta_solver"] == mv.SOLVER_PCG
+        want = mv.SOLVER_PCG if solver == mv.SOLVER_PCG else mv.SOLVER_PCG_SPECTRAL
+        assert stats[k]["iters"] == iters and stats[k]["theta_solver"] == want
         assert rhos[k] == rho
         assert np.max(np.abs(thetas[k] - th)) <= 1e-9 * np.max(np.abs(th)), k
         assert stats[k]["r_norm"] == pytest.approx(st["r_norm"], rel=1e-8)

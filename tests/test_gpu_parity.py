@@ -84,13 +84,20 @@ def _rcpp_problem(meta, g):
     return mv.Problem(meta["m"], g["Oty"], wdiag=wdiag, deltas=meta["deltas"], order=mv.ORDER_CPP)
 
 
-SOLVERS = [mv.SOLVER_PCG, mv.SOLVER_AUTO]   # AUTO = spectral where exact (W = I, power-of-two mesh)
+# AUTO = spectral where exact (W = I, power-of-two mesh), PCG_SPECTRAL for W != I on power-of-two meshes
+SOLVERS = [mv.SOLVER_PCG, mv.SOLVER_AUTO, mv.SOLVER_PCG_SPECTRAL]
+
+
+def _skip_unless_pow2(meta, solver):
+    if solver == mv.SOLVER_PCG_SPECTRAL and any(v & (v - 1) for v in meta["m"]):
+        pytest.skip("the cosine-transform preconditioner needs power-of-two m_j")
 
 
 @pytest.mark.parametrize("solver", SOLVERS)
 @pytest.mark.parametrize("name", RCPP)
 def test_rcpp_trajectory(name, solver):
     meta, g = load_golden(name)
+    _skip_unless_pow2(meta, solver)
     P = _rcpp_problem(meta, g)
     for k in (1, 5, 20):
         th, u, rho, st = P.admm(meta["lam"], g["theta0"], u=np.zeros(P.E), rho=meta["rho0"],
@@ -111,6 +118,7 @@ def test_rcpp_trajectory(name, solver):
 @pytest.mark.parametrize("name", RCPP)
 def test_rcpp_converged(name, solver):
     meta, g = load_golden(name)
+    _skip_unless_pow2(meta, solver)
     P = _rcpp_problem(meta, g)
     th, u, rho, st = P.admm(meta["lam"], g["theta0"], u=np.zeros(P.E), rho=meta["rho0"], pcg_rtol=1e-13,
                             theta_solver=solver)
@@ -124,6 +132,8 @@ def test_rcpp_converged(name, solver):
 @pytest.mark.parametrize("solver", SOLVERS)
 def test_rcpp_warm_path_resident(solver):
     meta, g = load_golden("rcpp_path_2d_16")
+    if solver == mv.SOLVER_PCG_SPECTRAL:
+        pytest.skip("W = I: the spectral solve is exact there")
     y = g["y"]
     P = mv.Problem(meta["m"], y, deltas=meta["deltas"], order=mv.ORDER_CPP)
     assert P.spectral_ok()
@@ -143,6 +153,7 @@ def test_rcpp_warm_path_resident(solver):
 @pytest.mark.parametrize("name", ["cpp_2d_16", "cpp_3d_8_unit", "cpp_2d_12_frac"])
 def test_cpp_variant(name, solver):
     meta, g = load_golden(name)
+    _skip_unless_pow2(meta, solver)
     P = mv.Problem(meta["m"], g["y"], deltas=meta["deltas"], order=mv.ORDER_CPP, weighted=not meta["unit"])
     th, u, rho, st = P.admm(meta["lam"], g["theta0"], variant=mv.VARIANT_CPP, ymean=meta["ymean"], pcg_rtol=1e-13,
                             theta_solver=solver)

@@ -103,7 +103,7 @@ def test_spectral_rejected_when_not_exact():
     with mv.Problem([8, 8], rng.standard_normal(64), wdiag=rng.uniform(0, 2, 64).round(), deltas=[1, 1]) as P:
         assert not P.spectral_ok()                                               # W != I
         _, _, _, st = P.admm(1.0, np.zeros(64), u=np.zeros(P.E), rho=0.2, fixed_iters=2)
-        assert st["theta_solver"] == mv.SOLVER_PCG
+        assert st["theta_solver"] == mv.SOLVER_PCG_SPECTRAL                     # AUTO: power-of-two mesh
 
 
 def test_spectral_admm_towers_3d():
@@ -194,8 +194,8 @@ def _fold_problem(m, k, seed):
 
 @pytest.mark.parametrize("case", ["scat_32x32", "scat_16x16x16", "fold_64x64", "fold_16x16x16"])
 def test_spectrally_preconditioned_pcg(case):
-    """W != I (scattered data, CV folds): PCG preconditioned by mean(W) I + sigma D^T D (applied exactly
-    by cosine transforms) reproduces the SuperLU trajectory like Jacobi-PCG."""
+    """W != I (scattered data, CV folds): PCG preconditioned by S (mean(W) I + sigma D^T D) S (the middle
+    factor applied exactly by cosine transforms) reproduces the SuperLU trajectory like Jacobi-PCG."""
     kind, dims = case.split("_")
     m = [int(v) for v in dims.split("x")]
     W, oty = (_scattered_problem(m, 3 * int(np.prod(m)) // 5, seed=len(m)) if kind == "scat"
