@@ -60,6 +60,8 @@ def parse():
                     help="N > 1: independent fits per GPU (weak scaling, default) or one mesh slab-decomposed "
                          "over the GPUs (strong scaling; RCCL halo exchange + all-to-all transposes)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--slab-ranks", type=int, default=1,
+                    help="--mode slab without torchrun: ranks of an in-process rehearsal on one GPU (1: RCCL, one rank)")
     ap.add_argument("--cpu-planes", type=int, default=0,
                     help="cpu_baseline sample: slowest-dim planes of the mesh (0 = a quarter of them)")
     ap.add_argument("--cpu-full", action="store_true", help="cpu_baseline on the whole mesh (no extrapolation)")
@@ -170,52 +172,89 @@ def cpu_baseline(m, lam, pcg_iters, planes, full=False):
 
 
 def slab_main(a):
-    """One 3-D mesh decomposed over the ranks: strong scaling."""
+    """One mesh decomposed over the ranks: strong scaling. Every rank runs the whole
+    ADMM loop inside libmvtv (mvtv_slab_run) with RCCL collectives on its stream. World size 1 (no torchrun):
+    --slab-ranks R > 1 rehearses an R-rank decomposition on the one GPU with the in-process loopback
+    transport; R = 1 runs the slab loop over a one-rank RCCL communicator."""
     from multivartv_amd import slab
-    # MVTV_SLAB_BACKEND=gloo rehearses the decomposition with host-staged exchanges (several ranks may
-    # then share one GPU); the default is RCCL with device-resident exchange buffers
-    D = Dist(os.environ.get("MVTV_SLAB_BACKEND", "nccl"))
-    dev = D.local % max(1, mv.device_count())
     m = [a.size] * a.dims
     lam = a.lam
-    b = slab.plane_bounds(m[-1], D.world)
-    pl = int(np.prod(m[:-1]))
-    y = towers(m, start=int(b[D.rank]) * pl, count=int(b[D.rank + 1] - b[D.rank]) * pl)
-    ysum, = D.allreduce([float(y.sum())], "sum")
     deltas = [(1.0 + 2e-4) / v for v in m]
-    S = slab.SlabADMM(m, y, deltas, ysum / float(np.prod(m)), device=dev)
-    del y
-    if a.warmup > 0:
-        S.run(lam, fixed_iters=a.warmup)
-    D.barrier()
-    S.P.timing(True)
-    t0 = time.perf_counter()
-    st = S.run(lam, fixed_iters=a.steps)
-    t1 = time.perf_counter()
-    D.barrier()
-    tim = S.P.timings()
-    S.P.timing(False)
-    g_elapsed, = D.allreduce([t1 - t0], "max")
-    per = {k: dict(avg_ms=round(v["ms"] / v["launches"], 4), launches=v["launches"]) for k, v in tim.items() if v["launches"]}
-    dom = max((k for k in tim if tim[k]["bytes_per_launch"] > 0 and tim[k]["launches"]), key=lambda k: tim[k]["ms"])
-    d_avg = tim[dom]["ms"] / tim[dom]["launches"]
-    achieved = tim[dom]["bytes_per_launch"] / (d_avg * 1e-3) / 1e9
-    S.close()
-    if D.rank == 0:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        D = Dist("nccl")
+        dev = D.local % max(1, mv.device_count())
+        b = slab.plane_bounds(m[-1], D.world)
+        pl = int(np.prod(m[:-1]))
+        y = towers(m, start=int(b[D.rank]) * pl, count=int(b[D.rank + 1] - b[D.rank]) * pl)
+        ysum, = D.allreduce([float(y.sum())], "sum")
+        comm = slab.Comm.rccl(dev)
+        S = slab.SlabADMM(m, y, deltas, ysum / float(np.prod(m)), comm, device=dev)
+        del y
+        if a.warmup > 0:
+            S.run(lam, fixed_iters=a.warmup)
+        D.barrier()
+        S.P.timing(True)
+        t0 = time.perf_counter()
+        st = S.run(lam, fixed_iters=a.steps)
+        t1 = time.perf_counter()
+        D.barrier()
+        tim = S.P.timings()
+        S.P.timing(False)
+        g_elapsed, = D.allreduce([t1 - t0], "max")
+        rank, nranks, transport = D.rank, D.world, "RCCL"
+        S.close()
+        comm.close()
+    else:
+        D = Dist("gloo")
+        R = max(1, a.slab_ranks)
+        y = towers(m)
+        if R == 1:
+            comm = slab.Comm.rccl_single(0)
+            S = slab.SlabADMM(m, y, deltas, float(y.mean()), comm, device=0)
+            del y
+            if a.warmup > 0:
+                S.run(lam, fixed_iters=a.warmup)
+            S.P.timing(True)
+            t0 = time.perf_counter()
+            st = S.run(lam, fixed_iters=a.steps)
+            t1 = time.perf_counter()
+            tim = S.P.timings()
+            S.close()
+            comm.close()
+            transport = "RCCL (one rank)"
+        else:
+            if a.warmup > 0:
+                slab.run_local_group(m, y, deltas, lam, R, fixed_iters=a.warmup)
+            t0 = time.perf_counter()
+            outs, _ = slab.run_local_group(m, y, deltas, lam, R, fixed_iters=a.steps)
+            t1 = time.perf_counter()
+            st, tim = outs[0], {}
+            transport = f"in-process loopback, {R} ranks on one GPU"
+        g_elapsed, rank, nranks = t1 - t0, 0, R
+    per = {k: dict(avg_ms=round(v["ms"] / v["launches"], 4), launches=v["launches"]) for k, v in tim.items()
+           if v["launches"]}
+    roof = None
+    if any(v["bytes_per_launch"] > 0 and v["launches"] for v in tim.values()):
+        dom = max((k for k in tim if tim[k]["bytes_per_launch"] > 0 and tim[k]["launches"]), key=lambda k: tim[k]["ms"])
+        d_avg = tim[dom]["ms"] / tim[dom]["launches"]
+        achieved = tim[dom]["bytes_per_launch"] / (d_avg * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                "bytes_per_launch": tim[dom]["bytes_per_launch"], "avg_launch_ms": round(d_avg, 4)}
+    if rank == 0:
         print(json.dumps({
             "metric": "ADMM iters/sec on 512^3 fp64 mesh; achieved HBM GB/s vs peak at 1/2/4/8 GPUs",
-            "value": round(a.steps / g_elapsed, 4), "unit": "iters/s", "n_gpus": D.world, "steps": a.steps,
+            "value": round(a.steps / g_elapsed, 4), "unit": "iters/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(g_elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: 3D towers + 0.5 N(0,1) (splitmix64/Box-Muller, seed 0x4D565456), O = I",
+            "data": "synthetic: towers + 0.5 N(0,1) (splitmix64/Box-Muller, seed 0x4D565456), O = I",
             "config": {"workload": f"{a.dims}D {a.size}^{a.dims} fp64 mesh-TV ADMM, variant B, lambda={lam}, one mesh "
-                                   f"slab-decomposed along dim {a.dims - 1}", "mesh": m, "theta_solver": "spectral",
-                       "parallelism": f"slab x{D.world} ({'RCCL' if D.backend == 'nccl' else D.backend} halo planes, "
-                                      f"all-to-all transposes, 6-sum all-reduce)"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None},
-            "kernels_rank0": per, "residuals": {"r_norm": st["r_norm"], "s_norm": st["s_norm"]},
-            "cpu_baseline": None}), flush=True)
+                                   f"slab-decomposed along dim {a.dims - 1} over {nranks} ranks", "mesh": m,
+                       "theta_solver": "spectral (distributed: all-to-all transposes of the last dimension)",
+                       "parallelism": f"slab x{nranks} ({transport}: halo planes, all-to-all, 7-sum all-reduce)"},
+            "roofline": roof, "kernels_rank0": per,
+            "residuals": {"r_norm": st["r_norm"], "s_norm": st["s_norm"]}, "cpu_baseline": None}), flush=True)
     D.close()
 
 
@@ -292,7 +331,7 @@ def main():
         if a.size == 512 and a.dims == 3:   # config 4's shape unless given
             a.dims, a.size = 2, 2048
         return cv_main(a)
-    if a.mode == "slab" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    if a.mode == "slab":
         return slab_main(a)
     # the independent fits share nothing but the barrier, the max time and the final residual
     # all-reduce: RCCL (device scalars) by default, MVTV_DIST_BACKEND=gloo for host scalars

@@ -194,40 +194,35 @@ mvtv_status mvtv_lambda_max_cpp(mvtv_problem* prob, double* out, int32_t* iters)
 /* direct theta-solve (I + sigma D^T D) x = b by cosine transforms (MVTV_SOLVER_SPECTRAL) */
 mvtv_status mvtv_solve_spectral(mvtv_problem* prob, double sigma, const double* b, double* x_out);
 
-/* ---- slab decomposition of one mesh over ranks ---------------------
- * Rank r holds planes [z_begin, z_end) of the last dimension plus one ghost plane below
- * (unless z_begin = 0) and above (unless z_end = m_global); desc->m[p-1] counts owned + ghost
- * planes and desc->oty / wdiag cover them (ghost values are not used). The host drives the loop
- * (multivartv_amd/slab.py) and moves planes / line chunks between ranks with any transport
- * (RCCL device buffers or host-staged gloo) through mvtv_copy2d; every numerical step runs here.
- * Supported: variant B, W = I, power-of-two meshes (spectral theta-solve, distributed by an
- * all-to-all transpose of the last dimension). */
+/* ---- slab decomposition of one mesh over ranks (the metric at 2-8 GPUs) ---------
+ * Rank r holds planes [z_begin, z_end) of the last dimension plus one ghost plane below (unless
+ * z_begin = 0) and above (unless z_end = m_global); desc->m[p-1] counts owned + ghost planes and
+ * desc->oty covers them (ghost values are not used). Rank r owns planes [floor(m r / G), floor(m (r+1) / G)).
+ * mvtv_slab_run is the whole variant-B loop of one rank (rcpp…/solvers.cpp:110-133) with its
+ * collectives on the problem's stream: all-to-all transposes of the distributed cosine-transform solve,
+ * halo planes of theta and of the edge state, one 7-value all-reduce per iteration feeding the device-side
+ * adapt_step / stopping decision. Supported: variant B, W = I, power-of-two m_j, u0 = 0. */
 typedef struct mvtv_slab_desc {
     int64_t m_global;          /* planes of dim p-1 in the whole mesh */
     int64_t z_begin, z_end;    /* owned planes */
     int32_t ghost_lo, ghost_hi;
 } mvtv_slab_desc;
-typedef enum mvtv_buffer_id { MVTV_BUF_THETA = 0, MVTV_BUF_EDGES = 1, MVTV_BUF_SCRATCH = 2 } mvtv_buffer_id;
+typedef struct mvtv_comm mvtv_comm;
 mvtv_status mvtv_problem_create_slab(const mvtv_problem_desc* desc, const mvtv_slab_desc* slab, mvtv_problem** out);
-/* b = oty + ca g_alpha + cb g_uprev on the owned planes, forward DCT along dims 0..p-2 into theta */
-mvtv_status mvtv_slab_solve_fwd(mvtv_problem* prob, double ca, double cb, double sigma);
-/* forward DCT / divide / inverse along dim p-1 on nq full lines [m_global][nq] (line index fastest),
- * lines q0 .. q0+nq-1 of the mesh's dims 0..p-2; lines is a device pointer (nq a power of two) */
-mvtv_status mvtv_slab_solve_mid(mvtv_problem* prob, double* lines, int64_t q0, int64_t nq, double sigma);
-/* inverse DCT along dims p-2..0 on the owned planes of theta */
-mvtv_status mvtv_slab_solve_inv(mvtv_problem* prob);
-/* g_alpha = D^T D theta (start of a run; theta ghost planes must be current) */
-mvtv_status mvtv_slab_init(mvtv_problem* prob);
-/* edge update / D^T gather on the owned planes; red4 / red3 get this rank's partial sums
- * (|r|^2, |D theta|^2, |alpha|^2, -) and (|D^T u|^2, |s_B|^2 / rho^2, |s_A|^2 / rho^2) */
-mvtv_status mvtv_slab_edge(mvtv_problem* prob, int32_t umode, double t_old, double c_old, double t_new, double* red4);
-mvtv_status mvtv_slab_gather(mvtv_problem* prob, int32_t umode, double t, double c_prev, double* red3);
-/* rows x width doubles between library buffer `what` (at offset, row pitch lib_pitch) and an
- * external host or device buffer (row pitch ext_pitch); to_ext != 0 copies out */
-mvtv_status mvtv_copy2d(mvtv_problem* prob, int32_t what, int64_t offset, int64_t rows, int64_t width,
-                        int64_t lib_pitch, int64_t ext_pitch, void* ext, int32_t to_ext);
-/* device scratch of at least n doubles owned by the problem (host-staged transports) */
-double* mvtv_scratch(mvtv_problem* prob, int64_t n);
+/* RCCL transport (one process per GPU): rank 0 makes the id, every rank passes the same 128 bytes */
+mvtv_status mvtv_comm_unique_id(uint8_t* id128);
+mvtv_status mvtv_comm_create_rccl(const uint8_t* id128, int32_t nranks, int32_t rank, int32_t device, mvtv_comm** out);
+/* in-process loopback group of nranks handles (comms[0..nranks-1]): each rank's mvtv_slab_run on its own
+ * host thread, transfers as device copies (rehearsal of the decomposition on one GPU) */
+mvtv_status mvtv_comm_create_local(int32_t nranks, mvtv_comm** comms);
+void mvtv_comm_destroy(mvtv_comm* comm);
+int32_t mvtv_comm_rank(const mvtv_comm* comm);
+int32_t mvtv_comm_size(const mvtv_comm* comm);
+/* admm_update B from theta = theta0 on every node, u = 0, rho = rho0 (rcpp…/solvers.cpp:207-209); collective
+ * over the communicator. stats hold the global norms; theta of the owned planes: mvtv_state_get (ghosts
+ * included, planes as desc->m) */
+mvtv_status mvtv_slab_run(mvtv_problem* prob, mvtv_comm* comm, const mvtv_admm_opts* opts, double lambda,
+                          double theta0, double rho0, mvtv_admm_stats* stats);
 mvtv_status mvtv_sync(mvtv_problem* prob);
 
 /* ---- instrumentation (HIP events on the solver's stream) ---------------------------- */

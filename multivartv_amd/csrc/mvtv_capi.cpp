@@ -21,180 +21,17 @@
 
 #include "mvtv/mvtv.h"
 #include "mvtv_internal.h"
+#include "mvtv_problem.h"
 
 using namespace mvtv;
 
-namespace {
+namespace mvtv {
 thread_local std::string g_last_error;
-
-mvtv_status fail(mvtv_status s, const std::string& msg) {
-    g_last_error = msg;
-    return s;
-}
-
-#define HIP_TRY(expr)                                                                                 \
-    do {                                                                                              \
-        hipError_t _e = (expr);                                                                       \
-        if (_e != hipSuccess)                                                                         \
-            return fail(_e == hipErrorOutOfMemory ? MVTV_OUT_OF_MEMORY : MVTV_HIP_ERROR,              \
-                        std::string(#expr) + ": " + hipGetErrorString(_e));                           \
-    } while (0)
-
-#define MVTV_TRY(expr)                        \
-    do {                                      \
-        mvtv_status _s = (expr);              \
-        if (_s != MVTV_OK) return _s;         \
-    } while (0)
-
-constexpr int kPcgPoll = 8;   // PCG iterations enqueued between host polls of the done flag
-
-struct DevBuf {
-    double* p = nullptr;
-    size_t n = 0;
-};
-}  // namespace
-
-struct mvtv_problem {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    Geom g{};
-    int order = 0, weighted = 1, wmode = W_IDENTITY;
-    double deltas[MVTV_MAX_DIMS] = {0, 0, 0, 0};
-    int codes[kMaxBlocks] = {0};
-    int sprime[kMaxBlocks] = {0};
-    uint64_t blk_len[kMaxBlocks] = {0};
-    int64_t E = 0;
-    int grid = 1;
-    bool fused3d = true;   // fused Chronopoulos-Gear PCG for p = 3 (MVTV_PCG=classic disables)
-    int pcg_hint = 0;      // PCG iterations of the last theta-solve (poll schedule)
-
-    double *oty = nullptr, *wdiag = nullptr;
-    double *theta = nullptr, *edges = nullptr, *ga = nullptr, *gu = nullptr, *guprev = nullptr;
-    double *r = nullptr, *p = nullptr, *q = nullptr, *thold = nullptr, *p2 = nullptr;
-    double *partials = nullptr, *red = nullptr;
-    PcgState* st = nullptr;
-    double* stage = nullptr;
-    size_t stage_n = 0;
-    double* host_red = nullptr;   // pinned: reductions + PcgState mirror
-    PcgState* host_st = nullptr;
-    SpecPlan spec;                // spectral theta-solve tables (allocated when the mesh allows it)
-    bool spec_mesh = false;       // every m_j a power of two <= 4096
-    bool e3d = false;             // z-marching 3-D edge kernels
-    bool f3d = false;             // fused 3-D edge update + gather (needs the second edge buffer)
-    double* edges2 = nullptr;     // ping-pong partner of edges for the fused kernel
-    bool zpicked = false;         // the z ping-pong pair was chosen by timed probes (pick_zpair)
-    double* edges3 = nullptr;     // third z buffer of the spectral loop (MVTV_EBUF3=1). On boxes where the fused
-                                  // launches alternate fast / slow, the slow ones are those writing into
-                                  // `edges` (measured 4.60 / 4.97 ms alternating -> 4.60 / 4.53 / 5.00);
-                                  // +7.5 GB at 512^3
-    double* pcg_b = nullptr;      // right-hand side of the spectrally preconditioned PCG
-    double* g4 = nullptr;         // 4 N-arrays: the two-pass 4-D gather's partial sums
-    double wmean = 1.0;           // mean(W): the preconditioner's identity weight
-    double wstd = 0.0;            // std(W): chooses the diagonally scaled spectral preconditioner
-    double* pcg_s = nullptr;      // 1/s of the scaled spectral preconditioner
-    double* pcg_t = nullptr;      // r / s, the preconditioner's input
-    AdmmCtl* ctl = nullptr;       // device control block of the asynchronous ADMM loop
-    AdmmCtl* host_ctl = nullptr;  // pinned mirror
-    int admm_hint = 0;            // ADMM iterations of the last converged run (enqueue-ahead depth)
-
-    // slab decomposition (mvtv_problem_create_slab): this problem holds planes [zb, ze) of dim p-1
-    // of a mesh with m_global planes, plus ghost planes below / above
-    bool slab = false;
-    int64_t m_global = 0, zb = 0, ze = 0;
-    int g_lo = 0, g_hi = 0;
-    double* scratch = nullptr;
-    size_t scratch_n = 0;
-
-    // resident ADMM state
-    bool have_state = false;
-    bool u_default = true;
-    int edge_mode = U_EXPLICIT;
-    double t_z = 0.0, c_state = 1.0, rho = 0.0;
-
-    // instrumentation
-    bool timing = false;
-    struct Pending {
-        hipEvent_t a, b;
-        int kid;
-    };
-    std::vector<Pending> pending;
-    std::vector<hipEvent_t> ev_pool;
-    double ms[MVTV_K_COUNT] = {0};
-    int64_t launches[MVTV_K_COUNT] = {0};
-
-    Launch L() const { return Launch{stream, grid}; }
-
-    hipEvent_t get_event() {
-        if (!ev_pool.empty()) {
-            hipEvent_t e = ev_pool.back();
-            ev_pool.pop_back();
-            return e;
-        }
-        hipEvent_t e;
-        (void)hipEventCreate(&e);
-        return e;
-    }
-    int tstart(int kid) {
-        if (!timing) return -1;
-        Pending pd{get_event(), get_event(), kid};
-        g_timed = TimedLaunch{pd.a, pd.b};   // stamped by the next kernel dispatch (klaunch)
-        pending.push_back(pd);
-        return int(pending.size()) - 1;
-    }
-    void tstop(int h) {
-        if (h >= 0 && g_timed.start) pending[h].kid = -1;   // the launcher enqueued nothing
-        g_timed = TimedLaunch{};
-    }
-    // second launch of a two-kernel launcher (armed in g_timed_b, moved to g_timed by the launcher)
-    int tstart_b(int kid) {
-        if (!timing) return -1;
-        Pending pd{get_event(), get_event(), kid};
-        g_timed_b = TimedLaunch{pd.a, pd.b};
-        pending.push_back(pd);
-        return int(pending.size()) - 1;
-    }
-    void tstop_b(int h) {
-        if (h >= 0 && g_timed_b.start) pending[h].kid = -1;
-        g_timed_b = TimedLaunch{};
-    }
-    void harvest() {  // call after a stream sync
-        for (auto& pd : pending) {
-            float t = 0.f;
-            if (pd.kid >= 0 && hipEventElapsedTime(&t, pd.a, pd.b) == hipSuccess) {
-                ms[pd.kid] += t;
-                launches[pd.kid] += 1;
-            }
-            ev_pool.push_back(pd.a);
-            ev_pool.push_back(pd.b);
-        }
-        pending.clear();
-    }
-    mvtv_status sync() {
-        HIP_TRY(hipStreamSynchronize(stream));
-        harvest();
-        return MVTV_OK;
-    }
-};
+}  // namespace mvtv
 
 namespace {
 
 int popcount(int x) { return __builtin_popcount(unsigned(x)); }
-
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        (void)hipGetDevice(&prev);
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
-
-mvtv_status alloc(double** ptr, size_t n) {
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(ptr), std::max<size_t>(n, 1) * sizeof(double)));
-    return MVTV_OK;
-}
 
 // Placement-aware z ping-pong: the fused 3-D kernel's time depends on WHICH physical
 // edge buffer it reads z from and writes to (profiles/r01/v12_zflip_probe.txt: up to 4.70 against
@@ -279,7 +116,7 @@ mvtv_status pick_zpair(mvtv_problem* P, bool track_theta) {
 
 void free_all(mvtv_problem* P) {
     double** bufs[] = {&P->oty, &P->wdiag, &P->theta, &P->edges, &P->ga, &P->gu, &P->guprev, &P->r,
-                       &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->scratch,
+                       &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->slab_send, &P->slab_lines,
                        &P->edges2, &P->pcg_b, &P->g4, &P->edges3, &P->pcg_s, &P->pcg_t};
     for (double** b : bufs)
         if (*b) {
@@ -774,7 +611,7 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
     if (P->spec_mesh) s = spectral_plan(P);
     P->e3d = edge3d_ok(g);
     if (s == MVTV_OK && P->e3d && g.p == 4 && gather4_ok(g)) s = alloc(&P->g4, 4 * size_t(N));
-    P->f3d = !sl && fused3d_ok(g);
+    P->f3d = fused3d_ok(g);   // slab problems too: the fused pass runs on the owned planes (Geom.ibeg/iend)
     {   // chunked edge layout for the 3-D fused path (MVTV_EAOS=0 keeps block-major): the fused kernel's
         // launches 2-4 % shorter at 512^3 on the same box (4.21 -> 4.13 ms, 5.2-5.36 -> 5.13 ms)
         const char* e = probe_env("MVTV_EAOS");
@@ -1662,185 +1499,6 @@ mvtv_status mvtv_solve_spectral(mvtv_problem* P, double sigma, const double* b, 
         s = fail(MVTV_HIP_ERROR, "solve download");
     (void)hipFree(dx);
     return s;
-}
-
-// ------------------------------------------------------------------------------ slab decomposition
-}  // extern "C"
-namespace {
-mvtv_status slab_check(mvtv_problem* P) {
-    if (!P) return fail(MVTV_BAD_ARG, "null problem");
-    if (!P->slab) return fail(MVTV_BAD_ARG, "not a slab problem (mvtv_problem_create_slab)");
-    return MVTV_OK;
-}
-// geometry of the owned planes only (spectral passes along dims 0..p-2)
-Geom owned_geom(const mvtv_problem* P, size_t* off) {
-    Geom g = P->g;
-    const int p = g.p;
-    const uint32_t plane = g.N / g.m[p - 1];
-    const uint32_t nz = uint32_t(P->ze - P->zb);
-    g.m[p - 1] = nz;
-    g.N = plane * nz;
-    g.ibeg = 0;
-    g.iend = g.N;
-    if (off) *off = size_t(P->g_lo) * plane;
-    return g;
-}
-}  // namespace
-extern "C" {
-
-mvtv_status mvtv_slab_solve_fwd(mvtv_problem* P, double ca, double cb, double sigma) {
-    MVTV_TRY(slab_check(P));
-    if (!P->spec_mesh) return fail(MVTV_BAD_ARG, "slab solve needs power-of-two m_j <= 4096");
-    DeviceGuard dg(P->device);
-    size_t off = 0;
-    const Geom g = owned_geom(P, &off);
-    for (int d = 0; d < g.p - 1; ++d) {
-        const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
-        if (d == 0)
-            HIP_TRY(launch_dct_pass(P->spec, g, P->stream, 0, 0, P->oty + off, P->ga + off, ca, P->guprev + off, cb,
-                                    P->theta + off, sigma, 1.0));
-        else
-            HIP_TRY(launch_dct_pass(P->spec, g, P->stream, 0, d, P->theta + off, nullptr, 0.0, nullptr, 0.0,
-                                    P->theta + off, sigma, 1.0));
-        P->tstop(h);
-    }
-    HIP_TRY(hipStreamSynchronize(P->stream));
-    return MVTV_OK;
-}
-
-mvtv_status mvtv_slab_solve_mid(mvtv_problem* P, double* lines, int64_t q0, int64_t nq, double sigma) {
-    MVTV_TRY(slab_check(P));
-    if (!lines || nq <= 0 || q0 < 0) return fail(MVTV_BAD_ARG, "line chunk");
-    if ((nq & (nq - 1)) != 0) return fail(MVTV_BAD_ARG, "line chunk must be a power of two");
-    DeviceGuard dg(P->device);
-    Geom g = P->g;
-    const int p = g.p;
-    const uint32_t lines_total = g.N / g.m[p - 1];
-    if (uint64_t(q0) + uint64_t(nq) > lines_total) return fail(MVTV_BAD_ARG, "line chunk out of range");
-    // the chunk as a mesh: nq lines of m_global points, line index fastest (stride nq)
-    g.m[p - 1] = uint32_t(P->m_global);
-    g.stride[p - 1] = uint32_t(nq);
-    g.N = uint32_t(nq) * uint32_t(P->m_global);
-    const int h = P->tstart(MVTV_K_DCT);
-    const double inv_n = 1.0 / (double(lines_total) * double(P->m_global));
-    HIP_TRY(launch_dct_pass(P->spec, g, P->stream, 2, p - 1, lines, nullptr, 0.0, nullptr, 0.0, lines, sigma, 1.0,
-                            nullptr, uint32_t(q0), inv_n));
-    P->tstop(h);
-    HIP_TRY(hipStreamSynchronize(P->stream));
-    return MVTV_OK;
-}
-
-mvtv_status mvtv_slab_solve_inv(mvtv_problem* P) {
-    MVTV_TRY(slab_check(P));
-    DeviceGuard dg(P->device);
-    size_t off = 0;
-    const Geom g = owned_geom(P, &off);
-    for (int d = g.p - 2; d >= 0; --d) {
-        const int h = P->tstart(MVTV_K_DCT);
-        HIP_TRY(launch_dct_pass(P->spec, g, P->stream, 1, d, P->theta + off, nullptr, 0.0, nullptr, 0.0, P->theta + off,
-                                0.0, 1.0));
-        P->tstop(h);
-    }
-    HIP_TRY(hipStreamSynchronize(P->stream));
-    return MVTV_OK;
-}
-
-mvtv_status mvtv_slab_init(mvtv_problem* P) {
-    MVTV_TRY(slab_check(P));
-    DeviceGuard dg(P->device);
-    const Launch L = P->L();
-    // g_alpha = D^T D theta0 (needs both theta ghost planes); the owned planes are what is used
-    HIP_TRY(launch_apply_A(P->g, L, 1.0, W_NONE, nullptr, P->theta, P->ga, nullptr, nullptr));
-    HIP_TRY(hipStreamSynchronize(P->stream));
-    return MVTV_OK;
-}
-
-mvtv_status mvtv_slab_edge(mvtv_problem* P, int32_t umode, double t_old, double c_old, double t_new, double* red4) {
-    MVTV_TRY(slab_check(P));
-    DeviceGuard dg(P->device);
-    const Launch L = P->L();
-    int np = L.grid;
-    const int h = P->tstart(MVTV_K_EDGE_UPDATE);
-    if (P->e3d)
-        HIP_TRY(launch_edge3d(P->g, P->order, umode, P->stream, P->theta, P->edges, t_old, c_old, t_new, nullptr,
-                              P->partials, &np));
-    else
-        HIP_TRY(launch_edge_update(P->g, P->order, umode, L, P->theta, P->edges, t_old, c_old, t_new, nullptr,
-                                   P->partials));
-    P->tstop(h);
-    HIP_TRY(launch_finalize(P->stream, P->partials, np, ER_N, 1, 0, P->red, P->st));
-    HIP_TRY(hipMemcpyAsync(P->host_red, P->red, ER_N * sizeof(double), hipMemcpyDeviceToHost, P->stream));
-    HIP_TRY(hipStreamSynchronize(P->stream));
-    if (red4)
-        for (int k = 0; k < ER_N; ++k) red4[k] = P->host_red[k];
-    return MVTV_OK;
-}
-
-mvtv_status mvtv_slab_gather(mvtv_problem* P, int32_t umode, double t, double c_prev, double* red3) {
-    MVTV_TRY(slab_check(P));
-    DeviceGuard dg(P->device);
-    const Launch L = P->L();
-    int np = L.grid;
-    const bool expl = umode == U_EXPLICIT;
-    // explicit: P->guprev = D^T u; from z: P->gu = D^T u_new (with the dual residual against P->guprev), then swap
-    double* gout = expl ? P->guprev : P->gu;
-    const double* gprev = expl ? nullptr : P->guprev;
-    const int h = P->tstart(MVTV_K_GATHER);
-    if (P->e3d)
-        HIP_TRY(launch_gather3d(P->g, P->order, umode, P->stream, P->edges, t, expl ? nullptr : P->ga, gout, gprev,
-                                c_prev, P->partials, &np, nullptr, P->g4));
-    else
-        HIP_TRY(launch_gather(P->g, P->order, umode, L, P->edges, t, expl ? nullptr : P->ga, gout, gprev, c_prev,
-                              P->partials));
-    P->tstop(h);
-    HIP_TRY(launch_finalize(P->stream, P->partials, np, GR_N, 0, 0, P->red, P->st));
-    HIP_TRY(hipMemcpyAsync(P->host_red, P->red, GR_N * sizeof(double), hipMemcpyDeviceToHost, P->stream));
-    HIP_TRY(hipStreamSynchronize(P->stream));
-    if (red3)
-        for (int k = 0; k < GR_N; ++k) red3[k] = P->host_red[k];
-    if (!expl) std::swap(P->guprev, P->gu);
-    return MVTV_OK;
-}
-
-mvtv_status mvtv_copy2d(mvtv_problem* P, int32_t what, int64_t offset, int64_t rows, int64_t width, int64_t lib_pitch,
-                        int64_t ext_pitch, void* ext, int32_t to_ext) {
-    if (!P || !ext || rows < 0 || width < 0) return fail(MVTV_BAD_ARG, "null argument");
-    DeviceGuard dg(P->device);
-    double* base = nullptr;
-    size_t cap = 0;
-    switch (what) {
-        case MVTV_BUF_THETA: base = P->theta; cap = P->g.N; break;
-        case MVTV_BUF_EDGES: base = P->edges; cap = size_t(P->g.nb) * P->g.N; break;
-        case MVTV_BUF_SCRATCH: base = P->scratch; cap = P->scratch_n; break;
-        default: return fail(MVTV_BAD_ARG, "buffer id");
-    }
-    if (rows == 0 || width == 0) return MVTV_OK;
-    if (!base || offset < 0 || lib_pitch < width || ext_pitch < width ||
-        uint64_t(offset) + uint64_t(rows - 1) * uint64_t(lib_pitch) + uint64_t(width) > cap)
-        return fail(MVTV_BAD_ARG, "copy out of range");
-    double* lib = base + offset;
-    const size_t w = size_t(width) * sizeof(double);
-    if (to_ext)
-        HIP_TRY(hipMemcpy2DAsync(ext, size_t(ext_pitch) * sizeof(double), lib, size_t(lib_pitch) * sizeof(double), w,
-                                 size_t(rows), hipMemcpyDefault, P->stream));
-    else
-        HIP_TRY(hipMemcpy2DAsync(lib, size_t(lib_pitch) * sizeof(double), ext, size_t(ext_pitch) * sizeof(double), w,
-                                 size_t(rows), hipMemcpyDefault, P->stream));
-    HIP_TRY(hipStreamSynchronize(P->stream));
-    return MVTV_OK;
-}
-
-double* mvtv_scratch(mvtv_problem* P, int64_t n) {
-    if (!P || n <= 0) return nullptr;
-    DeviceGuard dg(P->device);
-    if (P->scratch_n < size_t(n)) {
-        if (P->scratch) (void)hipFree(P->scratch);
-        P->scratch = nullptr;
-        P->scratch_n = 0;
-        if (alloc(&P->scratch, size_t(n)) != MVTV_OK) return nullptr;
-        P->scratch_n = size_t(n);
-    }
-    return P->scratch;
 }
 
 mvtv_status mvtv_sync(mvtv_problem* P) {

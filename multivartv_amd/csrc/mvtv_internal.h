@@ -231,12 +231,18 @@ struct SpecPlan {
     double* lam = nullptr;    // per dim: m_j eigenvalues 4 sin^2(pi k/(2 m_j)) of the Neumann Laplacian
     uint32_t tw_off[kMaxDims] = {0, 0, 0, 0}, twq_off[kMaxDims] = {0, 0, 0, 0}, lam_off[kMaxDims] = {0, 0, 0, 0};
 };
+// The slab-decomposed solve's all-to-all buffer layout (mode 1: the pass writes `out` packed, 2: it
+// reads `in` packed): [rank][owned plane][line mod chunk], plane = 2^lpl lines, chunk = 2^lch lines
+struct DctPack {
+    int32_t mode = 0;
+    uint32_t lpl = 0, lch = 0, nz = 0;
+};
 // mode 0 forward DCT-II, 1 inverse (DCT-III, unnormalised), 2 forward + divide by mu * N + inverse;
 // ga != nullptr forms the input as in + ca*ga + cb*gb. In place (in == out) is allowed.
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
                            double w0, const AdmmCtl* ctl = nullptr, uint32_t q_off = 0, double inv_n = 0.0,
-                           const int32_t* skip = nullptr);
+                           const int32_t* skip = nullptr, const DctPack* pack = nullptr);
 // z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /
 // launch_gather, *nparts workgroup rows
 bool edge3d_ok(const Geom& g);

@@ -1,0 +1,659 @@
+// mvtv_slab.cpp — one mesh decomposed over ranks (SURVEY §8e, config 5 / the metric at 2-8 GPUs): the whole
+// variant-B ADMM loop (rcpp-code/MultivarTV/src/solvers.cpp:110-133) of one rank, enqueued on the problem's
+// stream with its collectives, decided on the device, polled by the host only every few iterations.
+//
+// Rank r owns planes [zb, ze) of the last dimension plus one ghost plane below / above
+// (mvtv_problem_create_slab). Per iteration:
+//   theta-solve  cosine transforms along dims 0..p-2 on the owned planes, the last of them writing the
+//                all-to-all send buffer directly in [rank][plane][line chunk] order; all-to-all (grouped
+//                send / recv) -> each rank holds full dim-(p-1) lines for 1/G of the lines; forward /
+//                divide / inverse along dim p-1; all-to-all back; the first inverse pass reads the packed
+//                buffer straight into theta. No pack or unpack copies.
+//   theta halo   first owned plane -> rank-1's upper ghost, last -> rank+1's lower ghost.
+//   edge update  p = 3: the fused pass (k_admm3a) on the owned planes: its chunk-start recompute of
+//   + gather     plane zb-1 reads theta's lower ghost and z_old's lower ghost plane, which rank-1 sent
+//                at the end of the previous iteration; p = 4: edge update, z lower-ghost halo, gather.
+//   reductions   one all-reduce of the 7 partial sums into the device control block; k_admm_control
+//                then takes adapt_step / stopping on every rank from bit-identical inputs.
+//   z halo       (p = 3) last owned plane of z_new -> rank+1's ghost plane of the same buffer.
+// Transports (mvtv_comm): RCCL over xGMI (one process per GPU; librccl is opened at run time, so the
+// library has no link-time dependency on it) or an in-process loopback group (every rank on its own host
+// thread, device-to-device copies between the ranks' buffers): the same loop, testable on one GPU.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+
+#include "mvtv_problem.h"
+
+// ============================================================================================ transports
+struct mvtv_comm {
+    int rank = 0, size = 1;
+    virtual ~mvtv_comm() = default;
+    // point-to-point transfers between begin() and end() progress together (all-to-all, halos)
+    virtual mvtv_status begin() = 0;
+    virtual mvtv_status send(const double* buf, size_t n, int peer, hipStream_t s) = 0;
+    virtual mvtv_status recv(double* buf, size_t n, int peer, hipStream_t s) = 0;
+    virtual mvtv_status end(hipStream_t s) = 0;
+    virtual mvtv_status allreduce_sum(double* buf, size_t n, hipStream_t s) = 0;
+};
+
+namespace {
+
+// ---- RCCL, resolved with dlopen ------------------------------------------------------------------
+struct RcclApi {
+    void* h = nullptr;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+mvtv_status rccl_api(RcclApi** out) {
+    static RcclApi api;
+    static bool tried = false;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!tried) {
+        tried = true;
+        for (const char* name : {"/opt/rocm/lib/librccl.so.1", "librccl.so.1", "librccl.so"}) {
+            api.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (api.h) break;
+        }
+        if (api.h) {
+            auto sym = [&](auto& fp, const char* n) { fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(api.h, n)); };
+            sym(api.GetUniqueId, "ncclGetUniqueId");
+            sym(api.CommInitRank, "ncclCommInitRank");
+            sym(api.CommDestroy, "ncclCommDestroy");
+            sym(api.Send, "ncclSend");
+            sym(api.Recv, "ncclRecv");
+            sym(api.GroupStart, "ncclGroupStart");
+            sym(api.GroupEnd, "ncclGroupEnd");
+            sym(api.AllReduce, "ncclAllReduce");
+            sym(api.GetErrorString, "ncclGetErrorString");
+        }
+    }
+    if (!api.h || !api.GetUniqueId || !api.CommInitRank || !api.Send || !api.Recv || !api.GroupStart ||
+        !api.GroupEnd || !api.AllReduce)
+        return fail(MVTV_HIP_ERROR, "RCCL (librccl.so.1) not available");
+    *out = &api;
+    return MVTV_OK;
+}
+
+#define NCCL_TRY(expr)                                                                              \
+    do {                                                                                            \
+        ncclResult_t _r = (expr);                                                                   \
+        if (_r != ncclSuccess)                                                                      \
+            return fail(MVTV_HIP_ERROR, std::string("RCCL: ") + #expr + ": " +                     \
+                                            (api_->GetErrorString ? api_->GetErrorString(_r) : "?")); \
+    } while (0)
+
+// a transfer to / from this rank itself is a device copy: sends are stashed, the matching recv copies
+struct SelfCopy {
+    std::deque<std::pair<const double*, size_t>> q;
+    mvtv_status recv(double* buf, size_t n, hipStream_t s) {
+        if (q.empty() || q.front().second != n) return fail(MVTV_BAD_ARG, "self transfer without its send");
+        HIP_TRY(hipMemcpyAsync(buf, q.front().first, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        q.pop_front();
+        return MVTV_OK;
+    }
+};
+
+struct RcclComm final : mvtv_comm {
+    RcclApi* api_ = nullptr;
+    ncclComm_t comm = nullptr;
+    SelfCopy self;
+    ~RcclComm() override {
+        if (comm && api_->CommDestroy) api_->CommDestroy(comm);
+    }
+    mvtv_status begin() override {
+        NCCL_TRY(api_->GroupStart());
+        return MVTV_OK;
+    }
+    mvtv_status send(const double* buf, size_t n, int peer, hipStream_t s) override {
+        if (peer == rank) {
+            self.q.emplace_back(buf, n);
+            return MVTV_OK;
+        }
+        NCCL_TRY(api_->Send(buf, n, ncclFloat64, peer, comm, s));
+        return MVTV_OK;
+    }
+    mvtv_status recv(double* buf, size_t n, int peer, hipStream_t s) override {
+        if (peer == rank) return self.recv(buf, n, s);
+        NCCL_TRY(api_->Recv(buf, n, ncclFloat64, peer, comm, s));
+        return MVTV_OK;
+    }
+    mvtv_status end(hipStream_t) override {
+        NCCL_TRY(api_->GroupEnd());
+        return MVTV_OK;
+    }
+    mvtv_status allreduce_sum(double* buf, size_t n, hipStream_t s) override {
+        if (size == 1) return MVTV_OK;
+        NCCL_TRY(api_->AllReduce(buf, buf, n, ncclFloat64, ncclSum, comm, s));
+        return MVTV_OK;
+    }
+};
+
+// ---- in-process loopback group --------------------------------------------------------------------
+// Every rank runs its loop on its own host thread; a transfer is a device-to-device copy enqueued by the
+// receiver after the sender's data-ready event, and the sender's stream waits for the copy's event before
+// it goes on (so it cannot overwrite the source early). The all-reduce copies every rank's vector into
+// each rank's staging rows and sums them in rank order, so all ranks get bit-identical sums.
+struct LocalHub {
+    int size = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    struct Msg {
+        const double* src;
+        size_t n;
+        hipEvent_t ready;   // sender's data is complete
+        hipEvent_t* done;   // receiver records its copy's completion here
+        bool* acked;
+    };
+    std::vector<std::deque<Msg>> box;   // box[from * size + to]
+    // all-reduce rendezvous
+    int arrive = 0, leave = 0;
+    long gen = 0;
+    std::vector<double*> bufs;
+    std::vector<hipEvent_t> bev, cev;
+    std::vector<hipEvent_t> pool;   // events of finished transfers, reused (guarded by mu)
+    explicit LocalHub(int g) : size(g), box(size_t(g) * size_t(g)), bufs(size_t(g)), bev(size_t(g)), cev(size_t(g)) {}
+    ~LocalHub() {
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+    hipEvent_t event() {   // call with mu held
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        return e;
+    }
+};
+
+__global__ void k_rowsum(const double* __restrict__ stage, int rows, int n, double* __restrict__ out) {
+    const int i = int(threadIdx.x);
+    if (i >= n) return;
+    double acc = 0.0;
+    for (int r = 0; r < rows; ++r) acc += stage[r * n + i];
+    out[i] = acc;
+}
+
+struct LocalComm final : mvtv_comm {
+    std::shared_ptr<LocalHub> hub;
+    struct Pending {
+        hipEvent_t ready;   // our data-ready event (recycled once the receiver has waited on it)
+        hipEvent_t done;    // the receiver's copy-complete event
+        bool acked;
+    };
+    std::deque<Pending> sent;   // this group's sends (stable addresses)
+    double* stage = nullptr;
+    size_t stage_n = 0;
+    SelfCopy self;
+    ~LocalComm() override {
+        if (stage) (void)hipFree(stage);
+    }
+    hipEvent_t event() {
+        std::lock_guard<std::mutex> lk(hub->mu);
+        return hub->event();
+    }
+    mvtv_status begin() override {
+        sent.clear();
+        return MVTV_OK;
+    }
+    mvtv_status send(const double* buf, size_t n, int peer, hipStream_t s) override {
+        if (peer == rank) {
+            self.q.emplace_back(buf, n);
+            return MVTV_OK;
+        }
+        hipEvent_t ready = event();
+        HIP_TRY(hipEventRecord(ready, s));
+        sent.push_back(Pending{ready, nullptr, false});
+        Pending& pd = sent.back();
+        std::lock_guard<std::mutex> lk(hub->mu);
+        hub->box[size_t(rank) * size_t(size) + size_t(peer)].push_back(LocalHub::Msg{buf, n, ready, &pd.done, &pd.acked});
+        hub->cv.notify_all();
+        return MVTV_OK;
+    }
+    mvtv_status recv(double* buf, size_t n, int peer, hipStream_t s) override {
+        if (peer == rank) return self.recv(buf, n, s);
+        LocalHub::Msg m{};
+        {
+            std::unique_lock<std::mutex> lk(hub->mu);
+            auto& q = hub->box[size_t(peer) * size_t(size) + size_t(rank)];
+            hub->cv.wait(lk, [&] { return !q.empty(); });
+            m = q.front();
+            q.pop_front();
+        }
+        if (m.n != n) return fail(MVTV_BAD_ARG, "loopback transfer size mismatch");
+        HIP_TRY(hipStreamWaitEvent(s, m.ready, 0));
+        HIP_TRY(hipMemcpyAsync(buf, m.src, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        hipEvent_t done = event();
+        HIP_TRY(hipEventRecord(done, s));
+        std::lock_guard<std::mutex> lk(hub->mu);
+        *m.done = done;
+        *m.acked = true;
+        hub->cv.notify_all();
+        return MVTV_OK;
+    }
+    mvtv_status end(hipStream_t s) override {
+        std::unique_lock<std::mutex> lk(hub->mu);
+        hub->cv.wait(lk, [&] {
+            for (auto& pd : sent)
+                if (!pd.acked) return false;
+            return true;
+        });
+        lk.unlock();
+        for (auto& pd : sent) HIP_TRY(hipStreamWaitEvent(s, pd.done, 0));
+        lk.lock();   // both events have been waited on by the streams that need them: reusable
+        for (auto& pd : sent) {
+            hub->pool.push_back(pd.ready);
+            hub->pool.push_back(pd.done);
+        }
+        sent.clear();
+        return MVTV_OK;
+    }
+    // generation barrier on the hub
+    void barrier(std::unique_lock<std::mutex>& lk) {
+        const long g = hub->gen;
+        if (++hub->arrive == size) {
+            hub->arrive = 0;
+            ++hub->gen;
+            hub->cv.notify_all();
+        } else {
+            hub->cv.wait(lk, [&] { return hub->gen != g; });
+        }
+    }
+    mvtv_status allreduce_sum(double* buf, size_t n, hipStream_t s) override {
+        if (size == 1) return MVTV_OK;
+        if (n > 64) return fail(MVTV_BAD_ARG, "loopback all-reduce of more than 64 values");
+        if (stage_n < n * size_t(size)) {
+            if (stage) (void)hipFree(stage);
+            stage = nullptr;
+            MVTV_TRY(alloc(&stage, n * size_t(size)));
+            stage_n = n * size_t(size);
+        }
+        hipEvent_t ready = event(), copied = event();
+        HIP_TRY(hipEventRecord(ready, s));
+        std::unique_lock<std::mutex> lk(hub->mu);
+        hub->bufs[size_t(rank)] = buf;
+        hub->bev[size_t(rank)] = ready;
+        barrier(lk);   // every rank's vector is posted
+        lk.unlock();
+        for (int r = 0; r < size; ++r) {
+            HIP_TRY(hipStreamWaitEvent(s, hub->bev[size_t(r)], 0));
+            HIP_TRY(hipMemcpyAsync(stage + size_t(r) * n, hub->bufs[size_t(r)], n * sizeof(double),
+                                   hipMemcpyDeviceToDevice, s));
+        }
+        HIP_TRY(hipEventRecord(copied, s));
+        lk.lock();
+        hub->cev[size_t(rank)] = copied;
+        barrier(lk);   // every rank has enqueued its copies
+        lk.unlock();
+        for (int r = 0; r < size; ++r)   // nobody overwrites its vector before all copies of it are done
+            if (r != rank) HIP_TRY(hipStreamWaitEvent(s, hub->cev[size_t(r)], 0));
+        hipLaunchKernelGGL(k_rowsum, dim3(1), dim3(64), 0, s, stage, size, int(n), buf);
+        HIP_TRY(hipGetLastError());
+        lk.lock();
+        barrier(lk);   // the hub's slots may be reused
+        hub->pool.push_back(ready);
+        hub->pool.push_back(copied);
+        lk.unlock();
+        return MVTV_OK;
+    }
+};
+
+}  // namespace
+
+// ============================================================================================ C ABI
+extern "C" {
+
+mvtv_status mvtv_comm_unique_id(uint8_t* out128) {
+    if (!out128) return fail(MVTV_BAD_ARG, "null argument");
+    RcclApi* api = nullptr;
+    MVTV_TRY(rccl_api(&api));
+    ncclUniqueId id;
+    if (api->GetUniqueId(&id) != ncclSuccess) return fail(MVTV_HIP_ERROR, "ncclGetUniqueId failed");
+    std::memcpy(out128, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_comm_create_rccl(const uint8_t* id128, int32_t nranks, int32_t rank, int32_t device,
+                                  mvtv_comm** out) {
+    if (!id128 || !out || nranks < 1 || rank < 0 || rank >= nranks) return fail(MVTV_BAD_ARG, "bad argument");
+    RcclApi* api = nullptr;
+    MVTV_TRY(rccl_api(&api));
+    DeviceGuard dg(device);
+    auto* c = new RcclComm();
+    c->api_ = api;
+    c->rank = rank;
+    c->size = nranks;
+    ncclUniqueId id;
+    std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
+    const ncclResult_t r = api->CommInitRank(&c->comm, nranks, id, rank);
+    if (r != ncclSuccess) {
+        c->comm = nullptr;
+        delete c;
+        return fail(MVTV_HIP_ERROR, std::string("ncclCommInitRank: ") + (api->GetErrorString ? api->GetErrorString(r) : "?"));
+    }
+    *out = c;
+    return MVTV_OK;
+}
+
+mvtv_status mvtv_comm_create_local(int32_t nranks, mvtv_comm** out) {
+    if (!out || nranks < 1 || nranks > 64) return fail(MVTV_BAD_ARG, "nranks must be 1..64");
+    auto hub = std::make_shared<LocalHub>(nranks);
+    for (int r = 0; r < nranks; ++r) {
+        auto* c = new LocalComm();
+        c->hub = hub;
+        c->rank = r;
+        c->size = nranks;
+        out[r] = c;
+    }
+    return MVTV_OK;
+}
+
+void mvtv_comm_destroy(mvtv_comm* c) { delete c; }
+int32_t mvtv_comm_rank(const mvtv_comm* c) { return c ? c->rank : -1; }
+int32_t mvtv_comm_size(const mvtv_comm* c) { return c ? c->size : 0; }
+
+}  // extern "C"
+
+// ============================================================================================ the loop
+namespace {
+
+struct SlabGeom {
+    uint32_t plane = 0, nz = 0, zb = 0, mg = 0, lines = 0, chunk = 0, lpl = 0, lch = 0;
+    size_t off = 0;   // first owned node
+};
+
+uint32_t ilog2(uint32_t v) {
+    uint32_t l = 0;
+    while ((1u << l) < v) ++l;
+    return l;
+}
+
+}  // namespace
+
+extern "C" mvtv_status mvtv_slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, double lambda,
+                                     double theta0, double rho0, mvtv_admm_stats* stats) {
+    if (!P || !C || !opts) return fail(MVTV_BAD_ARG, "null argument");
+    if (!P->slab) return fail(MVTV_BAD_ARG, "not a slab problem (mvtv_problem_create_slab)");
+    if (opts->variant != MVTV_VARIANT_RCPP) return fail(MVTV_BAD_ARG, "the slab loop runs variant B");
+    if (P->wmode != W_IDENTITY || !P->spec_mesh) return fail(MVTV_BAD_ARG, "slab loop: W = I, power-of-two m_j <= 4096");
+    if (!(lambda >= 0.0) || !(rho0 > 0.0)) return fail(MVTV_BAD_ARG, "lambda >= 0 and rho0 > 0");
+    const auto t0 = std::chrono::steady_clock::now();
+    DeviceGuard dg(P->device);
+    const int p = P->g.p, G = C->size, rk = C->rank;
+    hipStream_t s = P->stream;
+    SlabGeom sg;
+    sg.plane = P->g.N / P->g.m[p - 1];
+    sg.nz = uint32_t(P->ze - P->zb);
+    sg.zb = uint32_t(P->zb);
+    sg.mg = uint32_t(P->m_global);
+    sg.lines = sg.plane;
+    sg.off = size_t(P->g_lo) * sg.plane;
+    if (sg.lines % uint32_t(G) != 0) return fail(MVTV_BAD_ARG, "lines must split evenly over the ranks");
+    sg.chunk = sg.lines / uint32_t(G);
+    if (sg.chunk < 2 || (sg.chunk & (sg.chunk - 1))) return fail(MVTV_BAD_ARG, "line chunk must be a power of two >= 2");
+    sg.lpl = ilog2(sg.plane);
+    sg.lch = ilog2(sg.chunk);
+    // every rank's plane range, floor(m_global r / G) as plane_bounds (multivartv_amd/slab.py): the
+    // all-to-all counts
+    std::vector<uint32_t> zbs(size_t(G) + 1);
+    for (int r = 0; r <= G; ++r) zbs[size_t(r)] = uint32_t(uint64_t(sg.mg) * uint64_t(r) / uint64_t(G));
+    if (zbs[size_t(rk)] != sg.zb || zbs[size_t(rk) + 1] != sg.zb + sg.nz)
+        return fail(MVTV_BAD_ARG, "slab plane range differs from the even split of the communicator");
+
+    const double tol = opts->tol > 0 ? opts->tol : 1e-4;
+    const int max_counter = opts->max_counter > 0 ? opts->max_counter : 3000;
+    const bool fused = P->f3d;
+    // buffers of the distributed solve: send = the owned planes in packed order, lines = m_global x chunk.
+    // One rank: the packed order is the natural one and the lines are the owned planes, so the whole
+    // solve runs in place on theta with no transfers
+    const bool solo = G == 1;
+    if (!solo && !P->slab_send) MVTV_TRY(alloc(&P->slab_send, size_t(sg.nz) * sg.lines));
+    if (!solo && !P->slab_lines) MVTV_TRY(alloc(&P->slab_lines, size_t(sg.mg) * sg.chunk));
+    if (fused && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
+    const size_t nodes = P->g.N, ebytes = size_t(P->g.nb) * nodes * sizeof(double);
+
+    // ---- initial state: theta0 everywhere (ghosts included), u0 = 0, g_alpha = D^T D theta0 -----------
+    HIP_TRY(launch_fill(s, P->theta, theta0, nodes));
+    HIP_TRY(hipMemsetAsync(P->edges, 0, ebytes, s));
+    if (fused) HIP_TRY(hipMemsetAsync(P->edges2, 0, ebytes, s));
+    HIP_TRY(hipMemsetAsync(P->guprev, 0, nodes * sizeof(double), s));
+    HIP_TRY(launch_apply_A(P->g, P->L(), 1.0, W_NONE, nullptr, P->theta, P->ga, nullptr, nullptr));
+    AdmmCtl& c = *P->host_ctl;
+    std::memset(&c, 0, sizeof(c));
+    c.variant = MVTV_VARIANT_RCPP;
+    c.fixed_iters = opts->fixed_iters > 0 ? opts->fixed_iters : 0;
+    c.max_counter = max_counter;
+    c.lambda = lambda;
+    c.tol = tol;
+    c.sqrtN = std::sqrt(double(P->g.N / P->g.m[p - 1]) * double(sg.mg));
+    {   // global edge count: sum over blocks of prod_j (m_j - [j in S']) with the global last extent
+        double E = 0.0;
+        for (int k = 0; k < P->g.nb; ++k) {
+            double len = 1.0;
+            for (int j = 0; j < p; ++j) {
+                const double mj = j == p - 1 ? double(sg.mg) : double(P->g.m[j]);
+                len *= mj - double((P->sprime[k] >> j) & 1);
+            }
+            E += len;
+        }
+        c.sqrtE = std::sqrt(E);
+    }
+    c.rho = rho0;
+    c.sigma = rho0;
+    c.c_prev = 1.0;
+    c.t_z = 0.0;
+    c.t_next = lambda / rho0;
+    c.counter = 1;
+    c.dual_norm = c.primal_norm = 1.0;
+    c.eps_dual = c.eps_pri = tol;
+    HIP_TRY(hipMemcpyAsync(P->ctl, &c, sizeof(AdmmCtl), hipMemcpyHostToDevice, s));
+
+    // geometry of the owned planes (local passes) and of this rank's line chunk (the last dimension)
+    Geom og = P->g;
+    og.m[p - 1] = sg.nz;
+    og.N = sg.plane * sg.nz;
+    og.ibeg = 0;
+    og.iend = og.N;
+    Geom lg = P->g;
+    lg.m[p - 1] = sg.mg;
+    lg.stride[p - 1] = sg.chunk;
+    lg.N = sg.chunk * sg.mg;
+    DctPack pk_out{1, sg.lpl, sg.lch, sg.nz}, pk_in{2, sg.lpl, sg.lch, sg.nz};
+    const double inv_n = 1.0 / (double(sg.lines) * double(sg.mg));
+    double* th = P->theta + sg.off;
+    double* sendbuf = solo ? th : P->slab_send;
+    double* linebuf = solo ? th : P->slab_lines;
+    const DctPack* pko = solo ? nullptr : &pk_out;
+    const DctPack* pki = solo ? nullptr : &pk_in;
+    double* gbuf[2] = {P->guprev, P->gu};
+    double* ebuf[2] = {P->edges, fused ? P->edges2 : P->edges};
+    const size_t pl = sg.plane;
+    const size_t first_owned = size_t(P->g_lo) * pl, last_owned = first_owned + size_t(sg.nz - 1) * pl;
+
+    // edge plane e of buffer z (eaos: one contiguous run of nb * plane words; block-major: nb runs)
+    auto edge_plane_xfer = [&](double* z, size_t e, int peer, bool is_send) -> mvtv_status {
+        if (P->g.eaos) {
+            double* ptr = z + e * pl * size_t(P->g.nb);
+            return is_send ? C->send(ptr, pl * size_t(P->g.nb), peer, s) : C->recv(ptr, pl * size_t(P->g.nb), peer, s);
+        }
+        for (int k = 0; k < P->g.nb; ++k) {
+            double* ptr = z + size_t(k) * nodes + e * pl;
+            MVTV_TRY(is_send ? C->send(ptr, pl, peer, s) : C->recv(ptr, pl, peer, s));
+        }
+        return MVTV_OK;
+    };
+
+    auto enqueue = [&](int j) -> mvtv_status {
+        const int um = j == 0 ? U_EXPLICIT : U_FROM_Z;
+        double* gp = gbuf[j & 1];
+        double* gn = gbuf[(j + 1) & 1];
+        double* zo = ebuf[j & 1];
+        double* zn = ebuf[(j + 1) & 1];
+        // -- theta-solve: local forward passes, the last one into the packed send buffer
+        for (int d = 0; d <= p - 2; ++d) {
+            const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
+            const bool last = d == p - 2;
+            if (d == 0)
+                HIP_TRY(launch_dct_pass(P->spec, og, s, 0, 0, P->oty + sg.off, P->ga + sg.off, 0.0, gp + sg.off, 0.0,
+                                        last ? sendbuf : th, 0.0, 1.0, P->ctl, 0, 0.0, nullptr,
+                                        last ? pko : nullptr));
+            else
+                HIP_TRY(launch_dct_pass(P->spec, og, s, 0, d, th, nullptr, 0.0, nullptr, 0.0,
+                                        last ? sendbuf : th, 0.0, 1.0, P->ctl, 0, 0.0, nullptr,
+                                        last ? pko : nullptr));
+            P->tstop(h);
+        }
+        // -- all-to-all: my planes x rank r's chunk -> rank r; rank r's planes x my chunk <- rank r
+        if (!solo) {
+            MVTV_TRY(C->begin());
+            for (int r = 0; r < G; ++r)
+                MVTV_TRY(C->send(sendbuf + size_t(r) * sg.nz * sg.chunk, size_t(sg.nz) * sg.chunk, r, s));
+            for (int r = 0; r < G; ++r)
+                MVTV_TRY(C->recv(linebuf + size_t(zbs[size_t(r)]) * sg.chunk,
+                                 size_t(zbs[size_t(r) + 1] - zbs[size_t(r)]) * sg.chunk, r, s));
+            MVTV_TRY(C->end(s));
+        }
+        {
+            const int h = P->tstart(MVTV_K_DCT);
+            HIP_TRY(launch_dct_pass(P->spec, lg, s, 2, p - 1, linebuf, nullptr, 0.0, nullptr, 0.0, linebuf, 0.0, 1.0,
+                                    P->ctl, uint32_t(rk) * sg.chunk, inv_n));
+            P->tstop(h);
+        }
+        if (!solo) {
+            MVTV_TRY(C->begin());
+            for (int r = 0; r < G; ++r)
+                MVTV_TRY(C->send(linebuf + size_t(zbs[size_t(r)]) * sg.chunk,
+                                 size_t(zbs[size_t(r) + 1] - zbs[size_t(r)]) * sg.chunk, r, s));
+            for (int r = 0; r < G; ++r)
+                MVTV_TRY(C->recv(sendbuf + size_t(r) * sg.nz * sg.chunk, size_t(sg.nz) * sg.chunk, r, s));
+            MVTV_TRY(C->end(s));
+        }
+        // -- local inverse passes, the first one from the packed buffer
+        for (int d = p - 2; d >= 0; --d) {
+            const int h = P->tstart(MVTV_K_DCT);
+            const bool first = d == p - 2;
+            HIP_TRY(launch_dct_pass(P->spec, og, s, 1, d, first ? sendbuf : th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0,
+                                    P->ctl, 0, 0.0, nullptr, first ? pki : nullptr));
+            P->tstop(h);
+        }
+        // -- theta halo: both ghost planes
+        MVTV_TRY(C->begin());
+        if (rk > 0) MVTV_TRY(C->send(P->theta + first_owned, pl, rk - 1, s));
+        if (rk < G - 1) MVTV_TRY(C->send(P->theta + last_owned, pl, rk + 1, s));
+        if (rk > 0) MVTV_TRY(C->recv(P->theta, pl, rk - 1, s));
+        if (rk < G - 1) MVTV_TRY(C->recv(P->theta + last_owned + pl, pl, rk + 1, s));
+        MVTV_TRY(C->end(s));
+        // -- edge update + gather on the owned planes, partial sums into P->red
+        if (fused) {
+            int h = P->tstart(MVTV_K_ADMM_FUSED);
+            int npf = 0;
+            HIP_TRY(launch_admm3d(P->g, P->order, um, s, P->theta, zo, zn, 0.0, 1.0, 0.0, 1.0, nullptr, P->ga, gn, gp,
+                                  P->partials, &npf, P->ctl));
+            P->tstop(h);
+            HIP_TRY(launch_finalize(s, P->partials, npf, ER_N + GR_N, -(1 << ER_DTH), 0, P->red, P->st, 0.0, 0, P->ctl));
+        } else {
+            int h = P->tstart(MVTV_K_EDGE_UPDATE);
+            int npe = P->grid;
+            if (P->e3d)
+                HIP_TRY(launch_edge3d(P->g, P->order, um, s, P->theta, P->edges, 0.0, 1.0, 0.0, nullptr, P->partials,
+                                      &npe, P->ctl));
+            else
+                HIP_TRY(launch_edge_update(P->g, P->order, um, P->L(), P->theta, P->edges, 0.0, 1.0, 0.0, nullptr,
+                                           P->partials, P->ctl));
+            P->tstop(h);
+            HIP_TRY(launch_finalize(s, P->partials, npe, ER_N, 1, 0, P->red, P->st, 0.0, 0, P->ctl));
+            // D^T at the first owned plane reads the new z of plane zb-1 (rank-1's last plane)
+            MVTV_TRY(C->begin());
+            if (rk < G - 1) MVTV_TRY(edge_plane_xfer(P->edges, last_owned / pl, rk + 1, true));
+            if (rk > 0) MVTV_TRY(edge_plane_xfer(P->edges, 0, rk - 1, false));
+            MVTV_TRY(C->end(s));
+            h = P->tstart(MVTV_K_GATHER);
+            const int hb = P->tstart_b(MVTV_K_GATHER4B);
+            int npg = P->grid;
+            if (P->e3d)
+                HIP_TRY(launch_gather3d(P->g, P->order, U_FROM_Z, s, P->edges, 0.0, P->ga, gn, gp, 1.0, P->partials,
+                                        &npg, P->ctl, P->g4));
+            else
+                HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, P->L(), P->edges, 0.0, P->ga, gn, gp, 1.0,
+                                      P->partials, P->ctl));
+            P->tstop(h);
+            P->tstop_b(hb);
+            HIP_TRY(launch_finalize(s, P->partials, npg, GR_N, 0, 0, P->red + ER_N, P->st, 0.0, 0, P->ctl));
+        }
+        // -- global sums, then every rank's identical decision
+        MVTV_TRY(C->allreduce_sum(P->red, ER_N + GR_N, s));
+        HIP_TRY(launch_admm_control(s, P->ctl, P->red));
+        // -- z halo for the next iteration's chunk-start recompute (fused): rank-1's last plane of z_new
+        if (fused) {
+            MVTV_TRY(C->begin());
+            if (rk < G - 1) MVTV_TRY(edge_plane_xfer(zn, last_owned / pl, rk + 1, true));
+            if (rk > 0) MVTV_TRY(edge_plane_xfer(zn, 0, rk - 1, false));
+            MVTV_TRY(C->end(s));
+        }
+        return MVTV_OK;
+    };
+
+    // batches of iterations between polls: a schedule that depends only on the (identical) decisions, so
+    // every rank enqueues the same collectives
+    const int limit = opts->fixed_iters > 0 ? opts->fixed_iters : max_counter + 1;
+    int target = opts->fixed_iters > 0 ? opts->fixed_iters : 16;
+    int enq = 0;
+    std::vector<size_t> mark;
+    for (;;) {
+        while (enq < target && enq < limit) {
+            mark.push_back(P->pending.size());
+            MVTV_TRY(enqueue(enq++));
+        }
+        HIP_TRY(hipMemcpyAsync(P->host_ctl, P->ctl, sizeof(AdmmCtl), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (c.done || enq >= limit) break;
+        target = enq + std::max(4, enq / 4);
+    }
+    const int it_done = c.it;
+    if (P->timing && it_done < int(mark.size()))
+        for (size_t e = mark[size_t(it_done)]; e < P->pending.size(); ++e) P->pending[e].kid = -1;
+    P->harvest();
+    if (it_done & 1) {
+        std::swap(P->guprev, P->gu);
+        if (fused) std::swap(P->edges, P->edges2);
+    }
+    P->edge_mode = it_done > 0 ? U_FROM_Z : U_EXPLICIT;
+    P->t_z = c.t_z;
+    P->c_state = c.c_prev;
+    P->rho = c.rho;
+    P->have_state = true;
+    P->u_default = false;
+    mvtv_admm_stats S{};
+    S.iters = it_done;
+    S.rho = c.rho;
+    S.r_norm = c.r_norm;
+    S.s_norm = c.s_norm;
+    S.eps_pri = c.eps_pri;
+    S.eps_dual = c.eps_dual;
+    S.theta_solver = MVTV_SOLVER_SPECTRAL;
+    S.status = c.status ? MVTV_MAXITER : MVTV_OK;
+    S.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = S;
+    return S.status == MVTV_OK ? MVTV_OK : MVTV_MAXITER;
+}

@@ -68,7 +68,19 @@ struct SpecArgs {
     uint32_t q_off;          // MID: global index of line 0 (slab-decomposed solve works on a line chunk)
     const int32_t* skip;     // != nullptr and *skip: return at once (preconditioner of a converged PCG)
     const AdmmCtl* ctl;      // asynchronous ADMM loop: sigma, ca = rho, cb = rho c_prev from the device
+    // slab decomposition: `out` (pk = 1) or `in` (pk = 2) is the all-to-all buffer of the distributed
+    // solve, packed as [rank s][owned plane z][line q mod chunk] with line q = the index over dims 0..p-2
+    // (plane size 2^pk_lpl, chunk 2^pk_lch lines per rank, pk_nz owned planes)
+    int32_t pk;
+    uint32_t pk_lpl, pk_lch, pk_nz;
 };
+
+// element offset in a packed all-to-all buffer of the element at offset i of the owned planes
+__device__ __forceinline__ uint32_t pack_index(const SpecArgs& a, uint32_t i) {
+    const uint32_t z = i >> a.pk_lpl, q = i & ((1u << a.pk_lpl) - 1u);
+    const uint32_t s = q >> a.pk_lch;
+    return ((s * a.pk_nz + z) << a.pk_lch) | (q & ((1u << a.pk_lch) - 1u));
+}
 
 enum SpecMode { SPEC_FWD = 0, SPEC_INV = 1, SPEC_MID = 2 };
 
@@ -542,17 +554,17 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
         if (D0) {
             if (va) {
                 const uint32_t g = gaddr(la, k);
-                v.x = __builtin_nontemporal_load(a.in + g);
+                v.x = __builtin_nontemporal_load(a.in + (a.pk == 2 ? pack_index(a, g) : g));
                 if (FORMB) v.x += ca * __builtin_nontemporal_load(a.ga + g) + cb * __builtin_nontemporal_load(a.gb + g);
             }
             if (vb) {
                 const uint32_t g = gaddr(lb, k);
-                v.y = __builtin_nontemporal_load(a.in + g);
+                v.y = __builtin_nontemporal_load(a.in + (a.pk == 2 ? pack_index(a, g) : g));
                 if (FORMB) v.y += ca * __builtin_nontemporal_load(a.ga + g) + cb * __builtin_nontemporal_load(a.gb + g);
             }
         } else if (va) {   // d > 0: lines la, lb are adjacent words (vb == va)
             const uint32_t g = gaddr(la, k);
-            v = ldnt2(a.in + g);
+            v = ldnt2(a.in + (a.pk == 2 ? pack_index(a, g) : g));
             if (FORMB) {
                 const double2 x1 = ldnt2(a.ga + g);
                 const double2 x2 = ldnt2(a.gb + g);
@@ -562,12 +574,13 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
         }
         return v;
     };
+    auto po = [&](uint32_t g) -> uint32_t { return a.pk == 1 ? pack_index(a, g) : g; };
     auto st2 = [&](uint32_t k, double2 v) {
         if (D0) {
-            if (va) __builtin_nontemporal_store(v.x, a.out + gaddr(la, k));
-            if (vb) __builtin_nontemporal_store(v.y, a.out + gaddr(lb, k));
+            if (va) __builtin_nontemporal_store(v.x, a.out + po(gaddr(la, k)));
+            if (vb) __builtin_nontemporal_store(v.y, a.out + po(gaddr(lb, k)));
         } else if (va) {
-            stnt2(a.out + gaddr(la, k), v);
+            stnt2(a.out + po(gaddr(la, k)), v);
         }
     };
 
@@ -583,7 +596,7 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
                 double2 xa = make_double2(0.0, 0.0), xb = make_double2(0.0, 0.0);
                 if (va) {
                     const uint32_t g = gaddr(la, uint32_t(2 * n));
-                    xa = ldnt2(a.in + g);
+                    xa = ldnt2(a.in + (a.pk == 2 ? pack_index(a, g) : g));
                     if (FORMB) {
                         const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
                         xa.x += ca * g1.x + cb * g2.x;
@@ -592,7 +605,7 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
                 }
                 if (vb) {
                     const uint32_t g = gaddr(lb, uint32_t(2 * n));
-                    xb = ldnt2(a.in + g);
+                    xb = ldnt2(a.in + (a.pk == 2 ? pack_index(a, g) : g));
                     if (FORMB) {
                         const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
                         xb.x += ca * g1.x + cb * g2.x;
@@ -682,8 +695,8 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
             for (int s4 = 0; s4 < 4; ++s4) {
                 const int n = j + s4 * TPL;
                 const double2 v0 = X[spec8::slot(n, cx)], v1 = X[spec8::slot(M - 1 - n, cx)];
-                if (va) stnt2(a.out + gaddr(la, uint32_t(2 * n)), make_double2(v0.x, v1.x));
-                if (vb) stnt2(a.out + gaddr(lb, uint32_t(2 * n)), make_double2(v0.y, v1.y));
+                if (va) stnt2(a.out + po(gaddr(la, uint32_t(2 * n))), make_double2(v0.x, v1.x));
+                if (vb) stnt2(a.out + po(gaddr(lb, uint32_t(2 * n))), make_double2(v0.y, v1.y));
             }
         } else {
             stages_from<L, R0, 1, true, true>(z, j, X, cx, tw);
@@ -750,8 +763,15 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
 
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
-                           double w0, const AdmmCtl* ctl, uint32_t q_off, double inv_n, const int32_t* skip) {
+                           double w0, const AdmmCtl* ctl, uint32_t q_off, double inv_n, const int32_t* skip,
+                           const DctPack* pack) {
     SpecArgs a{};
+    if (pack && pack->mode) {
+        a.pk = pack->mode;
+        a.pk_lpl = pack->lpl;
+        a.pk_lch = pack->lch;
+        a.pk_nz = pack->nz;
+    }
     a.ctl = ctl;
     a.skip = skip;
     a.q_off = q_off;
@@ -784,6 +804,7 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     while ((1u << a.L) < m) ++a.L;
     if ((1u << a.L) != m || m > 4096) return hipErrorInvalidValue;
     const bool formb = ga != nullptr;
+    if (a.pk && a.L < 3) return hipErrorInvalidValue;   // the packed layout is served by k_dct8 only
     if (a.L >= 3 && !probe_env("MVTV_DCT_LDS")) {
         static constexpr int tq8[13] = {0, 0, 0, 16, 16, 16, 16, 16, 16, 16, 8, 4, 2};
         int tq = tq8[a.L];
