@@ -83,3 +83,21 @@ def test_config4_fold_path_2048_vs_c_oracle(solver):
         assert np.max(np.abs(thetas[k] - th)) <= 1e-9 * np.max(np.abs(th)), k
         assert stats[k]["r_norm"] == pytest.approx(st["r_norm"], rel=1e-8)
         assert stats[k]["s_norm"] == pytest.approx(st["s_norm"], rel=1e-8)
+
+
+def test_config5_128_4d_eight_rank_decomposition():
+    """Config 5 at its shape: 128^4 slab-decomposed over 8 ranks (16 planes of dim 3 each), the ranks'
+    mvtv_slab_run loops on one GPU over the in-process loopback transport, against the one-GPU run:
+    2 fixed iterations, rho exact, theta to 1e-11 (only the order of the global sums differs)."""
+    from multivartv_amd import slab
+    m, lam, iters = [128, 128, 128, 128], 1.0, 2
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        P.state_set(np.full(y.size, y.mean()), None, lam / 5.0)
+        st = P.run(lam, fixed_iters=iters)
+        th, _, rho = P.state_get(want_u=False)
+    out, theta = slab.run_local_group(m, y, deltas, lam, 8, fixed_iters=iters)
+    assert all(o["iters"] == iters and o["rho"] == rho for o in out)
+    assert out[0]["r_norm"] == pytest.approx(st["r_norm"], rel=1e-9)
+    assert np.max(np.abs(theta - th)) <= 1e-11 * np.max(np.abs(th))
