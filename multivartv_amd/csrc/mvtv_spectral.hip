@@ -711,6 +711,205 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
     }
 }
 
+// =============================================================================================
+// Last dimension by a tridiagonal solve instead of DCT / divide / inverse DCT.
+//
+// After the forward transforms along dims 0..p-2, line q of the last dimension d carries the 1-D
+// operator c0(q) I + c1(q) T, T = D1^T D1 = tridiag(-1, [1, 2, ..., 2, 1], -1) (the Neumann
+// Laplacian the DCT along d would diagonalise: mu = c0 + c1 lam_d(k)). Solving it directly costs
+// ~6 flops per element against two length-m FFTs, a divide and the DCT pre/post twiddles, with the
+// same 2N words of HBM traffic; the pass stops being VALU/latency bound.
+//
+// Partitioned Thomas: a thread owns SEG consecutive rows of one line and eliminates them with the
+// left / right neighbours x[lo-1] = L, x[hi+1] = R kept symbolic: x_i = G_i + H_i L + K_i R. The
+// line's Toeplitz interior makes 1/den_i, e_i, H_i, K_i the same for every segment (line constants,
+// built once per workgroup in LDS); the Neumann ends are the mirror conditions x[-1] = x[0],
+// x[m] = x[m-1]. One thread per line then solves the 2 x NSEG interface system (u_j = x at a
+// segment's first row, v_j at its last) by block elimination, and every thread finishes its rows.
+// The result is the exact solve (the system is strictly diagonally dominant: c0 > 0, c1 >= 0),
+// scaled by inv_n * m_d (the normalisation of the transforms along the other dims).
+namespace tri {
+constexpr int TQ = 16;    // lines per workgroup: one 128-B row per position (d > 0)
+template <int L, int SEG>
+struct Shape {
+    static constexpr int M = 1 << L;
+    static constexpr int NSEG = M / SEG;   // segments (threads) per line
+    static constexpr int NT = TQ * NSEG;
+};
+}  // namespace tri
+
+template <int L, int SEG>
+__global__ __launch_bounds__((tri::Shape<L, SEG>::NT)) void k_tri(const SpecArgs a) {
+    using S = tri::Shape<L, SEG>;
+    constexpr int TQ = tri::TQ, NSEG = S::NSEG;
+    double sigma = a.sigma;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+    }
+    __shared__ double t_id[SEG][TQ], t_e[SEG][TQ], t_h[SEG][TQ], t_k[SEG][TQ];   // line constants
+    __shared__ double s_a[TQ];                                                    // -c1 per line
+    __shared__ double s_u[NSEG][TQ], s_v[NSEG][TQ], s_bu[NSEG][TQ], s_bv[NSEG][TQ];
+    const int t = threadIdx.x, c = t % TQ, sj = t / TQ;
+    const uint32_t q0 = blockIdx.x * uint32_t(TQ);
+    const uint32_t q = q0 + uint32_t(c);
+    const bool valid = q < a.nlines;
+    const uint32_t base = (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (uint32_t(sj * SEG) << a.ls);
+
+    double g[SEG];
+#pragma unroll
+    for (int i = 0; i < SEG; ++i) g[i] = valid ? __builtin_nontemporal_load(a.in + base + (uint32_t(i) << a.ls)) : 0.0;
+
+    if (t < TQ) {
+        // c0 + c1 T along d for this line (q indexes dims 0..p-2 column-major, as k_dct8's MID)
+        const uint32_t ql = a.q_off + (valid ? q : q0);
+        double lamv[kMaxDims] = {0, 0, 0, 0};
+        uint32_t rest = ql;
+        const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
+        for (int jj = 0; jj < a.p; ++jj) {
+            if (jj == a.d) continue;
+            const uint32_t qq = (jj < jlast) ? a.fd[jj].div(rest) : 0u;
+            lamv[jj] = a.lam[a.lam_off[jj] + (rest - qq * a.m[jj])];
+            rest = qq;
+        }
+        double c0 = a.w0, c1 = 0.0;
+        for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
+            if (a.cS[Sm] == 0.0) continue;
+            double prod = sigma * a.cS[Sm];
+            for (int jj = 0; jj < a.p; ++jj)
+                if (jj != a.d && ((Sm >> jj) & 1)) prod *= lamv[jj];
+            if ((Sm >> a.d) & 1) c1 += prod;
+            else c0 += prod;
+        }
+        // Thomas on one interior segment: den_i = B - A e_{i-1}, e_i = A / den_i, h_i = -A h_{i-1} / den_i
+        const double A = -c1, B = c0 + 2.0 * c1;
+        double e = 0.0, h = 1.0;
+#pragma unroll 1
+        for (int i = 0; i < SEG; ++i) {
+            const double id = 1.0 / (B - A * e);
+            e = A * id;
+            h = -A * h * id;
+            t_id[i][c] = id;
+            t_e[i][c] = e;
+            t_h[i][c] = h;
+        }
+        // back substitution of the L / R responses: H_i = h_i - e_i H_{i+1}, K_i = -e_i K_{i+1}
+        double H = t_h[SEG - 1][c], K = -t_e[SEG - 1][c];
+        t_k[SEG - 1][c] = K;
+#pragma unroll 1
+        for (int i = SEG - 2; i >= 0; --i) {
+            const double ei = t_e[i][c];
+            H = t_h[i][c] - ei * H;
+            K = -ei * K;
+            t_h[i][c] = H;
+            t_k[i][c] = K;
+        }
+        s_a[c] = A;
+    }
+    __syncthreads();
+
+    // this segment with L = R = 0: forward elimination, then back substitution
+    {
+        const double A = s_a[c];
+        g[0] *= t_id[0][c];
+#pragma unroll
+        for (int i = 1; i < SEG; ++i) g[i] = (g[i] - A * g[i - 1]) * t_id[i][c];
+#pragma unroll
+        for (int i = SEG - 2; i >= 0; --i) g[i] -= t_e[i][c] * g[i + 1];
+        s_u[sj][c] = g[0];
+        s_v[sj][c] = g[SEG - 1];
+    }
+    __syncthreads();
+
+    if (t < TQ) {
+        // interface system: u_j = G0_j + H0 L_j + K0 R_j, v_j = G1_j + H1 L_j + K1 R_j with
+        // L_j = v_{j-1} (L_0 = u_0), R_j = u_{j+1} (R_last = v_last). Eliminate forward to
+        // z_j = (au, av) + (bu, bv) u_{j+1}, solve the last 2 x 2 block, substitute back.
+        const double H0 = t_h[0][c], K0 = t_k[0][c], H1 = t_h[SEG - 1][c], K1 = t_k[SEG - 1][c];
+        double av = 0.0, bv = 0.0;   // v_{j-1} = av + bv u_j
+#pragma unroll 1
+        for (int j = 0; j < NSEG - 1; ++j) {
+            const double g0 = s_u[j][c], g1 = s_v[j][c];
+            double au, bu;
+            if (j == 0) {
+                const double id = 1.0 / (1.0 - H0);
+                au = g0 * id;
+                bu = K0 * id;
+                av = g1 + H1 * au;
+                bv = K1 + H1 * bu;
+            } else {
+                const double id = 1.0 / (1.0 - H0 * bv);
+                au = (g0 + H0 * av) * id;
+                bu = K0 * id;
+                const double nav = g1 + H1 * av + H1 * bv * au;
+                bv = K1 + H1 * bv * bu;
+                av = nav;
+            }
+            s_u[j][c] = au;
+            s_bu[j][c] = bu;
+            s_v[j][c] = av;
+            s_bv[j][c] = bv;
+        }
+        constexpr int J = NSEG - 1;
+        const double a11 = 1.0 - H0 * bv, a12 = -K0, a21 = -H1 * bv, a22 = 1.0 - K1;
+        const double b1 = s_u[J][c] + H0 * av, b2 = s_v[J][c] + H1 * av;
+        const double idet = 1.0 / (a11 * a22 - a12 * a21);
+        double u = (b1 * a22 - a12 * b2) * idet;
+        s_u[J][c] = u;
+        s_v[J][c] = (a11 * b2 - a21 * b1) * idet;
+#pragma unroll 1
+        for (int j = J - 1; j >= 0; --j) {
+            const double un = u;
+            u = s_u[j][c] + s_bu[j][c] * un;
+            s_v[j][c] = s_v[j][c] + s_bv[j][c] * un;
+            s_u[j][c] = u;
+        }
+    }
+    __syncthreads();
+
+    const double Lj = sj == 0 ? s_u[0][c] : s_v[sj - 1][c];
+    const double Rj = sj == NSEG - 1 ? s_v[NSEG - 1][c] : s_u[sj + 1][c];
+    const double sc = a.inv_n * double(S::M);
+    if (!valid) return;
+#pragma unroll
+    for (int i = 0; i < SEG; ++i)
+        __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + (uint32_t(i) << a.ls));
+}
+
+// k_tri serves the last-dimension pass when the lines are long enough for >= 4 segments, short
+// enough for <= 64 (one workgroup <= 1024 threads), 16 lines make a 128-B row (stride >= 16) and
+// there are enough line tiles to fill the chip (the 2-D configs keep the FFT pass)
+static bool tri_ok(const SpecArgs& a, int mode, bool formb) {
+    if (mode != SPEC_MID || a.d == 0 || formb || a.pk) return false;
+    if (a.L < 6 || a.L > 10 || a.stride < uint32_t(tri::TQ)) return false;
+    if (a.nlines / uint32_t(tri::TQ) < 256u) return false;
+    const char* e = probe_env("MVTV_DCT_TRI");
+    return !e || std::atoi(e) != 0;
+}
+
+template <int SEG>
+static void launch_tri_seg(SpecArgs& a, hipStream_t s) {
+    const dim3 grid((a.nlines + uint32_t(tri::TQ) - 1) / uint32_t(tri::TQ));
+    switch (a.L) {
+        case 6: klaunch(k_tri<6, SEG>, grid, dim3(tri::Shape<6, SEG>::NT), 0, s, a); break;
+        case 7: klaunch(k_tri<7, SEG>, grid, dim3(tri::Shape<7, SEG>::NT), 0, s, a); break;
+        case 8: klaunch(k_tri<8, SEG>, grid, dim3(tri::Shape<8, SEG>::NT), 0, s, a); break;
+        case 9: klaunch(k_tri<9, SEG>, grid, dim3(tri::Shape<9, SEG>::NT), 0, s, a); break;
+        case 10: klaunch(k_tri<10, SEG>, grid, dim3(tri::Shape<10, SEG>::NT), 0, s, a); break;
+    }
+}
+
+static void launch_tri(SpecArgs& a, hipStream_t s) {
+    a.tq = tri::TQ;
+    static const int seg = [] {
+        const char* e = probe_env("MVTV_TRI_SEG");
+        return e && std::atoi(e) == 32 ? 32 : 16;
+    }();
+    if (seg == 32) launch_tri_seg<32>(a, s);
+    else launch_tri_seg<16>(a, s);
+}
+
 // ------------------------------------------------------------------------------ launcher
 // strided (d > 0) passes of long lines: twice the default tile (one 148-KB workgroup per CU) so a
 // line position is a 64-B (L = 11) / 128-B (L = 10) row instead of 32 / 64 B. 2-D 2048^2: the two
@@ -805,6 +1004,10 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     if ((1u << a.L) != m || m > 4096) return hipErrorInvalidValue;
     const bool formb = ga != nullptr;
     if (a.pk && a.L < 3) return hipErrorInvalidValue;   // the packed layout is served by k_dct8 only
+    if (tri_ok(a, mode, formb)) {
+        launch_tri(a, s);
+        return hipGetLastError();
+    }
     if (a.L >= 3 && !probe_env("MVTV_DCT_LDS")) {
         static constexpr int tq8[13] = {0, 0, 0, 16, 16, 16, 16, 16, 16, 16, 8, 4, 2};
         int tq = tq8[a.L];

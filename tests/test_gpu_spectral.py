@@ -35,7 +35,10 @@ CASES = [([2], None, "cpp", False), ([8], None, "cpp", False), ([1024], None, "p
          ([32, 32], None, "py", False), ([8, 8, 8], [0.5, 0.25, 0.125], "cpp", False),
          ([16, 16, 16], [0.2, 0.3, 0.4], "cpp", True), ([8, 8, 8], [0.5, 0.25, 0.125], "py", False),
          ([4, 4, 4, 4], [0.5, 0.25, 0.125, 0.3], "cpp", False), ([4, 4, 4, 4], None, "py", False),
-         ([8, 8, 8, 8], [0.1, 0.2, 0.3, 0.4], "cpp", False)]
+         ([8, 8, 8, 8], [0.1, 0.2, 0.3, 0.4], "cpp", False),
+         # >= 4096 lines of >= 64 points along the last dim: the tridiagonal last-dimension pass (k_tri)
+         # (3-D and 4-D meshes large enough for it are checked by residual and against PCG below)
+         ([4096, 64], [0.3, 0.7], "cpp", False), ([4096, 128], None, "py", False)]
 
 
 def _problem(m, deltas, order, unit, seed=0):
