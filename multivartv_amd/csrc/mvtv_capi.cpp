@@ -128,6 +128,7 @@ void free_all(mvtv_problem* P) {
     if (P->host_ctl) (void)hipHostFree(P->host_ctl);
     for (double* t : {P->spec.tw, P->spec.twq, P->spec.lam})
         if (t) (void)hipFree(t);
+    if (P->spec.perm) (void)hipFree(P->spec.perm);
     P->spec = SpecPlan{};
     if (P->host_red) (void)hipHostFree(P->host_red);
     for (auto& pd : P->pending) {
@@ -270,6 +271,7 @@ bool spectral_ok(const mvtv_problem* P) { return P->spec_mesh && P->wmode == W_I
 // Device tables of the spectral solve. Twiddles and eigenvalues are evaluated in long double.
 mvtv_status spectral_plan(mvtv_problem* P) {
     std::vector<double> tw, twq, lam;
+    std::vector<uint32_t> perm;
     SpecPlan& sp = P->spec;
     const long double pi = 3.141592653589793238462643383279502884L;
     for (int j = 0; j < P->g.p; ++j) {
@@ -289,6 +291,23 @@ mvtv_status spectral_plan(mvtv_problem* P) {
             const long double sn = sinl(pi * k / (2.0L * m));
             lam.push_back(double(4.0L * sn * sn));
         }
+        // k_dctg's input order: sample k goes to Makhoul position n (x[2n], x[2(m-1-n)+1]) at its
+        // digit-reversed place for the radix plan (n = sum of digits d_s, most significant first in
+        // stage order reversed; position = sum d_s prod_{u<s} rad[u])
+        int rad[8], nrad = 0;
+        const bool planned = dct_radix_plan(m, rad, &nrad);
+        for (uint32_t k = 0; k < m; ++k) {
+            uint32_t n = (k & 1u) ? m - 1u - (k >> 1) : (k >> 1), pos = 0;
+            if (planned) {
+                for (int st = nrad - 1; st >= 0; --st) {
+                    uint32_t mul = 1;
+                    for (int u = 0; u < st; ++u) mul *= uint32_t(rad[u]);
+                    pos += (n % uint32_t(rad[st])) * mul;
+                    n /= uint32_t(rad[st]);
+                }
+            }
+            perm.push_back(pos);
+        }
     }
     auto up = [&](double** dst, const std::vector<double>& v) -> mvtv_status {
         MVTV_TRY(alloc(dst, v.size()));
@@ -298,6 +317,8 @@ mvtv_status spectral_plan(mvtv_problem* P) {
     MVTV_TRY(up(&sp.tw, tw));
     MVTV_TRY(up(&sp.twq, twq));
     MVTV_TRY(up(&sp.lam, lam));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&sp.perm), perm.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(sp.perm, perm.data(), perm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     return MVTV_OK;
 }
 
@@ -603,11 +624,14 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
         return s;
     }
     P->host_st = reinterpret_cast<PcgState*>(P->host_red + 16);
-    P->spec_mesh = true;
+    P->spec_mesh = P->spec_pow2 = true;
     for (int j = 0; j < p; ++j) {
         const uint32_t mj = uint32_t(mg[j]);
-        if ((mj & (mj - 1)) != 0 || mj > 4096) P->spec_mesh = false;
+        int rad[8], nrad = 0;
+        if (mj > 4096 || !dct_radix_plan(mj, rad, &nrad)) P->spec_mesh = false;
+        if ((mj & (mj - 1)) != 0) P->spec_pow2 = false;
     }
+    if (!P->spec_mesh) P->spec_pow2 = false;
     if (P->spec_mesh) s = spectral_plan(P);
     P->e3d = edge3d_ok(g);
     if (s == MVTV_OK && P->e3d && g.p == 4 && gather4_ok(g)) s = alloc(&P->g4, 4 * size_t(N));
@@ -737,12 +761,12 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     if (o.theta_solver < MVTV_SOLVER_AUTO || o.theta_solver > MVTV_SOLVER_PCG_SPECTRAL)
         return fail(MVTV_BAD_ARG, "theta_solver");
     if (o.theta_solver == MVTV_SOLVER_SPECTRAL && !spectral_ok(P))
-        return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and power-of-two m_j <= 4096");
+        return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and every m_j <= 4096 a product of 2, 3, 5, 7");
     if (o.theta_solver == MVTV_SOLVER_PCG_SPECTRAL && (!P->spec_mesh || P->wmode == W_NONE))
-        return fail(MVTV_BAD_ARG, "spectral preconditioner needs power-of-two m_j <= 4096");
+        return fail(MVTV_BAD_ARG, "spectral preconditioner needs every m_j <= 4096 a product of 2, 3, 5, 7");
     const bool spectral = o.theta_solver == MVTV_SOLVER_SPECTRAL ||
                           (o.theta_solver == MVTV_SOLVER_AUTO && spectral_ok(P));
-    // AUTO with W != I on a power-of-two mesh: PCG with the spectral preconditioner (K an order of magnitude
+    // AUTO with W != I on a spectral mesh: PCG with the spectral preconditioner (K an order of magnitude
     // below Jacobi's once sigma D^T D dominates); other meshes: Jacobi-PCG
     const bool pcg_spec = o.theta_solver == MVTV_SOLVER_PCG_SPECTRAL ||
                           (o.theta_solver == MVTV_SOLVER_AUTO && !spectral && P->spec_mesh && P->wmode != W_NONE &&
@@ -1485,7 +1509,7 @@ mvtv_status mvtv_lambda_max_cpp(mvtv_problem* P, double* out, int32_t* iters) {
 
 mvtv_status mvtv_solve_spectral(mvtv_problem* P, double sigma, const double* b, double* x_out) {
     if (!P || !b || !x_out) return fail(MVTV_BAD_ARG, "null argument");
-    if (!spectral_ok(P)) return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and power-of-two m_j <= 4096");
+    if (!spectral_ok(P)) return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and every m_j <= 4096 a product of 2, 3, 5, 7");
     DeviceGuard dg(P->device);
     double* dx = nullptr;
     MVTV_TRY(alloc(&dx, P->g.N));

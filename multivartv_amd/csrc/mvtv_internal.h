@@ -229,6 +229,7 @@ struct SpecPlan {
     double* tw = nullptr;     // per dim: m_j complex FFT twiddles e^{-2 pi i k/m_j}
     double* twq = nullptr;    // per dim: m_j complex twiddles e^{-i pi k/(2 m_j)}
     double* lam = nullptr;    // per dim: m_j eigenvalues 4 sin^2(pi k/(2 m_j)) of the Neumann Laplacian
+    uint32_t* perm = nullptr; // per dim (at lam_off): position of sample k in the mixed-radix FFT's input order
     uint32_t tw_off[kMaxDims] = {0, 0, 0, 0}, twq_off[kMaxDims] = {0, 0, 0, 0}, lam_off[kMaxDims] = {0, 0, 0, 0};
 };
 // The slab-decomposed solve's all-to-all buffer layout (mode 1: the pass writes `out` packed, 2: it
@@ -237,6 +238,8 @@ struct DctPack {
     int32_t mode = 0;
     uint32_t lpl = 0, lch = 0, nz = 0;
 };
+// radices (8, 4, 2, 3, 5, 7 in stage order) of a line length m = 2^a 3^b 5^c 7^d; false for any other m
+bool dct_radix_plan(uint32_t m, int* rad, int* nrad);
 // mode 0 forward DCT-II, 1 inverse (DCT-III, unnormalised), 2 forward + divide by mu * N + inverse;
 // ga != nullptr forms the input as in + ca*ga + cb*gb. In place (in == out) is allowed.
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,

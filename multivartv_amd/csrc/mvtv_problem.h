@@ -79,7 +79,8 @@ struct mvtv_problem {
     double* host_red = nullptr;   // pinned: reductions + PcgState mirror
     PcgState* host_st = nullptr;
     SpecPlan spec;                // spectral theta-solve tables (allocated when the mesh allows it)
-    bool spec_mesh = false;       // every m_j a power of two <= 4096
+    bool spec_mesh = false;       // every m_j <= 4096 a product of 2, 3, 5, 7 (spectral solve)
+    bool spec_pow2 = false;       // ... and a power of two (slab decomposition, k_dct8 / k_tri passes)
     bool e3d = false;             // z-marching 3-D edge kernels
     bool f3d = false;             // fused 3-D edge update + gather (needs the second edge buffer)
     double* edges2 = nullptr;     // ping-pong partner of edges for the fused kernel

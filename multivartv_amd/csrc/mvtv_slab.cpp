@@ -396,7 +396,7 @@ extern "C" mvtv_status mvtv_slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_a
     if (!P || !C || !opts) return fail(MVTV_BAD_ARG, "null argument");
     if (!P->slab) return fail(MVTV_BAD_ARG, "not a slab problem (mvtv_problem_create_slab)");
     if (opts->variant != MVTV_VARIANT_RCPP) return fail(MVTV_BAD_ARG, "the slab loop runs variant B");
-    if (P->wmode != W_IDENTITY || !P->spec_mesh) return fail(MVTV_BAD_ARG, "slab loop: W = I, power-of-two m_j <= 4096");
+    if (P->wmode != W_IDENTITY || !P->spec_pow2) return fail(MVTV_BAD_ARG, "slab loop: W = I, power-of-two m_j <= 4096");
     if (!(lambda >= 0.0) || !(rho0 > 0.0)) return fail(MVTV_BAD_ARG, "lambda >= 0 and rho0 > 0");
     const auto t0 = std::chrono::steady_clock::now();
     DeviceGuard dg(P->device);

@@ -73,6 +73,13 @@ struct SpecArgs {
     // (plane size 2^pk_lpl, chunk 2^pk_lch lines per rank, pk_nz owned planes)
     int32_t pk;
     uint32_t pk_lpl, pk_lch, pk_nz;
+    // mixed-radix lengths (k_dctg): the FFT's radices in stage order, division by the line stride
+    int32_t nrad;
+    int32_t rad[8];
+    FastDiv fds;              // division by the line stride
+    FastDiv fm;               // division by m
+    FastDiv fper[8], fL[8];   // stage s: butterflies per line (m / rad[s]) and the span before it
+    const uint32_t* perm;     // position of sample k in the digit-reversed Makhoul order (this dim)
 };
 
 // element offset in a packed all-to-all buffer of the element at offset i of the owned planes
@@ -712,6 +719,312 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
 }
 
 // =============================================================================================
+// Mixed-radix lengths: m = 2^a 3^b 5^c 7^d <= 4096 that is not a power of two (meshes such as
+// 24 x 40, 100^3 or 1000^2). Same Makhoul pairing and pass structure as k_dct8, with the complex
+// FFT of length m run in LDS as in-place Cooley-Tukey stages of radix 8, 4, 2, 3, 5, 7: decimation
+// in time on input stored at digit-reversed positions (forward), decimation in frequency leaving
+// digit-reversed output (inverse), so both permutations fold into the load / store index as the
+// bit reversal does for k_dct. Line addresses take a general stride (FastDiv).
+namespace dctg {
+constexpr int NT = 512;   // threads per workgroup: 16 lines of <= 512 points (two workgroups per CU)
+// cos / sin (2 pi k / R), k < R
+__device__ __constant__ const double c3[3] = {1.0, -0.5, -0.5};
+__device__ __constant__ const double s3[3] = {0.0, 0.86602540378443864676, -0.86602540378443864676};
+__device__ __constant__ const double c5[5] = {1.0, 0.30901699437494742410, -0.80901699437494742410,
+                                             -0.80901699437494742410, 0.30901699437494742410};
+__device__ __constant__ const double s5[5] = {0.0, 0.95105651629515357212, 0.58778525229247312917,
+                                             -0.58778525229247312917, -0.95105651629515357212};
+__device__ __constant__ const double c7[7] = {1.0, 0.62348980185873353053, -0.22252093395631440429,
+                                             -0.90096886790241912624, -0.90096886790241912624,
+                                             -0.22252093395631440429, 0.62348980185873353053};
+__device__ __constant__ const double s7[7] = {0.0, 0.78183148246802980871, 0.97492791218182360702,
+                                             0.43388373911755812048, -0.43388373911755812048,
+                                             -0.97492791218182360702, -0.78183148246802980871};
+}  // namespace dctg
+
+// natural-order DFT of z[0..R-1] for R in {3, 5, 7}
+template <int R, bool INV>
+__device__ __forceinline__ void dft_odd(double2* z) {
+    const double* C = R == 3 ? dctg::c3 : (R == 5 ? dctg::c5 : dctg::c7);
+    const double* Sn = R == 3 ? dctg::s3 : (R == 5 ? dctg::s5 : dctg::s7);
+    double2 y[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        double2 acc = z[0];
+#pragma unroll
+        for (int q = 1; q < R; ++q) {
+            const int k = (q * r) % R;
+            const double c = C[k], s = INV ? Sn[k] : -Sn[k];   // e^{-+ i 2 pi k / R}
+            acc.x += z[q].x * c - z[q].y * s;
+            acc.y += z[q].x * s + z[q].y * c;
+        }
+        y[r] = acc;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) z[r] = y[r];
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void dft_any(double2* z) {
+    if constexpr (R == 2 || R == 4 || R == 8) dft_r<R, INV>(z);
+    else dft_odd<R, INV>(z);
+}
+
+// One in-place stage over ncl lines of pitch LP: butterflies (block b of L1 = L R, column j < L) on
+// elements b L1 + j + r L. DIT: twiddle w^{r j m / L1} then DFT; DIF: DFT then twiddle.
+template <int R, bool DIF, bool INV>
+__device__ __forceinline__ void mr_stage(double2* __restrict__ buf, const double2* __restrict__ tw, int ncl, int m,
+                                         int LP, int L, const FastDiv& fper, const FastDiv& fL) {
+    const int L1 = L * R, per = m / R, nb = ncl * per, tstep = m / L1;
+    for (int t = threadIdx.x; t < nb; t += dctg::NT) {
+        const int line = int(fper.div(uint32_t(t))), bi = t - line * per;
+        const int b = int(fL.div(uint32_t(bi))), j = bi - b * L;
+        double2* x = buf + line * LP + b * L1 + j;
+        double2 z[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) z[r] = x[r * L];
+        if (!DIF) {
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                const double2 w = tw[r * j * tstep];   // r j m / L1 < m
+                z[r] = cmul(z[r], INV ? cconj(w) : w);
+            }
+        }
+        dft_any<R, INV>(z);
+        if (DIF) {
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                const double2 w = tw[r * j * tstep];
+                z[r] = cmul(z[r], INV ? cconj(w) : w);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r * L] = z[r];
+    }
+    __syncthreads();
+}
+
+template <bool DIF, bool INV>
+__device__ __forceinline__ void mr_fft(double2* buf, const double2* tw, int ncl, int m, int LP, const SpecArgs& a) {
+    auto stage = [&](int s, int L) {
+        switch (a.rad[s]) {
+            case 2: mr_stage<2, DIF, INV>(buf, tw, ncl, m, LP, L, a.fper[s], a.fL[s]); break;
+            case 3: mr_stage<3, DIF, INV>(buf, tw, ncl, m, LP, L, a.fper[s], a.fL[s]); break;
+            case 4: mr_stage<4, DIF, INV>(buf, tw, ncl, m, LP, L, a.fper[s], a.fL[s]); break;
+            case 5: mr_stage<5, DIF, INV>(buf, tw, ncl, m, LP, L, a.fper[s], a.fL[s]); break;
+            case 7: mr_stage<7, DIF, INV>(buf, tw, ncl, m, LP, L, a.fper[s], a.fL[s]); break;
+            default: mr_stage<8, DIF, INV>(buf, tw, ncl, m, LP, L, a.fper[s], a.fL[s]); break;
+        }
+    };
+    if (!DIF) {
+        for (int s = 0, L = 1; s < a.nrad; ++s) {
+            stage(s, L);
+            L *= a.rad[s];
+        }
+    } else {
+        for (int s = a.nrad - 1, L1 = m; s >= 0; --s) {
+            const int L = L1 / a.rad[s];
+            stage(s, L);
+            L1 = L;
+        }
+    }
+}
+
+template <int MODE, bool D0, bool FORMB>
+__global__ __launch_bounds__(dctg::NT) __attribute__((amdgpu_waves_per_eu(4))) void k_dctg(const SpecArgs a) {
+    double sigma = a.sigma, ca = a.ca, cb = a.cb;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+        ca = a.ctl->rho;
+        cb = a.ctl->rho * a.ctl->c_prev;
+    }
+    extern __shared__ double2 buf[];   // tq / 2 lines of m + PAD complex slots (launch-time size)
+    __shared__ double lc0[16], lc1[16];
+    const int m = int(a.m[a.d]);
+    const int tq = a.tq, ncl = tq >> 1;
+    const int LP = m + spec::PAD;
+    const uint32_t q0 = blockIdx.x * uint32_t(tq);
+
+    if (MODE == SPEC_MID && threadIdx.x < uint32_t(tq)) {
+        const uint32_t q = a.q_off + q0 + threadIdx.x;
+        double lamv[kMaxDims] = {0, 0, 0, 0};
+        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
+        const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
+        for (int j = 0; j < a.p; ++j) {
+            if (j == a.d) continue;
+            const uint32_t qq = (j < jlast) ? a.fd[j].div(rest) : 0u;
+            lamv[j] = a.lam[a.lam_off[j] + (rest - qq * a.m[j])];
+            rest = qq;
+        }
+        double c0 = a.w0, c1 = 0.0;
+        for (int S = 1; S < (1 << a.p); ++S) {
+            if (a.cS[S] == 0.0) continue;
+            double prod = sigma * a.cS[S];
+            for (int j = 0; j < a.p; ++j)
+                if (j != a.d && ((S >> j) & 1)) prod *= lamv[j];
+            if ((S >> a.d) & 1) c1 += prod;
+            else c0 += prod;
+        }
+        lc0[threadIdx.x] = c0;
+        lc1[threadIdx.x] = c1;
+    }
+
+    // global offset of (local line ql, position k): line q = (block q / stride, offset q % stride)
+    auto gaddr = [&](uint32_t ql, uint32_t k) -> uint32_t {
+        const uint32_t q = q0 + ql;
+        if (D0) return q * uint32_t(m) + k;
+        const uint32_t hi = a.fds.div(q);
+        return (q - hi * a.stride) + hi * a.stride * uint32_t(m) + k * a.stride;
+    };
+    const int ltq = __ffs(tq) - 1;   // tq is a power of two
+
+    double* bw = reinterpret_cast<double*>(buf);
+    const int total = tq * m;
+    for (int e = threadIdx.x; e < total; e += dctg::NT) {
+        const int ql = D0 ? int(a.fm.div(uint32_t(e))) : (e & (tq - 1));
+        const int k = D0 ? e - ql * m : (e >> ltq);
+        double v = 0.0;
+        if (q0 + uint32_t(ql) < a.nlines) {
+            const uint32_t gi = gaddr(uint32_t(ql), uint32_t(k));
+            v = __builtin_nontemporal_load(a.in + gi);
+            if (FORMB) v += ca * __builtin_nontemporal_load(a.ga + gi) + cb * __builtin_nontemporal_load(a.gb + gi);
+        }
+        const int pos = MODE == SPEC_INV ? k : int(a.perm[k]);
+        bw[2 * ((ql >> 1) * LP + pos) + (ql & 1)] = v;
+    }
+    __syncthreads();
+
+    const double2* tw = a.tw;
+    if (MODE != SPEC_INV) mr_fft<false, false>(buf, tw, ncl, m, LP, a);
+
+    // spectrum <-> DCT coefficients over the pairs (k, m-k); k = 0 pairs with itself, and so does
+    // k = m/2 for even m (handled with k = 0)
+    {
+        const int half = m >> 1, npl = (m & 1) ? half + 1 : half;
+        const int npairs = ncl * npl;
+        for (int t = threadIdx.x; t < npairs; t += dctg::NT) {
+            const int line = t / npl, k = t - line * npl;
+            double2* x = buf + line * LP;
+            const bool self = k == 0;
+            const bool mid = self && !(m & 1);   // also the self pair m/2
+            const int ka = k, kb = self ? half : m - k;
+            double2 Xk, Xmk = make_double2(0.0, 0.0);
+            if (MODE != SPEC_INV) {
+                const double2 Z1 = x[ka], q1 = a.twq[ka];
+                if (self) {
+                    Xk = make_double2(q1.x * Z1.x, q1.x * Z1.y);
+                    if (mid) {
+                        const double2 Z2 = x[kb], q2 = a.twq[kb];
+                        Xmk = make_double2(q2.x * Z2.x, q2.x * Z2.y);
+                    }
+                } else {
+                    const double2 Z2 = x[kb], q2 = a.twq[kb];
+                    const double2 Ap = make_double2(0.5 * (Z1.x + Z2.x), 0.5 * (Z1.y - Z2.y));
+                    const double2 Bp = make_double2(0.5 * (Z1.y + Z2.y), -0.5 * (Z1.x - Z2.x));
+                    Xk = make_double2(q1.x * Ap.x - q1.y * Ap.y, q1.x * Bp.x - q1.y * Bp.y);
+                    Xmk = make_double2(q2.x * Ap.x + q2.y * Ap.y, q2.x * Bp.x + q2.y * Bp.y);
+                }
+            } else {
+                Xk = x[ka];
+                if (!self || mid) Xmk = x[kb];
+            }
+            if (MODE == SPEC_MID) {
+                const double* lamd = a.lam + a.lam_off[a.d];
+                const int l0 = 2 * line, l1 = 2 * line + 1;
+                const double la = lamd[ka];
+                Xk.x *= a.inv_n / (lc0[l0] + lc1[l0] * la);
+                Xk.y *= a.inv_n / (lc0[l1] + lc1[l1] * la);
+                if (!self || mid) {
+                    const double lb = lamd[kb];
+                    Xmk.x *= a.inv_n / (lc0[l0] + lc1[l0] * lb);
+                    Xmk.y *= a.inv_n / (lc0[l1] + lc1[l1] * lb);
+                }
+            }
+            if (MODE == SPEC_FWD) {
+                x[ka] = Xk;
+                if (!self || mid) x[kb] = Xmk;
+                continue;
+            }
+            const double2 q2 = cconj(a.twq[kb]);
+            if (self) {
+                x[0] = Xk;   // X[m] = 0: V[0] = X[0]
+                if (mid) {
+                    const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xmk.x));
+                    const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xmk.y));
+                    x[half] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+                }
+            } else {
+                const double2 q1 = cconj(a.twq[ka]);
+                const double2 va1 = cmul(q1, make_double2(Xk.x, -Xmk.x));
+                const double2 vb1 = cmul(q1, make_double2(Xk.y, -Xmk.y));
+                const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xk.x));
+                const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xk.y));
+                x[ka] = make_double2(va1.x - vb1.y, va1.y + vb1.x);
+                x[kb] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+            }
+        }
+        __syncthreads();
+    }
+
+    if (MODE != SPEC_FWD) mr_fft<true, true>(buf, tw, ncl, m, LP, a);
+
+    for (int e = threadIdx.x; e < total; e += dctg::NT) {
+        const int ql = D0 ? int(a.fm.div(uint32_t(e))) : (e & (tq - 1));
+        const int k = D0 ? e - ql * m : (e >> ltq);
+        if (q0 + uint32_t(ql) >= a.nlines) continue;
+        const int pos = MODE == SPEC_FWD ? k : int(a.perm[k]);
+        __builtin_nontemporal_store(bw[2 * ((ql >> 1) * LP + pos) + (ql & 1)], a.out + gaddr(uint32_t(ql), uint32_t(k)));
+    }
+}
+
+static void launch_dctg(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
+    const dim3 grid((a.nlines + uint32_t(a.tq) - 1) / uint32_t(a.tq)), block(dctg::NT);
+    const size_t smem = size_t(a.tq / 2) * (a.m[a.d] + spec::PAD) * sizeof(double2);
+    // (m = 4096 over a general stride: one complex line of 4097 slots is just above 64 KB)
+#define MVTV_DCTG(MODE, D0, FB)                                                                               \
+    do {                                                                                                       \
+        if (smem > 65536)                                                                                      \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dctg<MODE, D0, FB>),                    \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(smem));                  \
+        klaunch(k_dctg<MODE, D0, FB>, grid, block, uint32_t(smem), s, a);                                      \
+    } while (0)
+    if (mode == SPEC_FWD) {
+        if (d0) {
+            if (formb) MVTV_DCTG(SPEC_FWD, true, true);
+            else MVTV_DCTG(SPEC_FWD, true, false);
+        } else {
+            MVTV_DCTG(SPEC_FWD, false, false);
+        }
+    } else if (mode == SPEC_INV) {
+        if (d0) MVTV_DCTG(SPEC_INV, true, false);
+        else MVTV_DCTG(SPEC_INV, false, false);
+    } else {
+        if (d0) {
+            if (formb) MVTV_DCTG(SPEC_MID, true, true);
+            else MVTV_DCTG(SPEC_MID, true, false);
+        } else {
+            MVTV_DCTG(SPEC_MID, false, false);
+        }
+    }
+#undef MVTV_DCTG
+}
+
+// radices of m = 2^a 3^b 5^c 7^d in stage order (8s first); false if m has another prime factor
+bool dct_radix_plan(uint32_t m, int* rad, int* nrad) {
+    int n = 0;
+    for (const uint32_t r : {8u, 4u, 2u, 3u, 5u, 7u})
+        while (m % r == 0 && m > 1) {
+            if (n == 8) return false;
+            rad[n++] = int(r);
+            m /= r;
+        }
+    *nrad = n;
+    return m == 1;
+}
+
+// =============================================================================================
 // Last dimension by a tridiagonal solve instead of DCT / divide / inverse DCT.
 //
 // After the forward transforms along dims 0..p-2, line q of the last dimension d carries the 1-D
@@ -877,6 +1190,163 @@ __global__ __launch_bounds__((tri::Shape<L, SEG>::NT)) void k_tri(const SpecArgs
         __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + (uint32_t(i) << a.ls));
 }
 
+// k_trig: the same solve for any line length m = NSEG * s (segment length s <= 32 chosen at launch,
+// NSEG <= 64) and any line stride (FastDiv addressing): the last-dimension pass of the mixed-radix
+// meshes. Rows past s in the fixed-size register arrays are predicated off.
+namespace trig {
+constexpr int SMAX = 32, NSMAX = 64, TQ = 16;
+}
+
+__global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nseg) {
+    constexpr int TQ = trig::TQ, SMAX = trig::SMAX;
+    double sigma = a.sigma;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+    }
+    __shared__ double t_id[SMAX][TQ], t_e[SMAX][TQ], t_h[SMAX][TQ], t_k[SMAX][TQ];
+    __shared__ double s_a[TQ];
+    __shared__ double s_u[trig::NSMAX][TQ], s_v[trig::NSMAX][TQ], s_bu[trig::NSMAX][TQ], s_bv[trig::NSMAX][TQ];
+    const int t = threadIdx.x, c = t % TQ, sj = t / TQ;
+    const uint32_t m = a.m[a.d];
+    const uint32_t q0 = blockIdx.x * uint32_t(TQ);
+    const uint32_t q = q0 + uint32_t(c);
+    const bool valid = q < a.nlines;
+    const uint32_t qq = valid ? q : q0;
+    const uint32_t hi = a.fds.div(qq);
+    const uint32_t base = (qq - hi * a.stride) + hi * a.stride * m + uint32_t(sj * sl) * a.stride;
+
+    double g[SMAX];
+#pragma unroll
+    for (int i = 0; i < SMAX; ++i)
+        g[i] = (valid && i < sl) ? __builtin_nontemporal_load(a.in + base + uint32_t(i) * a.stride) : 0.0;
+
+    if (t < TQ) {
+        const uint32_t ql = a.q_off + qq;
+        double lamv[kMaxDims] = {0, 0, 0, 0};
+        uint32_t rest = ql;
+        const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
+        for (int jj = 0; jj < a.p; ++jj) {
+            if (jj == a.d) continue;
+            const uint32_t qd = (jj < jlast) ? a.fd[jj].div(rest) : 0u;
+            lamv[jj] = a.lam[a.lam_off[jj] + (rest - qd * a.m[jj])];
+            rest = qd;
+        }
+        double c0 = a.w0, c1 = 0.0;
+        for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
+            if (a.cS[Sm] == 0.0) continue;
+            double prod = sigma * a.cS[Sm];
+            for (int jj = 0; jj < a.p; ++jj)
+                if (jj != a.d && ((Sm >> jj) & 1)) prod *= lamv[jj];
+            if ((Sm >> a.d) & 1) c1 += prod;
+            else c0 += prod;
+        }
+        const double A = -c1, B = c0 + 2.0 * c1;
+        double e = 0.0, h = 1.0;
+#pragma unroll 1
+        for (int i = 0; i < sl; ++i) {
+            const double id = 1.0 / (B - A * e);
+            e = A * id;
+            h = -A * h * id;
+            t_id[i][c] = id;
+            t_e[i][c] = e;
+            t_h[i][c] = h;
+        }
+        double H = t_h[sl - 1][c], K = -t_e[sl - 1][c];
+        t_k[sl - 1][c] = K;
+#pragma unroll 1
+        for (int i = sl - 2; i >= 0; --i) {
+            const double ei = t_e[i][c];
+            H = t_h[i][c] - ei * H;
+            K = -ei * K;
+            t_h[i][c] = H;
+            t_k[i][c] = K;
+        }
+        s_a[c] = A;
+    }
+    __syncthreads();
+
+    {
+        const double A = s_a[c];
+        g[0] *= t_id[0][c];
+#pragma unroll
+        for (int i = 1; i < SMAX; ++i)
+            if (i < sl) g[i] = (g[i] - A * g[i - 1]) * t_id[i][c];
+        double last = 0.0;
+#pragma unroll
+        for (int i = SMAX - 1; i >= 0; --i) {
+            if (i == sl - 1) last = g[i];
+            if (i < sl - 1) g[i] -= t_e[i][c] * g[i + 1];
+        }
+        s_u[sj][c] = g[0];
+        s_v[sj][c] = last;
+    }
+    __syncthreads();
+
+    if (t < TQ) {
+        const double H0 = t_h[0][c], K0 = t_k[0][c], H1 = t_h[sl - 1][c], K1 = t_k[sl - 1][c];
+        double av = 0.0, bv = 0.0;
+#pragma unroll 1
+        for (int j = 0; j < nseg - 1; ++j) {
+            const double g0 = s_u[j][c], g1 = s_v[j][c];
+            double au, bu;
+            if (j == 0) {
+                const double id = 1.0 / (1.0 - H0);
+                au = g0 * id;
+                bu = K0 * id;
+                av = g1 + H1 * au;
+                bv = K1 + H1 * bu;
+            } else {
+                const double id = 1.0 / (1.0 - H0 * bv);
+                au = (g0 + H0 * av) * id;
+                bu = K0 * id;
+                const double nav = g1 + H1 * av + H1 * bv * au;
+                bv = K1 + H1 * bv * bu;
+                av = nav;
+            }
+            s_u[j][c] = au;
+            s_bu[j][c] = bu;
+            s_v[j][c] = av;
+            s_bv[j][c] = bv;
+        }
+        const int J = nseg - 1;
+        const double a11 = 1.0 - H0 * bv, a12 = -K0, a21 = -H1 * bv, a22 = 1.0 - K1;
+        const double b1 = s_u[J][c] + H0 * av, b2 = s_v[J][c] + H1 * av;
+        const double idet = 1.0 / (a11 * a22 - a12 * a21);
+        double u = (b1 * a22 - a12 * b2) * idet;
+        s_u[J][c] = u;
+        s_v[J][c] = (a11 * b2 - a21 * b1) * idet;
+#pragma unroll 1
+        for (int j = J - 1; j >= 0; --j) {
+            const double un = u;
+            u = s_u[j][c] + s_bu[j][c] * un;
+            s_v[j][c] = s_v[j][c] + s_bv[j][c] * un;
+            s_u[j][c] = u;
+        }
+    }
+    __syncthreads();
+
+    const double Lj = sj == 0 ? s_u[0][c] : s_v[sj - 1][c];
+    const double Rj = sj == nseg - 1 ? s_v[nseg - 1][c] : s_u[sj + 1][c];
+    const double sc = a.inv_n * double(m);
+    if (!valid) return;
+#pragma unroll
+    for (int i = 0; i < SMAX; ++i)
+        if (i < sl)
+            __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + uint32_t(i) * a.stride);
+}
+
+// segment length for k_trig: the smallest divisor of m in [16, 32], else the largest in [4, 16),
+// with at most 64 segments; 0 when there is none
+static int trig_seg(uint32_t m) {
+    for (uint32_t sl = 16; sl <= uint32_t(trig::SMAX); ++sl)
+        if (m % sl == 0 && m / sl <= uint32_t(trig::NSMAX) && m / sl >= 2) return int(sl);
+    for (uint32_t sl = 15; sl >= 4; --sl)
+        if (m % sl == 0 && m / sl <= uint32_t(trig::NSMAX) && m / sl >= 2) return int(sl);
+    return 0;
+}
+
 // k_tri serves the last-dimension pass when the lines are long enough for >= 4 segments, short
 // enough for <= 64 (one workgroup <= 1024 threads), 16 lines make a 128-B row (stride >= 16) and
 // there are enough line tiles to fill the chip (the 2-D configs keep the FFT pass)
@@ -1001,8 +1471,34 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     a.p = g.p;
     a.L = 0;
     while ((1u << a.L) < m) ++a.L;
-    if ((1u << a.L) != m || m > 4096) return hipErrorInvalidValue;
     const bool formb = ga != nullptr;
+    if (m > 4096) return hipErrorInvalidValue;
+    if ((1u << a.L) != m || (1u << a.ls) != a.stride) {   // mixed radix, or a power of two over a general stride
+        if (a.pk || !dct_radix_plan(m, a.rad, &a.nrad)) return hipErrorInvalidValue;
+        a.fds = FastDiv(a.stride);
+        a.fm = FastDiv(m);
+        for (int st = 0, L = 1; st < a.nrad; ++st) {
+            a.fper[st] = FastDiv(m / uint32_t(a.rad[st]));
+            a.fL[st] = FastDiv(uint32_t(L));
+            L *= a.rad[st];
+        }
+        a.perm = sp.perm + sp.lam_off[d];
+        if (mode == SPEC_MID && d > 0 && !formb && a.nlines / uint32_t(trig::TQ) >= 256u && !probe_env("MVTV_DCT_TRI0")) {
+            const int sl = trig_seg(m);
+            if (sl > 0) {
+                const int nseg = int(m) / sl;
+                const dim3 grid((a.nlines + uint32_t(trig::TQ) - 1) / uint32_t(trig::TQ));
+                klaunch(k_trig, grid, dim3(trig::TQ * nseg), 0, s, a, sl, nseg);
+                return hipGetLastError();
+            }
+        }
+        // <= 16 lines (128-B rows for d > 0) in <= 64 KB of LDS
+        int tq = 16;
+        while (tq > 2 && (tq / 2) * int(m + spec::PAD) > spec::LDS_WORDS / 2 + 8 * spec::PAD) tq /= 2;
+        a.tq = tq;
+        launch_dctg(a, s, mode, d == 0, formb);
+        return hipGetLastError();
+    }
     if (a.pk && a.L < 3) return hipErrorInvalidValue;   // the packed layout is served by k_dct8 only
     if (tri_ok(a, mode, formb)) {
         launch_tri(a, s);

@@ -38,7 +38,15 @@ CASES = [([2], None, "cpp", False), ([8], None, "cpp", False), ([1024], None, "p
          ([8, 8, 8, 8], [0.1, 0.2, 0.3, 0.4], "cpp", False),
          # >= 4096 lines of >= 64 points along the last dim: the tridiagonal last-dimension pass (k_tri)
          # (3-D and 4-D meshes large enough for it are checked by residual and against PCG below)
-         ([4096, 64], [0.3, 0.7], "cpp", False), ([4096, 128], None, "py", False)]
+         ([4096, 64], [0.3, 0.7], "cpp", False), ([4096, 128], None, "py", False),
+         # mixed-radix lengths (k_dctg), also powers of two over a general stride
+         ([3], None, "cpp", False), ([1000], None, "py", False), ([2187], None, "cpp", False),
+         ([12, 8], [0.3, 0.7], "cpp", False), ([24, 40], [0.5, 0.5], "cpp", False), ([63, 10], None, "py", False),
+         ([6, 6, 6], [0.5, 0.25, 0.125], "cpp", False), ([10, 10, 10], None, "py", False),
+         ([5, 5, 5, 5], [0.1, 0.2, 0.3, 0.4], "cpp", False), ([6, 6, 6, 6], None, "py", False),
+         ([7, 7, 7], [0.2, 0.3, 0.4], "cpp", True), ([3, 4096], [0.5, 0.5], "cpp", False),
+         # mixed-radix mesh whose last dimension takes the general-length tridiagonal pass (k_trig)
+         ([4096, 100], [0.5, 0.5], "cpp", False)]
 
 
 def _problem(m, deltas, order, unit, seed=0):
@@ -66,9 +74,11 @@ def test_spectral_vs_superlu(m, deltas, order, unit, sigma):
     P.close()
 
 
-@pytest.mark.parametrize("m", [[256, 256, 256], [1024, 1024], [64, 64, 64, 64]])
+@pytest.mark.parametrize("m", [[256, 256, 256], [1024, 1024], [64, 64, 64, 64], [100, 100, 100], [240, 240, 240],
+                               [60, 60, 60, 60]])
 def test_spectral_residual_baseline_sizes(m):
-    """Config-sized meshes (3D 256^3, 2D 1024^2; 4D at 64^4): residual through the stencil operator."""
+    """Config-sized meshes (3D 256^3, 2D 1024^2; 4D at 64^4) and mixed-radix ones (k_dctg passes, k_trig
+    last dimension): residual through the stencil operator."""
     p = len(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     N = int(np.prod(m))
@@ -95,18 +105,18 @@ def test_spectral_matches_pcg_large():
 
 def test_spectral_rejected_when_not_exact():
     rng = np.random.default_rng(0)
-    with mv.Problem([12, 8], rng.standard_normal(96), deltas=[1, 1]) as P:       # 12 is not a power of two
+    with mv.Problem([22, 8], rng.standard_normal(176), deltas=[1, 1]) as P:      # 22 = 2 * 11
         assert not P.spectral_ok()
         with pytest.raises(mv.MvtvError):
-            P.solve_spectral(1.0, np.zeros(96))
+            P.solve_spectral(1.0, np.zeros(176))
         with pytest.raises(mv.MvtvError):
-            P.admm(1.0, np.zeros(96), u=np.zeros(P.E), rho=0.2, theta_solver=mv.SOLVER_SPECTRAL)
-        _, _, _, st = P.admm(1.0, np.zeros(96), u=np.zeros(P.E), rho=0.2, fixed_iters=2)
+            P.admm(1.0, np.zeros(176), u=np.zeros(P.E), rho=0.2, theta_solver=mv.SOLVER_SPECTRAL)
+        _, _, _, st = P.admm(1.0, np.zeros(176), u=np.zeros(P.E), rho=0.2, fixed_iters=2)
         assert st["theta_solver"] == mv.SOLVER_PCG
     with mv.Problem([8, 8], rng.standard_normal(64), wdiag=rng.uniform(0, 2, 64).round(), deltas=[1, 1]) as P:
         assert not P.spectral_ok()                                               # W != I
         _, _, _, st = P.admm(1.0, np.zeros(64), u=np.zeros(P.E), rho=0.2, fixed_iters=2)
-        assert st["theta_solver"] == mv.SOLVER_PCG_SPECTRAL                     # AUTO: power-of-two mesh
+        assert st["theta_solver"] == mv.SOLVER_PCG_SPECTRAL                     # AUTO: 2-3-5-7 mesh
 
 
 def test_spectral_admm_towers_3d():
