@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--pcg-rtol", type=float, default=1e-10)
     ap.add_argument("--solver", choices=["auto", "pcg", "spectral"], default="auto",
                     help="theta-solve: auto = spectral (exact DCT solve) where it applies, else the spectrally "
-                         "preconditioned PCG (power-of-two meshes), else Jacobi-PCG; pcg = Jacobi-PCG; "
+                         "preconditioned PCG (2-3-5-7 meshes), else Jacobi-PCG; pcg = Jacobi-PCG; "
                          "spectral = the exact solve (--mode cv: the spectrally preconditioned PCG)")
     ap.add_argument("--pcg-steps", type=int, default=10,
                     help="steps of the secondary Jacobi-PCG leg reported beside the main one (0 = skip)")

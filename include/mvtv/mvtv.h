@@ -85,14 +85,15 @@ typedef struct mvtv_admm_opts {
 /* theta-solve of (W + sigma D^T D) theta = b. The reference factorises with SuperLU every
  * iteration (rcpp…/solvers.cpp:113, cpp-code/solvers.cpp:116, code/solvers.py:72). */
 typedef enum mvtv_theta_solver {
-    MVTV_SOLVER_AUTO = 0,      /* SPECTRAL where it is exact; else PCG_SPECTRAL on power-of-two meshes <= 4096; else PCG */
+    MVTV_SOLVER_AUTO = 0,      /* SPECTRAL where it is exact; else PCG_SPECTRAL on the same meshes; else PCG */
     MVTV_SOLVER_PCG = 1,       /* Jacobi-PCG on the 3^p-point stencil, warm-started, pcg_rtol */
-    MVTV_SOLVER_SPECTRAL = 2,  /* direct: cosine transforms + diagonal divide. Exact for W = I (mesh == data)
-                                  with every m_j a power of two <= 4096; MVTV_BAD_ARG otherwise */
+    MVTV_SOLVER_SPECTRAL = 2,  /* direct: cosine transforms + a tridiagonal solve along the last dim. Exact for
+                                  W = I (mesh == data) with every m_j <= 4096 a product of 2, 3, 5, 7;
+                                  MVTV_BAD_ARG otherwise */
     MVTV_SOLVER_PCG_SPECTRAL = 3 /* PCG preconditioned by S (mean(W) I + sigma D^T D) S, its middle factor inverted
                                   exactly by cosine transforms, S = I or a Jacobi-like diagonal scaling when W varies
                                   strongly against sigma D^T D's diagonal: for W != I (scattered data, CV folds) on
-                                  power-of-two meshes */
+                                  the meshes SPECTRAL accepts */
 } mvtv_theta_solver;
 
 typedef struct mvtv_admm_stats {
@@ -129,7 +130,7 @@ int32_t mvtv_problem_blocks(const mvtv_problem* prob);
 mvtv_status mvtv_problem_block_info(const mvtv_problem* prob, int32_t k, int32_t* code, int32_t* sprime, double* weight);
 /* new O^T y and W for the same mesh (CV folds re-run create_cache_objects, rcpp…/solvers.cpp:347-348) */
 mvtv_status mvtv_problem_set_data(mvtv_problem* prob, const double* oty, const double* wdiag);
-/* 1 if MVTV_SOLVER_SPECTRAL applies to this problem (W = I, power-of-two m_j <= 4096), else 0 */
+/* 1 if MVTV_SOLVER_SPECTRAL applies to this problem (W = I, every m_j <= 4096 a product of 2, 3, 5, 7), else 0 */
 int32_t mvtv_problem_spectral_ok(const mvtv_problem* prob);
 
 /* ---- the hot path ------------------------------------------------------------------ */
