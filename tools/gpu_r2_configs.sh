@@ -11,7 +11,8 @@ run() {  # name, args...
   timeout -k 10 400 python bench.py "$@" > $O/$n.json 2> $O/$n.err
 }
 run b512 && run b1024 --dims 2 --size 1024 && run b2048 --dims 2 --size 2048 && run b256 --dims 3 --size 256 && \
-run b128_4d --dims 4 --size 128 --pcg-steps 4 && run bcv --mode cv --steps 40 --warmup 5 || exit 1
+run b128_4d --dims 4 --size 128 --pcg-steps 4 && run bcv --mode cv --steps 40 --warmup 5 && \
+run b500 --dims 3 --size 500 --steps 10 --warmup 2 --pcg-steps 5 && run b1000 --dims 2 --size 1000 --pcg-steps 20 || exit 1
 cd /tmp && export TMPDIR=/tmp
 kt() {
   local n=$1; shift
@@ -19,5 +20,6 @@ kt() {
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_$n -o run --output-format csv -- python3 $R/bench.py --no-cpu "$@" > $O/kt_$n.log 2>&1
 }
 kt b512 --steps 10 --warmup 2 && kt b1024 --dims 2 --size 1024 --pcg-steps 2 && kt b256 --dims 3 --size 256 --pcg-steps 2 && \
-kt b128_4d --dims 4 --size 128 --pcg-steps 2 --steps 6 && kt bcv --mode cv --steps 20 --warmup 2
+kt b128_4d --dims 4 --size 128 --pcg-steps 2 --steps 6 && kt bcv --mode cv --steps 20 --warmup 2 && \
+kt b500 --dims 3 --size 500 --steps 5 --warmup 1 --pcg-steps 2
 echo "rc=$?"
