@@ -45,12 +45,19 @@
 namespace mvtv {
 
 namespace cg3d {
-constexpr int NT = 512, NW = NT / 64;    // threads, waves per workgroup
 constexpr int IW = 64;                   // image row = one wavefront
 constexpr int RPW = 3;                   // image rows per wave
-constexpr int IH = NW * RPW;             // 24 image rows
-constexpr int TX = IW - 4, TY = IH - 4;  // 60 x 20 output tile
-constexpr int IMG = (IH + 2) * IW + 2;   // + a guard row above and below, + 1 word each end
+constexpr int TX = IW - 4;               // 60 output columns
+// NWV waves per workgroup: 8 -> 24 image rows (60 x 20 output tile), 16 -> 48 rows (60 x 44): the
+// taller tile re-reads fewer halo rows of r and p (64 x 48 / (60 x 44) = 1.16 loads per owned cell
+// against 64 x 24 / (60 x 20) = 1.28)
+template <int NWV>
+struct Shape {
+    static constexpr int NT = NWV * 64, NW = NWV;
+    static constexpr int IH = NW * RPW;
+    static constexpr int TY = IH - 4;
+    static constexpr int IMG = (IH + 2) * IW + 2;   // + a guard row above and below, + 1 word each end
+};
 }  // namespace cg3d
 
 struct Cg3dArgs {
@@ -101,9 +108,11 @@ __device__ __forceinline__ void wave_rows(const double* img, const double* K, do
 
 // MODE 0: prologue (r0 = b - A x0 with b = oty + ca ga + cb gb; reductions gamma0, delta0,
 // |r0|^2, |b|^2); MODE 1: first iteration (beta = 0, p_{-1} not read); MODE 2: iteration.
-template <int WM, int MODE>
-__global__ __launch_bounds__(cg3d::NT, 4) void k_cg3d(const Cg3dArgs a) {
+template <int WM, int MODE, int NWV>
+__global__ __launch_bounds__(cg3d::Shape<NWV>::NT, 32 / NWV) void k_cg3d(const Cg3dArgs a) {
     using namespace cg3d;
+    using Sh = Shape<NWV>;
+    constexpr int NT = Sh::NT, IH = Sh::IH, TY = Sh::TY, IMG = Sh::IMG;
     __shared__ double sP[IMG];   // plane z of p_i (x_0 in the prologue)
     __shared__ double sU[IMG];   // u_{i+1} of one plane
     __shared__ double sD[8];     // 1 / diag (W = I) or sigma diag(D^T D) (W diagonal), by pattern
@@ -326,6 +335,11 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
                        const double* oty, const double* ga, double ca, const double* gb, double cb,
                        const PcgState* st, double* partials, int* nblocks_out) {
     using namespace cg3d;
+    static const int nwv = [] {
+        const char* e = probe_env("MVTV_CG3D_NW");
+        return e && std::atoi(e) == 8 ? 8 : 16;
+    }();
+    const int TY = nwv == 16 ? Shape<16>::TY : Shape<8>::TY;
     Cg3dArgs a{};
     a.m0 = int(g.m[0]);
     a.m1 = int(g.m[1]);
@@ -394,17 +408,21 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
     a.st = st;
     a.partials = partials;
     auto go = [&](auto kern) {
-        klaunch(kern, dim3(nblocks), dim3(NT), 0, s, a);
+        klaunch(kern, dim3(nblocks), dim3(nwv * 64), 0, s, a);
         return hipGetLastError();
     };
-    if (wmode == W_DIAG) {
-        if (mode == 0) return go(k_cg3d<W_DIAG, 0>);
-        if (mode == 1) return go(k_cg3d<W_DIAG, 1>);
-        return go(k_cg3d<W_DIAG, 2>);
-    }
-    if (mode == 0) return go(k_cg3d<W_IDENTITY, 0>);
-    if (mode == 1) return go(k_cg3d<W_IDENTITY, 1>);
-    return go(k_cg3d<W_IDENTITY, 2>);
+    auto pick = [&](auto nc) {
+        constexpr int NV = decltype(nc)::value;
+        if (wmode == W_DIAG) {
+            if (mode == 0) return go(k_cg3d<W_DIAG, 0, NV>);
+            if (mode == 1) return go(k_cg3d<W_DIAG, 1, NV>);
+            return go(k_cg3d<W_DIAG, 2, NV>);
+        }
+        if (mode == 0) return go(k_cg3d<W_IDENTITY, 0, NV>);
+        if (mode == 1) return go(k_cg3d<W_IDENTITY, 1, NV>);
+        return go(k_cg3d<W_IDENTITY, 2, NV>);
+    };
+    return nwv == 16 ? pick(std::integral_constant<int, 16>{}) : pick(std::integral_constant<int, 8>{});
 }
 
 
