@@ -1061,11 +1061,11 @@ struct Gather4Args {
     int wlo, whi, wchunk, nwc, n3, nblocks_b;            // pass B: owned planes [wlo, whi)
 };
 namespace g4 {
-constexpr int TX = 64, TY = 4, NT = TX * TY, NTB = 256;
+constexpr int TX = 64, NTB = 256;   // pass A: 64-column tiles of g4_ty() rows; pass B: 256 threads
 }
 
-template <int ORD, int UM, int NB>
-__global__ __launch_bounds__(g4::NT) void k_gather4a(const Gather4Args a) {
+template <int ORD, int UM, int NB, int TYV>
+__global__ __launch_bounds__(64 * TYV) void k_gather4a(const Gather4Args a) {
     constexpr int P = 4;
     const Geom& g = a.g;
     double tt = a.t;
@@ -1081,7 +1081,7 @@ __global__ __launch_bounds__(g4::NT) void k_gather4a(const Gather4Args a) {
     const int tz = rem / nt;
     rem -= tz * nt;
     const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
-    const int x = tx * g4::TX + int(threadIdx.x & 63), y = ty * g4::TY + int(threadIdx.x >> 6);
+    const int x = tx * g4::TX + int(threadIdx.x & 63), y = ty * TYV + int(threadIdx.x >> 6);
     const int w = a.wa + tw;
     const int z0 = tz * a.zchunk, z1 = min(int(g.m[2]), z0 + a.zchunk);
     if (x >= int(g.m[0]) || y >= int(g.m[1])) return;
@@ -1227,6 +1227,17 @@ bool gather4_ok(const Geom& g) {
     return per <= kMaxCgBlocks && nwp >= 1;
 }
 
+// rows (waves) of a pass-A tile: the y - 1 neighbours of all but the first row are the tile's own loads.
+// 128^4, same box: 4 rows 9.39-9.42 ms, 8 rows 9.05, 16 rows 11.4 (profiles/r02/v14_gather4_rows)
+static int g4_ty() {
+    static const int ty = [] {
+        const char* e = probe_env("MVTV_G4_TY");
+        const int v = e ? std::atoi(e) : 8;
+        return (v == 4 || v == 16) ? v : 8;
+    }();
+    return ty;
+}
+
 hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                           double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
                           int* nparts, const AdmmCtl* ctl, double* scratch) {
@@ -1250,7 +1261,7 @@ hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, co
     a.wa = std::max(0, a.wlo - 1);   // Gw of the plane below the owned range (slab ghost) too
     a.wb = a.whi;
     a.tiles_x = int((g.m[0] + g4::TX - 1) / g4::TX);
-    a.tiles_y = int((g.m[1] + g4::TY - 1) / g4::TY);
+    a.tiles_y = int((g.m[1] + g4_ty() - 1) / g4_ty());
     const int per_w = a.tiles_x * a.tiles_y;
     const int nw = a.wb - a.wa;
     a.nzc = std::max(1, std::min(int(g.m[2]), 8192 / std::max(1, per_w * nw)));
@@ -1267,13 +1278,18 @@ hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, co
     a.nblocks_b = per * a.nwc;
     const bool expl = umode == U_EXPLICIT;
     auto goa = [&](auto kern) {
-        klaunch(kern, dim3((a.nblocks + 7) / 8 * 8), dim3(g4::NT), 0, s, a);
+        klaunch(kern, dim3((a.nblocks + 7) / 8 * 8), dim3(64 * g4_ty()), 0, s, a);
         return hipGetLastError();
     };
-    hipError_t e;
-    if (order == 0) e = expl ? goa(k_gather4a<0, U_EXPLICIT, 15>) : goa(k_gather4a<0, U_FROM_Z, 15>);
-    else if (g.nb == 14) e = expl ? goa(k_gather4a<1, U_EXPLICIT, 14>) : goa(k_gather4a<1, U_FROM_Z, 14>);
-    else e = expl ? goa(k_gather4a<1, U_EXPLICIT, 15>) : goa(k_gather4a<1, U_FROM_Z, 15>);
+    auto pick = [&](auto tc) {
+        constexpr int T = decltype(tc)::value;
+        if (order == 0) return expl ? goa(k_gather4a<0, U_EXPLICIT, 15, T>) : goa(k_gather4a<0, U_FROM_Z, 15, T>);
+        if (g.nb == 14) return expl ? goa(k_gather4a<1, U_EXPLICIT, 14, T>) : goa(k_gather4a<1, U_FROM_Z, 14, T>);
+        return expl ? goa(k_gather4a<1, U_EXPLICIT, 15, T>) : goa(k_gather4a<1, U_FROM_Z, 15, T>);
+    };
+    const int ty = g4_ty();
+    const hipError_t e = ty == 16 ? pick(std::integral_constant<int, 16>{})
+                                  : (ty == 8 ? pick(std::integral_constant<int, 8>{}) : pick(std::integral_constant<int, 4>{}));
     if (e != hipSuccess) return e;
     if (g_timed_b.start) {   // the caller timed both passes
         g_timed = g_timed_b;
