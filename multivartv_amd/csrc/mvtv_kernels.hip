@@ -347,10 +347,15 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     __shared__ double res[kMaxRed];
     for (int k = 0; k < nr; ++k) {
         const bool mx = nmax >= 0 ? k >= nr - nmax : ((-nmax >> k) & 1) != 0;
-        double acc = mx ? 0.0 : 0.0;
-        for (int b = threadIdx.x; b < nparts; b += 1024) {
-            const double v = partials[b * nr + k];
-            acc = mx ? fmax(acc, v) : acc + v;
+        // lane t sums rows t, t + 1024, ... in order; the row loads of a batch of 8 are issued together
+        double acc = 0.0;
+        for (int b0 = threadIdx.x; b0 < nparts; b0 += 8 * 1024) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = b0 + u * 1024 < nparts ? partials[(b0 + u * 1024) * nr + k] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (b0 + u * 1024 < nparts) acc = mx ? fmax(acc, v[u]) : acc + v[u];
         }
         sm[threadIdx.x] = acc;
         __syncthreads();
