@@ -80,6 +80,7 @@ struct SpecArgs {
     FastDiv fm;               // division by m
     FastDiv fper[8], fL[8];   // stage s: butterflies per line (m / rad[s]) and the span before it
     const uint32_t* perm;     // position of sample k in the digit-reversed Makhoul order (this dim)
+    int32_t xcd;              // k_dct8: tiles dealt to the XCDs in contiguous runs (grid a multiple of 8)
 };
 
 // element offset in a packed all-to-all buffer of the element at offset i of the owned planes
@@ -517,7 +518,10 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
     const int t = threadIdx.x;
     const int j = D0 ? (t % TPL) : (t / NCL);
     const int c = D0 ? (t / TPL) : (t % NCL);
-    const uint32_t q0 = blockIdx.x * uint32_t(a.tq);
+    // xcd: workgroup b runs on XCD b % 8; dealing tiles in contiguous runs per XCD keeps the tiles that
+    // share a 128-B row of a strided pass (d > 0, < 16 lines per tile) in one L2
+    const uint32_t bx = a.xcd ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const uint32_t q0 = bx * uint32_t(a.tq);
     const int la = 2 * c, lb = 2 * c + 1;
     const bool va = la < a.tq && q0 + la < a.nlines;
     const bool vb = lb < a.tq && q0 + lb < a.nlines;
@@ -1381,34 +1385,15 @@ static void launch_tri(SpecArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------ launcher
-// strided (d > 0) passes of long lines: twice the default tile (one 148-KB workgroup per CU) so a
-// line position is a 64-B (L = 11) / 128-B (L = 10) row instead of 32 / 64 B. 2-D 2048^2: the two
-// strided passes 49 -> 28 us, 3670 -> 4320 ADMM it/s (MVTV_DCT_WIDE=0 restores the default tile)
-template <int L>
-constexpr int wide_tq() { return (L >= 10 && L <= 12) ? 2 * spec8::Shape<L>::TQ : 0; }
-
-template <int L>
-static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
-    using S = spec8::Shape<L>;
-    if constexpr (wide_tq<L>() > 0) {
-        static const bool wide = [] {
-            const char* e = probe_env("MVTV_DCT_WIDE");
-            return !e || std::atoi(e) != 0;
-        }();
-        if (wide && !d0 && a.tq == S::TQ && uint32_t(wide_tq<L>()) <= a.stride) {
-            constexpr int TW = wide_tq<L>();
-            a.tq = TW;
-            const dim3 grid((a.nlines + uint32_t(TW) - 1) / uint32_t(TW)), block(spec8::ShapeK<L, TW>::NT);
-            if (mode == SPEC_FWD) klaunch(k_dct8<L, SPEC_FWD, false, false, TW>, grid, block, 0, s, a);
-            else if (mode == SPEC_INV) klaunch(k_dct8<L, SPEC_INV, false, false, TW>, grid, block, 0, s, a);
-            else klaunch(k_dct8<L, SPEC_MID, false, false, TW>, grid, block, 0, s, a);
-            return;
-        }
-    }
-    // tile size: 16 lines (128-B rows for d > 0) measured best; 8 lines (64-B rows) cost +50 % per
-    // pass and 32 lines (one 150-KB workgroup per CU) +6 % at 512^3
-    const dim3 grid((a.nlines + uint32_t(a.tq) - 1) / uint32_t(a.tq)), block(S::NT);
-#define MVTV_DCT8(MODE, D0, FB) klaunch(k_dct8<L, MODE, D0, FB>, grid, block, 0, s, a)
+// One k_dct8 pass with TQW real lines per workgroup (NT = TQW / 2 * m / 8 threads).
+// (tq < TQW: narrow meshes whose stride is below the tile; the extra lanes idle)
+template <int L, int TQW>
+static void launch_dct8_tile(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb, int tq = TQW) {
+    a.tq = tq;
+    const uint32_t grid = (a.nlines + uint32_t(tq) - 1) / uint32_t(tq);
+    a.xcd = a.xcd && (grid & 7u) == 0u;
+    const dim3 block(spec8::ShapeK<L, TQW>::NT);
+#define MVTV_DCT8(MODE, D0, FB) klaunch(k_dct8<L, MODE, D0, FB, TQW>, dim3(grid), block, 0, s, a)
     if (mode == SPEC_FWD) {
         if (d0) {
             if (formb) MVTV_DCT8(SPEC_FWD, true, true);
@@ -1428,6 +1413,72 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
         }
     }
 #undef MVTV_DCT8
+}
+
+// tile sizes a pass may take: a power of two in [max(2, 1024 / m), 16 * 2^(L <= 9 ? 1 : 0)], with
+// NT = TQW / 2 * m / 8 in [64, 1024] and <= ~150 KB of LDS
+template <int L>
+constexpr bool tile_ok(int tq) {
+    constexpr int M = 1 << L;
+    return tq >= 2 && (tq / 2) * (M / 8) >= 64 && (tq / 2) * (M / 8) <= 1024 &&
+           (tq / 2) * spec8::Shape<L>::LP * 16 <= 152 * 1024;
+}
+template <int L, int TQW>
+static bool try_tile(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb, int want) {
+    if constexpr (tile_ok<L>(TQW)) {
+        if (want == TQW) {
+            launch_dct8_tile<L, TQW>(a, s, mode, d0, formb);
+            return true;
+        }
+    }
+    return false;
+}
+
+// Tile choice. Default: 16 lines (128-B rows for d > 0) up to 512 points per line, then 8 / 4 / 2 for
+// 1024 / 2048 / 4096 (LDS); strided passes of 1024 - 4096-point lines twice that (one ~148-KB workgroup
+// per CU: 2048^2 strided passes 49 -> 28 us, 3670 -> 4320 ADMM it/s). Meshes with few lines (2-D) would
+// leave CUs idle with those tiles: a d = 0 pass under 1024 workgroups takes the smallest tile (>= one wave),
+// a strided pass under 128 wide workgroups takes 4 lines (32-B rows) with the tiles dealt to the XCDs in
+// contiguous runs, so the 4 tiles of a 128-B row share one L2. 1024^2: 8355 -> 9650 ADMM it/s (d = 0
+// passes 17.5 -> 14.8 us, strided 18.7 -> 11.8 us); 2048^2: 4797 -> 4862 (profiles/r02/v17_dct_tiles).
+// Probe builds: MVTV_DCT_T0 / _T1 set the d = 0 / d > 0 tile, MVTV_DCT_XCD=0/1 the XCD runs.
+template <int L>
+static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
+    using S = spec8::Shape<L>;
+    constexpr int TMIN = tile_ok<L>(2) ? 2 : (tile_ok<L>(4) ? 4 : (tile_ok<L>(8) ? 8 : 16));
+    int want = S::TQ;
+    bool xcd_def = false;
+    if (d0) {
+        if (a.nlines / uint32_t(S::TQ) < 1024u) want = std::min(TMIN, S::TQ);
+    } else if (L >= 10 && L <= 12 && 2 * S::TQ <= int(a.stride)) {
+        want = 2 * S::TQ;
+        if (a.nlines / uint32_t(want) < 128u && tile_ok<L>(4) && int(a.stride) >= 4) {
+            want = 4;
+            xcd_def = true;
+        }
+    }
+    static const int t0 = [] {
+        const char* e = probe_env("MVTV_DCT_T0");
+        return e ? std::atoi(e) : 0;
+    }();
+    static const int t1 = [] {
+        const char* e = probe_env("MVTV_DCT_T1");
+        return e ? std::atoi(e) : 0;
+    }();
+    static const int xcd_env = [] {
+        const char* e = probe_env("MVTV_DCT_XCD");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (d0 && t0 > 0) want = t0;
+    if (!d0 && t1 > 0) want = t1;
+    if (!d0) want = std::min<int>(want, int(a.stride));
+    a.xcd = xcd_env >= 0 ? xcd_env : (xcd_def ? 1 : 0);
+    if (try_tile<L, 2>(a, s, mode, d0, formb, want) || try_tile<L, 4>(a, s, mode, d0, formb, want) ||
+        try_tile<L, 8>(a, s, mode, d0, formb, want) || try_tile<L, 16>(a, s, mode, d0, formb, want) ||
+        try_tile<L, 32>(a, s, mode, d0, formb, want))
+        return;
+    a.xcd = 0;
+    launch_dct8_tile<L, S::TQ>(a, s, mode, d0, formb, std::min(want, S::TQ));   // the default tile
 }
 
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
@@ -1505,10 +1556,6 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
         return hipGetLastError();
     }
     if (a.L >= 3 && !probe_env("MVTV_DCT_LDS")) {
-        static constexpr int tq8[13] = {0, 0, 0, 16, 16, 16, 16, 16, 16, 16, 8, 4, 2};
-        int tq = tq8[a.L];
-        if (d > 0) tq = std::min<int>(tq, int(g.stride[d]));
-        a.tq = tq;
         switch (a.L) {
             case 3: launch_dct8<3>(a, s, mode, d == 0, formb); break;
             case 4: launch_dct8<4>(a, s, mode, d == 0, formb); break;
