@@ -1047,18 +1047,20 @@ bool dct_radix_plan(uint32_t m, int* rad, int* nrad) {
 // scaled by inv_n * m_d (the normalisation of the transforms along the other dims).
 namespace tri {
 constexpr int TQ = 16;    // lines per workgroup: one 128-B row per position (d > 0)
-template <int L, int SEG>
+template <int L, int SEG, int TQL = TQ>
 struct Shape {
     static constexpr int M = 1 << L;
     static constexpr int NSEG = M / SEG;   // segments (threads) per line
-    static constexpr int NT = TQ * NSEG;
+    static constexpr int NT = TQL * NSEG;
 };
 }  // namespace tri
 
-template <int L, int SEG>
-__global__ __launch_bounds__((tri::Shape<L, SEG>::NT)) void k_tri(const SpecArgs a) {
-    using S = tri::Shape<L, SEG>;
-    constexpr int TQ = tri::TQ, NSEG = S::NSEG;
+// TQL lines per workgroup: 16 (128-B rows) by default; 2-D meshes with few lines take 4 or 8 with the
+// tiles dealt to the XCDs in contiguous runs (a.xcd), as k_dct8's strided passes
+template <int L, int SEG, int TQL = tri::TQ>
+__global__ __launch_bounds__((tri::Shape<L, SEG, TQL>::NT)) void k_tri(const SpecArgs a) {
+    using S = tri::Shape<L, SEG, TQL>;
+    constexpr int TQ = TQL, NSEG = S::NSEG;
     double sigma = a.sigma;
     if (a.skip && *a.skip) return;
     if (a.ctl) {
@@ -1069,7 +1071,8 @@ __global__ __launch_bounds__((tri::Shape<L, SEG>::NT)) void k_tri(const SpecArgs
     __shared__ double s_a[TQ];                                                    // -c1 per line
     __shared__ double s_u[NSEG][TQ], s_v[NSEG][TQ], s_bu[NSEG][TQ], s_bv[NSEG][TQ];
     const int t = threadIdx.x, c = t % TQ, sj = t / TQ;
-    const uint32_t q0 = blockIdx.x * uint32_t(TQ);
+    const uint32_t bx = a.xcd ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const uint32_t q0 = bx * uint32_t(TQ);
     const uint32_t q = q0 + uint32_t(c);
     const bool valid = q < a.nlines;
     const uint32_t base = (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (uint32_t(sj * SEG) << a.ls);
@@ -1351,37 +1354,62 @@ static int trig_seg(uint32_t m) {
     return 0;
 }
 
-// k_tri serves the last-dimension pass when the lines are long enough for >= 4 segments, short
-// enough for <= 64 (one workgroup <= 1024 threads), 16 lines make a 128-B row (stride >= 16) and
-// there are enough line tiles to fill the chip (the 2-D configs keep the FFT pass)
-static bool tri_ok(const SpecArgs& a, int mode, bool formb) {
-    if (mode != SPEC_MID || a.d == 0 || formb || a.pk) return false;
-    if (a.L < 6 || a.L > 10 || a.stride < uint32_t(tri::TQ)) return false;
-    if (a.nlines / uint32_t(tri::TQ) < 256u) return false;
+// k_tri serves the last-dimension pass when the lines are long enough for >= 4 segments and short enough
+// for <= 64 (16 rows per segment up to 1024 points, 32 at 2048), the stride holds the tile's lines, and
+// either 16-line tiles fill the chip (>= 256 workgroups: 3-D and 4-D meshes) or, for the few 2048-point
+// lines of a 2-D mesh, 8-line tiles in XCD runs (2048^2: 4844 -> 5145 ADMM it/s on one box; at 1024^2 the
+// FFT pass stays faster: 9866 against 9381 with 8-line and 9050 with 4-line tiles, profiles/r02/v19_tri2d).
+// Probe builds: MVTV_DCT_TRI2D=0 / 4 / 8 forces the 2-D choice.
+static int tri_tiles(const SpecArgs& a, int mode, bool formb) {
+    if (mode != SPEC_MID || a.d == 0 || formb || a.pk) return 0;
     const char* e = probe_env("MVTV_DCT_TRI");
-    return !e || std::atoi(e) != 0;
+    if (e && std::atoi(e) == 0) return 0;
+    if (a.L < 6 || a.L > 11 || a.stride < 4u) return 0;
+    if (a.L <= 10 && a.stride >= uint32_t(tri::TQ) && a.nlines / uint32_t(tri::TQ) >= 256u) return tri::TQ;
+    static const int t2d_env = [] {
+        const char* v = probe_env("MVTV_DCT_TRI2D");
+        return v ? std::atoi(v) : -1;
+    }();
+    const int t2d = t2d_env >= 0 ? t2d_env : (a.L == 11 ? 8 : 0);
+    if (t2d != 4 && t2d != 8) return 0;
+    if (uint32_t(t2d) > a.stride || (a.nlines / uint32_t(t2d)) % 8u != 0u) return 0;
+    return t2d;
 }
 
-template <int SEG>
+template <int SEG, int TQL>
 static void launch_tri_seg(SpecArgs& a, hipStream_t s) {
-    const dim3 grid((a.nlines + uint32_t(tri::TQ) - 1) / uint32_t(tri::TQ));
+    const dim3 grid((a.nlines + uint32_t(TQL) - 1) / uint32_t(TQL));
     switch (a.L) {
-        case 6: klaunch(k_tri<6, SEG>, grid, dim3(tri::Shape<6, SEG>::NT), 0, s, a); break;
-        case 7: klaunch(k_tri<7, SEG>, grid, dim3(tri::Shape<7, SEG>::NT), 0, s, a); break;
-        case 8: klaunch(k_tri<8, SEG>, grid, dim3(tri::Shape<8, SEG>::NT), 0, s, a); break;
-        case 9: klaunch(k_tri<9, SEG>, grid, dim3(tri::Shape<9, SEG>::NT), 0, s, a); break;
-        case 10: klaunch(k_tri<10, SEG>, grid, dim3(tri::Shape<10, SEG>::NT), 0, s, a); break;
+        case 6: klaunch(k_tri<6, SEG, TQL>, grid, dim3(tri::Shape<6, SEG, TQL>::NT), 0, s, a); break;
+        case 7: klaunch(k_tri<7, SEG, TQL>, grid, dim3(tri::Shape<7, SEG, TQL>::NT), 0, s, a); break;
+        case 8: klaunch(k_tri<8, SEG, TQL>, grid, dim3(tri::Shape<8, SEG, TQL>::NT), 0, s, a); break;
+        case 9: klaunch(k_tri<9, SEG, TQL>, grid, dim3(tri::Shape<9, SEG, TQL>::NT), 0, s, a); break;
+        case 10: klaunch(k_tri<10, SEG, TQL>, grid, dim3(tri::Shape<10, SEG, TQL>::NT), 0, s, a); break;
     }
 }
 
-static void launch_tri(SpecArgs& a, hipStream_t s) {
-    a.tq = tri::TQ;
-    static const int seg = [] {
-        const char* e = probe_env("MVTV_TRI_SEG");
-        return e && std::atoi(e) == 32 ? 32 : 16;
-    }();
-    if (seg == 32) launch_tri_seg<32>(a, s);
-    else launch_tri_seg<16>(a, s);
+static void launch_tri(SpecArgs& a, hipStream_t s, int tq) {
+    a.tq = tq;
+    if (tq == tri::TQ) {
+        a.xcd = 0;
+        static const int seg = [] {
+            const char* e = probe_env("MVTV_TRI_SEG");
+            return e && std::atoi(e) == 32 ? 32 : 16;
+        }();
+        if (seg == 32) launch_tri_seg<32, tri::TQ>(a, s);
+        else launch_tri_seg<16, tri::TQ>(a, s);
+        return;
+    }
+    a.xcd = 1;   // 2-D: narrow tiles in XCD runs (grid a multiple of 8, tri_tiles)
+    const dim3 grid(a.nlines / uint32_t(tq));
+    if (a.L == 11) {   // 2048-point lines: 64 segments of 32 rows
+        if (tq == 4) klaunch(k_tri<11, 32, 4>, grid, dim3(tri::Shape<11, 32, 4>::NT), 0, s, a);
+        else klaunch(k_tri<11, 32, 8>, grid, dim3(tri::Shape<11, 32, 8>::NT), 0, s, a);
+    } else if (tq == 4) {
+        launch_tri_seg<16, 4>(a, s);
+    } else {
+        launch_tri_seg<16, 8>(a, s);
+    }
 }
 
 // ------------------------------------------------------------------------------ launcher
@@ -1551,8 +1579,8 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
         return hipGetLastError();
     }
     if (a.pk && a.L < 3) return hipErrorInvalidValue;   // the packed layout is served by k_dct8 only
-    if (tri_ok(a, mode, formb)) {
-        launch_tri(a, s);
+    if (const int tq = tri_tiles(a, mode, formb)) {
+        launch_tri(a, s, tq);
         return hipGetLastError();
     }
     if (a.L >= 3 && !probe_env("MVTV_DCT_LDS")) {
