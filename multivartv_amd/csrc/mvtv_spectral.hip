@@ -641,6 +641,17 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
     }
 
     // ---- spectrum <-> DCT coefficients for the pairs (k, M-k); k = 0 also takes M/2 -------------
+    // the inverse pass issues all 8 coefficient loads before the first LDS write (issued inside the loop,
+    // each group waited for its loads before writing LDS: four HBM round trips per workgroup instead of one)
+    double2 pre[8];
+    if constexpr (MODE == SPEC_INV) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = j + s * TPL;
+            pre[2 * s] = ld2(uint32_t(k));
+            pre[2 * s + 1] = ld2(uint32_t(k ? M - k : M / 2));
+        }
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int k = j + s * TPL;
@@ -660,8 +671,8 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
                 Xmk = make_double2(q2.x * Ap.x + q2.y * Ap.y, q2.x * Bp.x + q2.y * Bp.y);
             }
         } else {
-            Xk = ld2(uint32_t(ka));
-            Xmk = ld2(uint32_t(kb));
+            Xk = pre[2 * s];
+            Xmk = pre[2 * s + 1];
         }
         if (MODE == SPEC_FWD) {
             st2(uint32_t(ka), Xk);
@@ -1077,14 +1088,12 @@ __global__ __launch_bounds__((tri::Shape<L, SEG, TQL>::NT)) void k_tri(const Spe
     const bool valid = q < a.nlines;
     const uint32_t base = (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (uint32_t(sj * SEG) << a.ls);
 
-    double g[SEG];
-#pragma unroll
-    for (int i = 0; i < SEG; ++i) g[i] = valid ? __builtin_nontemporal_load(a.in + base + (uint32_t(i) << a.ls)) : 0.0;
-
+    // the line's eigenvalue loads are issued before the rows, so the line constants below wait for them
+    // alone (loads complete in order: issued after the rows, they would wait for all SEG row loads)
+    double lamv[kMaxDims] = {0, 0, 0, 0};
     if (t < TQ) {
         // c0 + c1 T along d for this line (q indexes dims 0..p-2 column-major, as k_dct8's MID)
         const uint32_t ql = a.q_off + (valid ? q : q0);
-        double lamv[kMaxDims] = {0, 0, 0, 0};
         uint32_t rest = ql;
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int jj = 0; jj < a.p; ++jj) {
@@ -1093,6 +1102,12 @@ __global__ __launch_bounds__((tri::Shape<L, SEG, TQL>::NT)) void k_tri(const Spe
             lamv[jj] = a.lam[a.lam_off[jj] + (rest - qq * a.m[jj])];
             rest = qq;
         }
+    }
+    double g[SEG];
+#pragma unroll
+    for (int i = 0; i < SEG; ++i) g[i] = valid ? __builtin_nontemporal_load(a.in + base + (uint32_t(i) << a.ls)) : 0.0;
+
+    if (t < TQ) {
         double c0 = a.w0, c1 = 0.0;
         for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
             if (a.cS[Sm] == 0.0) continue;
