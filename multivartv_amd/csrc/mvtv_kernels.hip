@@ -343,30 +343,45 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
                                                    double rtol2, int maxit, const AdmmCtl* ctl) {
     if ((op == 2 || op == 3 || op == 5) && st->done) return;
     if (ctl && ctl->done) return;
-    __shared__ double sm[1024];
+    // lane t sums rows t, t + 1024, ... in order for every slot k, then one halving tree over all slots
+    // (the same per-slot order as one tree per slot; 10 barriers instead of 10 nr). Rows are loaded in
+    // batches of 4 (4 nr loads in flight per lane).
+    __shared__ double sm[kMaxRed][1024];
     __shared__ double res[kMaxRed];
-    for (int k = 0; k < nr; ++k) {
-        const bool mx = nmax >= 0 ? k >= nr - nmax : ((-nmax >> k) & 1) != 0;
-        // lane t sums rows t, t + 1024, ... in order; the row loads of a batch of 8 are issued together
-        double acc = 0.0;
-        for (int b0 = threadIdx.x; b0 < nparts; b0 += 8 * 1024) {
-            double v[8];
+    double acc[kMaxRed];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = b0 + u * 1024 < nparts ? partials[(b0 + u * 1024) * nr + k] : 0.0;
+    for (int k = 0; k < kMaxRed; ++k) acc[k] = 0.0;
+    unsigned mxm = 0;   // bit k: slot k is a max
+    for (int k = 0; k < nr; ++k)
+        if (nmax >= 0 ? k >= nr - nmax : ((-nmax >> k) & 1) != 0) mxm |= 1u << k;
+    for (int b0 = threadIdx.x; b0 < nparts; b0 += 4 * 1024) {
+        double v[4][kMaxRed];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (b0 + u * 1024 < nparts) acc = mx ? fmax(acc, v[u]) : acc + v[u];
-        }
-        sm[threadIdx.x] = acc;
-        __syncthreads();
-        for (int s = 512; s > 0; s >>= 1) {
-            if (threadIdx.x < s) sm[threadIdx.x] = mx ? fmax(sm[threadIdx.x], sm[threadIdx.x + s])
-                                                      : sm[threadIdx.x] + sm[threadIdx.x + s];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) res[k] = sm[0];
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < kMaxRed; ++k)
+                v[u][k] = (k < nr && b0 + u * 1024 < nparts) ? partials[(b0 + u * 1024) * nr + k] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < kMaxRed; ++k)
+                if (k < nr && b0 + u * 1024 < nparts) acc[k] = ((mxm >> k) & 1u) ? fmax(acc[k], v[u][k]) : acc[k] + v[u][k];
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxRed; ++k)
+        if (k < nr) sm[k][threadIdx.x] = acc[k];
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if (threadIdx.x < s)
+#pragma unroll
+            for (int k = 0; k < kMaxRed; ++k)
+                if (k < nr)
+                    sm[k][threadIdx.x] = ((mxm >> k) & 1u) ? fmax(sm[k][threadIdx.x], sm[k][threadIdx.x + s])
+                                                          : sm[k][threadIdx.x] + sm[k][threadIdx.x + s];
         __syncthreads();
     }
+    if (threadIdx.x < nr) res[threadIdx.x] = sm[threadIdx.x][0];
+    __syncthreads();
     if (threadIdx.x != 0) return;
     if (out)
         for (int k = 0; k < nr; ++k) out[k] = res[k];
