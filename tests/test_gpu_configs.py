@@ -15,8 +15,8 @@ from multivartv_amd.synth import towers  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("m,iters", [([256, 256, 256], 4), ([1024, 1024], 6), ([64, 64, 64, 64], 3)],
-                         ids=["3d_256", "2d_1024", "4d_64"])
+@pytest.mark.parametrize("m,iters", [([256, 256, 256], 4), ([1024, 1024], 6), ([2048, 2048], 3), ([64, 64, 64, 64], 3)],
+                         ids=["3d_256", "2d_1024", "2d_2048", "4d_64"])
 def test_spectral_and_pcg_trajectories_agree(m, iters):
     y = towers(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
