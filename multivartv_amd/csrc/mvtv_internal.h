@@ -238,6 +238,20 @@ struct DctPack {
     int32_t mode = 0;
     uint32_t lpl = 0, lch = 0, nz = 0;
 };
+// PCG vector work folded into the d = 0 passes of a preconditioner solve (spectrally preconditioned PCG,
+// power-of-two m_0 >= 64): mode 1, first pass (`in` = r): r -= alpha q and x += alpha p on load (r, x
+// written back, the transform taken of sinv * r); mode 2, last pass: out = sinv * transform, (r.z, |r|^2)
+// per workgroup into `partials` (k_finalize op 3 layout, *nparts rows). sinv may be null.
+struct PcgFuse {
+    int32_t mode = 0;
+    const PcgState* st = nullptr;
+    double *x = nullptr, *r = nullptr;
+    const double *p = nullptr, *q = nullptr, *sinv = nullptr;
+    double* partials = nullptr;
+    int* nparts = nullptr;
+};
+// true when the d = 0 passes of this mesh run in k_dct8 with their partial rows within partial_words
+bool dct_pcg_fusable(const Geom& g, size_t partial_words);
 // radices (8, 4, 2, 3, 5, 7 in stage order) of a line length m = 2^a 3^b 5^c 7^d; false for any other m
 bool dct_radix_plan(uint32_t m, int* rad, int* nrad);
 // mode 0 forward DCT-II, 1 inverse (DCT-III, unnormalised), 2 forward + divide by mu * N + inverse;
@@ -245,7 +259,8 @@ bool dct_radix_plan(uint32_t m, int* rad, int* nrad);
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
                            double w0, const AdmmCtl* ctl = nullptr, uint32_t q_off = 0, double inv_n = 0.0,
-                           const int32_t* skip = nullptr, const DctPack* pack = nullptr);
+                           const int32_t* skip = nullptr, const DctPack* pack = nullptr,
+                           const PcgFuse* pf = nullptr);
 // z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /
 // launch_gather, *nparts workgroup rows
 bool edge3d_ok(const Geom& g);

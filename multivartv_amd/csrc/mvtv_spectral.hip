@@ -81,6 +81,7 @@ struct SpecArgs {
     FastDiv fper[8], fL[8];   // stage s: butterflies per line (m / rad[s]) and the span before it
     const uint32_t* perm;     // position of sample k in the digit-reversed Makhoul order (this dim)
     int32_t xcd;              // k_dct8: tiles dealt to the XCDs in contiguous runs (grid a multiple of 8)
+    PcgFuse pf;               // k_dct8 PC = 1 / 2: the PCG vector work of the preconditioner's d = 0 passes
 };
 
 // element offset in a packed all-to-all buffer of the element at offset i of the owned planes
@@ -500,12 +501,19 @@ struct LastStage {
     static constexpr int NS = (1 << L) / R;
 };
 
-template <int L, int MODE, bool D0, bool FORMB, int TQW = 0>
+// PC (PcgFuse, d = 0 passes of a preconditioner solve): 1 = first pass, r -= alpha q and x += alpha p on
+// load with r and x written back, input sinv * r; 2 = last pass, out = sinv * transform, r.z and |r|^2 per
+// workgroup
+template <int L, int MODE, bool D0, bool FORMB, int TQW = 0, int PC = 0>
 __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const SpecArgs a) {
     using S = spec8::ShapeK<L, TQW>;
+    static_assert(PC == 0 || (D0 && !FORMB && (PC == 1 ? MODE == SPEC_FWD : MODE == SPEC_INV)),
+                  "PCG fusion: d = 0 forward (PC 1) / inverse (PC 2) passes only");
     // scalars into locals: writing into the by-value argument struct would demote it to scratch
     double sigma = a.sigma, ca = a.ca, cb = a.cb;
     if (a.skip && *a.skip) return;
+    const double alpha = PC == 1 ? a.pf.st->alpha : 0.0;
+    double rz = 0.0, rr = 0.0;   // PC 2 reductions
     if (a.ctl) {
         if (a.ctl->done) return;
         sigma = a.ctl->sigma;
@@ -605,24 +613,36 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
             for (int s4 = 0; s4 < 4; ++s4) {
                 const int n = j + s4 * TPL;
                 double2 xa = make_double2(0.0, 0.0), xb = make_double2(0.0, 0.0);
-                if (va) {
-                    const uint32_t g = gaddr(la, uint32_t(2 * n));
-                    xa = ldnt2(a.in + (a.pk == 2 ? pack_index(a, g) : g));
-                    if (FORMB) {
-                        const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
-                        xa.x += ca * g1.x + cb * g2.x;
-                        xa.y += ca * g1.y + cb * g2.y;
+                auto ld_in = [&](uint32_t g) -> double2 {
+                    if constexpr (PC == 1) {   // the operations of k_pcgs_vec op 1
+                        double2 rv = ldnt2(a.pf.r + g);
+                        const double2 qv = ldnt2(a.pf.q + g);
+                        double2 xv = ldnt2(a.pf.x + g);
+                        const double2 pv = ldnt2(a.pf.p + g);
+                        rv.x = fma(-alpha, qv.x, rv.x);
+                        rv.y = fma(-alpha, qv.y, rv.y);
+                        xv.x = fma(alpha, pv.x, xv.x);
+                        xv.y = fma(alpha, pv.y, xv.y);
+                        stnt2(a.pf.r + g, rv);
+                        stnt2(a.pf.x + g, xv);
+                        if (a.pf.sinv) {
+                            const double2 sv = ldnt2(a.pf.sinv + g);
+                            rv.x *= sv.x;
+                            rv.y *= sv.y;
+                        }
+                        return rv;
+                    } else {
+                        double2 v = ldnt2(a.in + (a.pk == 2 ? pack_index(a, g) : g));
+                        if (FORMB) {
+                            const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
+                            v.x += ca * g1.x + cb * g2.x;
+                            v.y += ca * g1.y + cb * g2.y;
+                        }
+                        return v;
                     }
-                }
-                if (vb) {
-                    const uint32_t g = gaddr(lb, uint32_t(2 * n));
-                    xb = ldnt2(a.in + (a.pk == 2 ? pack_index(a, g) : g));
-                    if (FORMB) {
-                        const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
-                        xb.x += ca * g1.x + cb * g2.x;
-                        xb.y += ca * g1.y + cb * g2.y;
-                    }
-                }
+                };
+                if (va) xa = ld_in(gaddr(la, uint32_t(2 * n)));
+                if (vb) xb = ld_in(gaddr(lb, uint32_t(2 * n)));
                 X[spec8::slot(n, cx)] = make_double2(xa.x, xb.x);
                 X[spec8::slot(M - 1 - n, cx)] = make_double2(xa.y, xb.y);
             }
@@ -717,8 +737,29 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
             for (int s4 = 0; s4 < 4; ++s4) {
                 const int n = j + s4 * TPL;
                 const double2 v0 = X[spec8::slot(n, cx)], v1 = X[spec8::slot(M - 1 - n, cx)];
-                if (va) stnt2(a.out + po(gaddr(la, uint32_t(2 * n))), make_double2(v0.x, v1.x));
-                if (vb) stnt2(a.out + po(gaddr(lb, uint32_t(2 * n))), make_double2(v0.y, v1.y));
+                auto st_out = [&](uint32_t g, double2 v) {
+                    if constexpr (PC == 2) {   // the operations of k_pcgs_vec op 2
+                        if (a.pf.sinv) {
+                            const double2 sv = ldnt2(a.pf.sinv + g);
+                            v.x *= sv.x;
+                            v.y *= sv.y;
+                        }
+                        const double2 rv = ldnt2(a.pf.r + g);
+                        rz = fma(rv.x, v.x, rz);
+                        rr = fma(rv.x, rv.x, rr);
+                        rz = fma(rv.y, v.y, rz);
+                        rr = fma(rv.y, rv.y, rr);
+                        stnt2(a.out + g, v);
+                    } else {
+                        stnt2(a.out + po(g), v);
+                    }
+                };
+                if (va) st_out(gaddr(la, uint32_t(2 * n)), make_double2(v0.x, v1.x));
+                if (vb) st_out(gaddr(lb, uint32_t(2 * n)), make_double2(v0.y, v1.y));
+            }
+            if constexpr (PC == 2) {
+                double red[2] = {rz, rr};
+                block_reduce_store<2, 0, S::NT>(red, a.pf.partials);
             }
         } else {
             stages_from<L, R0, 1, true, true>(z, j, X, cx, tw);
@@ -1436,6 +1477,14 @@ static void launch_dct8_tile(SpecArgs& a, hipStream_t s, int mode, bool d0, bool
     const uint32_t grid = (a.nlines + uint32_t(tq) - 1) / uint32_t(tq);
     a.xcd = a.xcd && (grid & 7u) == 0u;
     const dim3 block(spec8::ShapeK<L, TQW>::NT);
+    if constexpr (L >= 6 && spec8::ShapeK<L, TQW>::NT >= 64) {
+        if (a.pf.mode) {   // PCG-fused d = 0 passes (dct_pcg_fusable)
+            if (a.pf.nparts) *a.pf.nparts = int(grid);
+            if (a.pf.mode == 1) klaunch(k_dct8<L, SPEC_FWD, true, false, TQW, 1>, dim3(grid), block, 0, s, a);
+            else klaunch(k_dct8<L, SPEC_INV, true, false, TQW, 2>, dim3(grid), block, 0, s, a);
+            return;
+        }
+    }
 #define MVTV_DCT8(MODE, D0, FB) klaunch(k_dct8<L, MODE, D0, FB, TQW>, dim3(grid), block, 0, s, a)
     if (mode == SPEC_FWD) {
         if (d0) {
@@ -1524,10 +1573,22 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
     launch_dct8_tile<L, S::TQ>(a, s, mode, d0, formb, std::min(want, S::TQ));   // the default tile
 }
 
+bool dct_pcg_fusable(const Geom& g, size_t partial_words) {
+    const uint32_t m = g.m[0];
+    if (g.p < 2 || m < 64 || m > 4096 || (m & (m - 1)) != 0 || probe_env("MVTV_DCT_LDS") || probe_env("MVTV_PCGS_NINE"))
+        return false;
+    // partial rows of the last pass: one per tile of launch_dct8's d = 0 choice (16 lines up to m = 512,
+    // 8192 / m beyond; the smallest one-wave tile, >= 1024 / m lines, when that leaves < 1024 tiles)
+    const size_t nlines = g.N / m, tq = std::min<size_t>(16, 8192 / m);
+    const size_t tmin = std::max<size_t>(2, 1024 / m);
+    const size_t rows = nlines / tq >= 1024 ? (nlines + tq - 1) / tq : (nlines + tmin - 1) / tmin;
+    return 2 * rows <= partial_words;
+}
+
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
                            double w0, const AdmmCtl* ctl, uint32_t q_off, double inv_n, const int32_t* skip,
-                           const DctPack* pack) {
+                           const DctPack* pack, const PcgFuse* pf) {
     SpecArgs a{};
     if (pack && pack->mode) {
         a.pk = pack->mode;
@@ -1567,6 +1628,11 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     while ((1u << a.L) < m) ++a.L;
     const bool formb = ga != nullptr;
     if (m > 4096) return hipErrorInvalidValue;
+    if (pf && pf->mode) {   // PCG-fused d = 0 pass (dct_pcg_fusable meshes): k_dct8 only
+        if (d != 0 || formb || pack || (1u << a.L) != m || a.L < 6 || mode != (pf->mode == 1 ? SPEC_FWD : SPEC_INV))
+            return hipErrorInvalidValue;
+        a.pf = *pf;
+    }
     if ((1u << a.L) != m || (1u << a.ls) != a.stride) {   // mixed radix, or a power of two over a general stride
         if (a.pk || !dct_radix_plan(m, a.rad, &a.nrad)) return hipErrorInvalidValue;
         a.fds = FastDiv(a.stride);
