@@ -934,8 +934,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
                 P->tstop(hh);
                 hh = P->tstart(MVTV_K_REDUCE);
                 HIP_TRY(launch_finalize(P->stream, P->partials, npf, ER_N + GR_N, -(1 << ER_DTH), 0, P->red, P->st, 0.0,
-                                        0, P->ctl));
-                HIP_TRY(launch_admm_control(P->stream, P->ctl, P->red));
+                                        0, P->ctl, P->ctl, P->red));   // + the control step
                 P->tstop(hh);
                 return MVTV_OK;
             }
@@ -963,8 +962,8 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
             P->tstop(hh);
             P->tstop_b(hb);
             hh = P->tstart(MVTV_K_REDUCE);
-            HIP_TRY(launch_finalize(P->stream, P->partials, npg, GR_N, 0, 0, P->red + ER_N, P->st, 0.0, 0, P->ctl));
-            HIP_TRY(launch_admm_control(P->stream, P->ctl, P->red));
+            HIP_TRY(launch_finalize(P->stream, P->partials, npg, GR_N, 0, 0, P->red + ER_N, P->st, 0.0, 0, P->ctl, P->ctl,
+                                    P->red));   // + the control step
             P->tstop(hh);
             return MVTV_OK;
         };

@@ -185,8 +185,11 @@ hipError_t launch_pcg_pupdate(const Geom& g, const Launch& L, double sigma, int 
                               const double* r, double* p, const PcgState* st);
 // op: 0 plain (sums; max in the last nmax slots, or in the slots of bitmask -nmax when nmax < 0), 1 pcg-init, 2 pcg-after-Ap, 3 pcg-after-update,
 // 4 cg3d prologue, 5 cg3d iteration
+// ctl_step: after writing `out`, take the asynchronous ADMM loop's control step (k_admm_control) on ctl_step
+// from the reduction vector step_red in the same launch
 hipError_t launch_finalize(hipStream_t s, const double* partials, int nparts, int nr, int nmax, int op, double* out,
-                           PcgState* st, double rtol2 = 0.0, int maxit = 0, const AdmmCtl* ctl = nullptr);
+                           PcgState* st, double rtol2 = 0.0, int maxit = 0, const AdmmCtl* ctl = nullptr,
+                           AdmmCtl* ctl_step = nullptr, const double* step_red = nullptr);
 // end of an asynchronous ADMM iteration: red = [|r|^2, |D theta|^2, |alpha|^2, max dtheta, |g_u|^2,
 // |s_B|^2, |s_A|^2]; adapt_step, stopping test and the next iteration's scalars (mvtv_capi.cpp mirror)
 hipError_t launch_admm_control(hipStream_t s, AdmmCtl* ctl, const double* red);

@@ -336,11 +336,88 @@ __global__ __launch_bounds__(kThreads) void k_pcg_pupdate(Geom g, double sigma, 
     }
 }
 
+// One thread: the host loop body of mvtv_admm_run after the reductions, verbatim (same operations
+// in the same order, so decisions match the synchronous loop), then the next iteration's top test.
+__device__ __forceinline__ void admm_control_step(AdmmCtl* __restrict__ c, const double* __restrict__ R) {
+    const double* G = R + ER_N;
+    const double r_norm = sqrt(R[ER_R2]);
+    const double rho = c->rho;
+    c->t_z = c->t_next;
+    c->it += 1;
+    c->counter += 1;
+    double c_next = 1.0, rho_next = rho;
+    int status = 0;
+    const bool fixed = c->fixed_iters > 0;
+    if (c->variant == 0) {   // B: rcpp-code/MultivarTV/src/solvers.cpp:117-125
+        c->dual_norm = fabs(rho) * sqrt(G[GR_S2B]);
+        c->primal_norm = r_norm;
+        c->eps_dual = c->tol * (c->sqrtN + sqrt(G[GR_GU2]));
+        c->eps_pri = c->tol * (c->sqrtE + fmax(sqrt(R[ER_D2]), sqrt(R[ER_A2])));
+        const double tau = 2.0;
+        if (c->primal_norm > 10 * c->dual_norm) {
+            rho_next = tau * rho;
+            c_next = 1.0 / tau;
+        } else if (c->dual_norm > 10 * c->primal_norm) {
+            rho_next = 1.0 / tau * rho;
+            c_next = tau;
+        }
+        c->s_norm = c->dual_norm;
+    } else if (c->variant == 1) {   // A: cpp-code/solvers.cpp:118-126
+        const double s_norm = fabs(rho) * sqrt(G[GR_S2A]);
+        c->dtheta = R[ER_DTH];
+        c->s_norm = s_norm;
+        if (!fixed && c->counter > c->max_counter) {
+            status = 1;
+            rho_next = rho;
+        } else {
+            if (r_norm > 20 * s_norm) {
+                rho_next = 20 * rho;
+                c_next = 0.05;
+            } else if (s_norm > 20 * r_norm) {
+                rho_next = 0.1 * rho;
+                c_next = 10.0;
+            }
+            rho_next = double(int(rho_next));
+        }
+    } else {
+        c->dtheta = R[ER_DTH];
+    }
+    c->r_norm = r_norm;
+    c->c_prev = c_next;
+    c->rho = rho_next;
+    if (c->variant == 0) c->sigma = rho_next;
+    c->t_next = rho_next != 0.0 ? c->lambda / rho_next : INFINITY;
+    if (status) {
+        c->status = 1;
+        c->done = 1;
+        return;
+    }
+    if (c->variant == 0 && !fixed && c->counter > c->max_counter) {
+        c->status = 1;
+        c->done = 1;
+        return;
+    }
+    // loop-top test of the next iteration
+    if (fixed) {
+        if (c->it >= c->fixed_iters) c->done = 1;
+    } else if (c->variant == 0) {
+        if (!(c->dual_norm > c->eps_dual || c->primal_norm > c->eps_pri)) c->done = 1;
+    } else {
+        if (!(c->dtheta > c->tol)) {
+            c->done = 1;
+        } else if (c->variant == 2 && c->it >= c->max_counter) {
+            c->status = 1;
+            c->done = 1;
+        }
+    }
+}
+
 // --------------------------------------------------------------------- reductions / scalars
 // Sums the per-block partials in a fixed order (deterministic), then applies the PCG scalar step.
 __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ partials, int nparts, int nr,
                                                    int nmax, int op, double* __restrict__ out, PcgState* st,
-                                                   double rtol2, int maxit, const AdmmCtl* ctl) {
+                                                   double rtol2, int maxit, const AdmmCtl* ctl,
+                                                   AdmmCtl* ctl_step, const double* step_red) {
     if ((op == 2 || op == 3 || op == 5) && st->done) return;
     if (ctl && ctl->done) return;
     // lane t sums rows t, t + 1024, ... in order for every slot k, then one halving tree over all slots
@@ -385,6 +462,10 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     if (threadIdx.x != 0) return;
     if (out)
         for (int k = 0; k < nr; ++k) out[k] = res[k];
+    if (ctl_step) {   // asynchronous ADMM loop: the iteration's control step in the same launch
+        admm_control_step(ctl_step, step_red);
+        return;
+    }
     if (op == 1) {
         st->bnorm2 = res[PR_B2];
         st->gamma = res[PR_RZ];
@@ -810,86 +891,16 @@ hipError_t launch_pcg_pupdate(const Geom& g, const Launch& L, double sigma, int 
 }
 
 hipError_t launch_finalize(hipStream_t s, const double* partials, int nparts, int nr, int nmax, int op, double* out,
-                           PcgState* st, double rtol2, int maxit, const AdmmCtl* ctl) {
-    klaunch(k_finalize, dim3(1), dim3(1024), 0, s, partials, nparts, nr, nmax, op, out, st, rtol2, maxit, ctl);
+                           PcgState* st, double rtol2, int maxit, const AdmmCtl* ctl, AdmmCtl* ctl_step,
+                           const double* step_red) {
+    klaunch(k_finalize, dim3(1), dim3(1024), 0, s, partials, nparts, nr, nmax, op, out, st, rtol2, maxit, ctl, ctl_step,
+            step_red);
     return hipGetLastError();
 }
 
-// One thread: the host loop body of mvtv_admm_run after the reductions, verbatim (same operations
-// in the same order, so decisions match the synchronous loop), then the next iteration's top test.
 __global__ void k_admm_control(AdmmCtl* __restrict__ c, const double* __restrict__ R) {
     if (c->done) return;
-    const double* G = R + ER_N;
-    const double r_norm = sqrt(R[ER_R2]);
-    const double rho = c->rho;
-    c->t_z = c->t_next;
-    c->it += 1;
-    c->counter += 1;
-    double c_next = 1.0, rho_next = rho;
-    int status = 0;
-    const bool fixed = c->fixed_iters > 0;
-    if (c->variant == 0) {   // B: rcpp-code/MultivarTV/src/solvers.cpp:117-125
-        c->dual_norm = fabs(rho) * sqrt(G[GR_S2B]);
-        c->primal_norm = r_norm;
-        c->eps_dual = c->tol * (c->sqrtN + sqrt(G[GR_GU2]));
-        c->eps_pri = c->tol * (c->sqrtE + fmax(sqrt(R[ER_D2]), sqrt(R[ER_A2])));
-        const double tau = 2.0;
-        if (c->primal_norm > 10 * c->dual_norm) {
-            rho_next = tau * rho;
-            c_next = 1.0 / tau;
-        } else if (c->dual_norm > 10 * c->primal_norm) {
-            rho_next = 1.0 / tau * rho;
-            c_next = tau;
-        }
-        c->s_norm = c->dual_norm;
-    } else if (c->variant == 1) {   // A: cpp-code/solvers.cpp:118-126
-        const double s_norm = fabs(rho) * sqrt(G[GR_S2A]);
-        c->dtheta = R[ER_DTH];
-        c->s_norm = s_norm;
-        if (!fixed && c->counter > c->max_counter) {
-            status = 1;
-            rho_next = rho;
-        } else {
-            if (r_norm > 20 * s_norm) {
-                rho_next = 20 * rho;
-                c_next = 0.05;
-            } else if (s_norm > 20 * r_norm) {
-                rho_next = 0.1 * rho;
-                c_next = 10.0;
-            }
-            rho_next = double(int(rho_next));
-        }
-    } else {
-        c->dtheta = R[ER_DTH];
-    }
-    c->r_norm = r_norm;
-    c->c_prev = c_next;
-    c->rho = rho_next;
-    if (c->variant == 0) c->sigma = rho_next;
-    c->t_next = rho_next != 0.0 ? c->lambda / rho_next : INFINITY;
-    if (status) {
-        c->status = 1;
-        c->done = 1;
-        return;
-    }
-    if (c->variant == 0 && !fixed && c->counter > c->max_counter) {
-        c->status = 1;
-        c->done = 1;
-        return;
-    }
-    // loop-top test of the next iteration
-    if (fixed) {
-        if (c->it >= c->fixed_iters) c->done = 1;
-    } else if (c->variant == 0) {
-        if (!(c->dual_norm > c->eps_dual || c->primal_norm > c->eps_pri)) c->done = 1;
-    } else {
-        if (!(c->dtheta > c->tol)) {
-            c->done = 1;
-        } else if (c->variant == 2 && c->it >= c->max_counter) {
-            c->status = 1;
-            c->done = 1;
-        }
-    }
+    admm_control_step(c, R);
 }
 
 hipError_t launch_admm_control(hipStream_t s, AdmmCtl* ctl, const double* red) {
