@@ -406,7 +406,8 @@ mvtv_status pcgs_solve(mvtv_problem* P, double sigma, const double* oty, const d
     const int32_t* skip = &P->st->done;
     // power-of-two m_0 >= 64: the x / r update rides on the preconditioner's first (d = 0) pass and the
     // s^-1 scaling with r.z, |r|^2 on its last, seven launches per iteration instead of nine
-    const bool fused7 = dct_pcg_fusable(P->g, size_t(std::max(kMaxGrid, kMaxCgBlocks)) * kMaxRed);
+    const size_t pwords = size_t(std::max(kMaxGrid, kMaxCgBlocks)) * kMaxRed;
+    const bool fused7 = dct_pcg_fusable(P->g, pwords);
     auto enqueue7 = [&]() -> mvtv_status {
         const int pdim = P->g.p;
         int np_last = 0;
@@ -423,6 +424,7 @@ mvtv_status pcgs_solve(mvtv_problem* P, double sigma, const double* oty, const d
                 f.q = q;
                 f.sinv = sinv;
                 f.partials = P->partials;
+                f.cap = pwords;
                 f.nparts = &np_last;
             }
             const int hh = P->tstart(t == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);

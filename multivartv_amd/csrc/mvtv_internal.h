@@ -244,13 +244,15 @@ struct DctPack {
 // PCG vector work folded into the d = 0 passes of a preconditioner solve (spectrally preconditioned PCG,
 // power-of-two m_0 >= 64): mode 1, first pass (`in` = r): r -= alpha q and x += alpha p on load (r, x
 // written back, the transform taken of sinv * r); mode 2, last pass: out = sinv * transform, (r.z, |r|^2)
-// per workgroup into `partials` (k_finalize op 3 layout, *nparts rows). sinv may be null.
+// per workgroup into `partials` (k_finalize op 3 layout, *nparts rows; a launch whose rows would exceed
+// `cap` words is refused with hipErrorInvalidValue). sinv may be null.
 struct PcgFuse {
     int32_t mode = 0;
     const PcgState* st = nullptr;
     double *x = nullptr, *r = nullptr;
     const double *p = nullptr, *q = nullptr, *sinv = nullptr;
     double* partials = nullptr;
+    size_t cap = 0;
     int* nparts = nullptr;
 };
 // true when the d = 0 passes of this mesh run in k_dct8 with their partial rows within partial_words

@@ -1479,6 +1479,10 @@ static void launch_dct8_tile(SpecArgs& a, hipStream_t s, int mode, bool d0, bool
     const dim3 block(spec8::ShapeK<L, TQW>::NT);
     if constexpr (L >= 6 && spec8::ShapeK<L, TQW>::NT >= 64) {
         if (a.pf.mode) {   // PCG-fused d = 0 passes (dct_pcg_fusable)
+            if (a.pf.mode == 2 && 2 * size_t(grid) > a.pf.cap) {   // the rows would overrun the partials
+                *a.pf.nparts = -1;
+                return;
+            }
             if (a.pf.nparts) *a.pf.nparts = int(grid);
             if (a.pf.mode == 1) klaunch(k_dct8<L, SPEC_FWD, true, false, TQW, 1>, dim3(grid), block, 0, s, a);
             else klaunch(k_dct8<L, SPEC_INV, true, false, TQW, 2>, dim3(grid), block, 0, s, a);
@@ -1629,7 +1633,8 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     const bool formb = ga != nullptr;
     if (m > 4096) return hipErrorInvalidValue;
     if (pf && pf->mode) {   // PCG-fused d = 0 pass (dct_pcg_fusable meshes): k_dct8 only
-        if (d != 0 || formb || pack || (1u << a.L) != m || a.L < 6 || mode != (pf->mode == 1 ? SPEC_FWD : SPEC_INV))
+        if (d != 0 || formb || pack || (1u << a.L) != m || a.L < 6 || mode != (pf->mode == 1 ? SPEC_FWD : SPEC_INV) ||
+            (pf->mode == 2 && !pf->nparts))
             return hipErrorInvalidValue;
         a.pf = *pf;
     }
@@ -1677,6 +1682,7 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
             case 11: launch_dct8<11>(a, s, mode, d == 0, formb); break;
             case 12: launch_dct8<12>(a, s, mode, d == 0, formb); break;
         }
+        if (pf && pf->mode == 2 && *pf->nparts < 0) return hipErrorInvalidValue;
         return hipGetLastError();
     }
     int tq = std::max(2, std::min(16, int(spec::LDS_WORDS / m)));
