@@ -437,9 +437,10 @@ mvtv_status pcgs_solve(mvtv_problem* P, double sigma, const double* oty, const d
     };
     auto enqueue = [&]() -> mvtv_status {
         int hh = P->tstart(MVTV_K_PCG_APPLY);
-        HIP_TRY(launch_apply_A(P->g, L, sigma, P->wmode, P->wdiag, p, q, P->partials, P->st));   // q = A p, p.q
+        int npa = L.grid;
+        HIP_TRY(launch_apply_A(P->g, L, sigma, P->wmode, P->wdiag, p, q, P->partials, P->st, &npa));   // q = A p, p.q
         P->tstop(hh);
-        HIP_TRY(launch_finalize(P->stream, P->partials, L.grid, 1, 0, 2, nullptr, P->st));         // alpha
+        HIP_TRY(launch_finalize(P->stream, P->partials, npa, 1, 0, 2, nullptr, P->st));              // alpha
         if (fused7) {
             MVTV_TRY(enqueue7());
             hh = P->tstart(MVTV_K_PCG_DIRECTION);

@@ -434,26 +434,31 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
 // two in-plane sums of the 8-weight symmetric stencil (dz = 0 layer, dz = +-1 layer); q(z) =
 // s1(z-1) + s0(z) + s1(z+1) with half-sample mirrored neighbours (the Neumann structure of
 // D^T D, as in k_cg3d). 2N words of HBM traffic against ~27 L2 reads per cell of the generic
-// grid-stride k_apply_A.
+// grid-stride k_apply_A. DOT (the PCG operator step): x.q per workgroup into `partials` (every
+// workgroup of the grid writes its row) and a no-op once the PCG state is done.
 struct Apply3dArgs {
     const double* x;
     double* q;
     const double* wdiag;
+    double* partials;
+    const PcgState* st;
     double K[8];
     int m0, m1, m2, tiles_x, tiles_y, zchunk, nblocks;
 };
 
-template <int WM>
+template <int WM, bool DOT>
 __global__ __launch_bounds__(256) void k_apply3d(const Apply3dArgs a) {
+    if (DOT && a.st->done) return;
     const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-    if (bid >= a.nblocks) return;
     const int nt = a.tiles_x * a.tiles_y;
     const int tz = bid / nt, rem = bid - tz * nt;
     const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
     const int x = tx * 64 + int(threadIdx.x & 63), y = ty * 4 + int(threadIdx.x >> 6);
     const int m0 = a.m0, m1 = a.m1, m2 = a.m2;
-    if (x >= m0 || y >= m1) return;   // no barriers below
-    const int z0 = tz * a.zchunk, z1 = min(m2, z0 + a.zchunk);
+    double red[1] = {0.0};
+    const bool act = bid < a.nblocks && x < m0 && y < m1;
+    if (!DOT && !act) return;   // no barriers below without DOT
+    const int z0 = tz * a.zchunk, z1 = act ? min(m2, z0 + a.zchunk) : z0;
     const size_t pl = size_t(m0) * size_t(m1);
     const int xl = mirror(x - 1, m0), xr = mirror(x + 1, m0);
     const size_t yd = size_t(mirror(y - 1, m1)) * m0, yc = size_t(y) * m0, yu = size_t(mirror(y + 1, m1)) * m0;
@@ -469,10 +474,12 @@ __global__ __launch_bounds__(256) void k_apply3d(const Apply3dArgs a) {
         s0 = fma(K0, c, fma(K1, h, fma(K2, v, K3 * d)));
         s1 = fma(K4, c, fma(K5, h, fma(K6, v, K7 * d)));
     };
-    double s0c, s1c, s0n, s1n, s1m;
-    sums(z0, s0c, s1c);
-    if (z0 > 0) sums(z0 - 1, s0n, s1m);
-    else s1m = s1c;
+    double s0c = 0.0, s1c = 0.0, s0n = 0.0, s1n = 0.0, s1m = 0.0;
+    if (act) {
+        sums(z0, s0c, s1c);
+        if (z0 > 0) sums(z0 - 1, s0n, s1m);
+        else s1m = s1c;
+    }
     for (int z = z0; z < z1; ++z) {
         if (z + 1 < m2) sums(z + 1, s0n, s1n);
         else s1n = s1c, s0n = s0c;
@@ -480,14 +487,16 @@ __global__ __launch_bounds__(256) void k_apply3d(const Apply3dArgs a) {
         double out = s1m + s0c + s1n;
         if (WM == W_DIAG) out = fma(a.wdiag[i], a.x[i], out);
         __builtin_nontemporal_store(out, a.q + i);
+        if constexpr (DOT) red[0] = fma(a.x[i], out, red[0]);
         s1m = s1c;
         s0c = s0n;
         s1c = s1n;
     }
+    if constexpr (DOT) block_reduce_store<1, 0>(red, a.partials);
 }
 
 hipError_t launch_apply3d(const Geom& g, hipStream_t s, double sigma, int wmode, const double* wdiag,
-                          const double* x, double* q) {
+                          const double* x, double* q, double* partials, const PcgState* st, int* nparts) {
     Apply3dArgs a{};
     a.m0 = int(g.m[0]);
     a.m1 = int(g.m[1]);
@@ -516,8 +525,17 @@ hipError_t launch_apply3d(const Geom& g, hipStream_t s, double sigma, int wmode,
     a.x = x;
     a.q = q;
     a.wdiag = wdiag;
-    if (wmode == W_DIAG) klaunch(k_apply3d<W_DIAG>, dim3(grid), dim3(256), 0, s, a);
-    else klaunch(k_apply3d<W_NONE>, dim3(grid), dim3(256), 0, s, a);
+    a.partials = partials;
+    a.st = st;
+    if (partials) {
+        if (!st || !nparts) return hipErrorInvalidValue;
+        *nparts = grid;
+        if (wmode == W_DIAG) klaunch(k_apply3d<W_DIAG, true>, dim3(grid), dim3(256), 0, s, a);
+        else klaunch(k_apply3d<W_NONE, true>, dim3(grid), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+    if (wmode == W_DIAG) klaunch(k_apply3d<W_DIAG, false>, dim3(grid), dim3(256), 0, s, a);
+    else klaunch(k_apply3d<W_NONE, false>, dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -821,7 +821,7 @@ hipError_t launch_edges_fill_valid(const Geom& g, int order, const Launch& L, do
 }
 
 hipError_t launch_apply_A(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
-                          const double* x, double* q, double* partials, const PcgState* st) {
+                          const double* x, double* q, double* partials, const PcgState* st, int* nparts) {
     // plain operator application on a whole 3-D mesh: the z-marching kernel (MVTV_APPLY3D=0: generic)
     static const bool a3d = [] {
         const char* e = probe_env("MVTV_APPLY3D");
@@ -829,6 +829,9 @@ hipError_t launch_apply_A(const Geom& g, const Launch& L, double sigma, int wmod
     }();
     if (a3d && g.p == 3 && !partials && g.ibeg == 0 && g.iend == g.N)
         return launch_apply3d(g, L.stream, sigma, wmode, wdiag, x, q);
+    if (a3d && g.p == 3 && partials && st && nparts && g.ibeg == 0 && g.iend == g.N)
+        return launch_apply3d(g, L.stream, sigma, wmode, wdiag, x, q, partials, st, nparts);
+    if (nparts) *nparts = L.grid;
     const StencilK sk = make_stencil(g);
     return dispatch_p(g.p, [&](auto pc) {
         constexpr int P = decltype(pc)::value;
