@@ -539,4 +539,100 @@ hipError_t launch_apply3d(const Geom& g, hipStream_t s, double sigma, int wmode,
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------ k_apply2d
+// The same for p = 2 (configs 2 and 4: the PCG operator step of a CV fold): a thread owns one dim-0
+// column over a chunk of >= 8 rows and marches dim 1; a row contributes s0 = K0 c + K1 (l + r) to its own
+// output and s1 = K2 c + K3 (l + r) to the rows above and below (K indexed by |dx| + 2 |dy|), with the
+// half-sample mirror at the ends. 2N words against the 9 L2 reads per cell of the generic stencil.
+struct Apply2dArgs {
+    const double* x;
+    double* q;
+    const double* wdiag;
+    double* partials;
+    const PcgState* st;
+    double K[4];
+    int m0, m1, tiles_x, ychunk, nblocks;
+};
+
+template <int WM, bool DOT>
+__global__ __launch_bounds__(256) void k_apply2d(const Apply2dArgs a) {
+    if (DOT && a.st->done) return;
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const int ty = bid / a.tiles_x, tx = bid - ty * a.tiles_x;
+    const int x = tx * 256 + int(threadIdx.x);
+    const int m0 = a.m0, m1 = a.m1;
+    double red[1] = {0.0};
+    const bool act = bid < a.nblocks && x < m0;
+    if (!DOT && !act) return;   // no barriers below without DOT
+    const int y0 = ty * a.ychunk, y1 = act ? min(m1, y0 + a.ychunk) : y0;
+    const int xl = mirror(x - 1, m0), xr = mirror(x + 1, m0);
+    const double K0 = a.K[0], K1 = a.K[1], K2 = a.K[2], K3 = a.K[3];
+    auto sums = [&](int y, double& s0, double& s1) {
+        const double* R = a.x + size_t(y) * size_t(m0);
+        const double c = R[x], h = R[xl] + R[xr];
+        s0 = fma(K0, c, K1 * h);
+        s1 = fma(K2, c, K3 * h);
+    };
+    double s0c = 0.0, s1c = 0.0, s0n = 0.0, s1n = 0.0, s1m = 0.0;
+    if (act) {
+        sums(y0, s0c, s1c);
+        if (y0 > 0) sums(y0 - 1, s0n, s1m);
+        else s1m = s1c;
+    }
+    for (int y = y0; y < y1; ++y) {
+        if (y + 1 < m1) sums(y + 1, s0n, s1n);
+        else s1n = s1c, s0n = s0c;
+        const size_t i = size_t(y) * size_t(m0) + size_t(x);
+        double out = s1m + s0c + s1n;
+        if (WM == W_DIAG) out = fma(a.wdiag[i], a.x[i], out);
+        __builtin_nontemporal_store(out, a.q + i);
+        if constexpr (DOT) red[0] = fma(a.x[i], out, red[0]);
+        s1m = s1c;
+        s0c = s0n;
+        s1c = s1n;
+    }
+    if constexpr (DOT) block_reduce_store<1, 0>(red, a.partials);
+}
+
+hipError_t launch_apply2d(const Geom& g, hipStream_t s, double sigma, int wmode, const double* wdiag,
+                          const double* x, double* q, double* partials, const PcgState* st, int* nparts) {
+    Apply2dArgs a{};
+    a.m0 = int(g.m[0]);
+    a.m1 = int(g.m[1]);
+    a.tiles_x = (a.m0 + 255) / 256;
+    int ny = std::max(1, std::min(std::max(1, a.m1 / 8), 8192 / a.tiles_x));   // >= 8 rows per chunk
+    a.ychunk = (a.m1 + ny - 1) / ny;
+    ny = (a.m1 + a.ychunk - 1) / a.ychunk;
+    a.nblocks = a.tiles_x * ny;
+    const int grid = (a.nblocks + 7) / 8 * 8;
+    for (int t = 0; t < 4; ++t) {   // K(|dx|, |dy|) = sigma sum_S cS[S] prod_j f_j, t = |dx| + 2 |dy|
+        double kk = 0.0;
+        for (int S = 1; S < 4; ++S) {
+            double prod = g.cS[S];
+            for (int j = 0; j < 2; ++j) {
+                const bool off = (t >> j) & 1;
+                prod *= ((S >> j) & 1) ? (off ? -1.0 : 2.0) : (off ? 0.0 : 1.0);
+            }
+            kk += prod;
+        }
+        a.K[t] = sigma * kk;
+    }
+    if (wmode == W_IDENTITY) a.K[0] += 1.0;
+    a.x = x;
+    a.q = q;
+    a.wdiag = wdiag;
+    a.partials = partials;
+    a.st = st;
+    if (partials) {
+        if (!st || !nparts || grid > kMaxCgBlocks * kMaxRed) return hipErrorInvalidValue;
+        *nparts = grid;
+        if (wmode == W_DIAG) klaunch(k_apply2d<W_DIAG, true>, dim3(grid), dim3(256), 0, s, a);
+        else klaunch(k_apply2d<W_NONE, true>, dim3(grid), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+    if (wmode == W_DIAG) klaunch(k_apply2d<W_DIAG, false>, dim3(grid), dim3(256), 0, s, a);
+    else klaunch(k_apply2d<W_NONE, false>, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 }  // namespace mvtv

@@ -173,8 +173,8 @@ hipError_t launch_edge_update(const Geom& g, int order, int umode, const Launch&
 hipError_t launch_gather(const Geom& g, int order, int umode, const Launch& L, const double* edges, double t,
                          double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
                          const AdmmCtl* ctl = nullptr);
-// partials: x.q per workgroup, L.grid rows, or *nparts rows when nparts is given (then a whole 3-D mesh
-// takes the z-marching k_apply3d)
+// partials: x.q per workgroup, L.grid rows, or *nparts rows when nparts is given (then a whole 2-D / 3-D
+// mesh takes the marching k_apply2d / k_apply3d)
 hipError_t launch_apply_A(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
                           const double* x, double* q, double* partials, const PcgState* st, int* nparts = nullptr);
 hipError_t launch_pcg_init(const Geom& g, const Launch& L, double sigma, int wmode, const double* wdiag,
@@ -197,6 +197,10 @@ hipError_t launch_finalize(hipStream_t s, const double* partials, int nparts, in
 hipError_t launch_admm_control(hipStream_t s, AdmmCtl* ctl, const double* red);
 // fused 3-D Chronopoulos-Gear PCG (mvtv_cg3d.hip): mode 0 prologue, 1 first iteration, 2 iteration;
 // partials get 4 values per workgroup (gamma, delta, |r|^2, |b|^2), *nblocks_out workgroups
+// z-marching q = (W + sigma D^T D) x for p = 2, same contract as launch_apply3d
+hipError_t launch_apply2d(const Geom& g, hipStream_t s, double sigma, int wmode, const double* wdiag,
+                          const double* x, double* q, double* partials = nullptr, const PcgState* st = nullptr,
+                          int* nparts = nullptr);
 // partials (with st, nparts): x.q per workgroup (*nparts rows), a no-op once st->done
 hipError_t launch_apply3d(const Geom& g, hipStream_t s, double sigma, int wmode, const double* wdiag,
                           const double* x, double* q, double* partials = nullptr, const PcgState* st = nullptr,

@@ -831,6 +831,8 @@ hipError_t launch_apply_A(const Geom& g, const Launch& L, double sigma, int wmod
         return launch_apply3d(g, L.stream, sigma, wmode, wdiag, x, q);
     if (a3d && g.p == 3 && partials && st && nparts && g.ibeg == 0 && g.iend == g.N)
         return launch_apply3d(g, L.stream, sigma, wmode, wdiag, x, q, partials, st, nparts);
+    if (a3d && g.p == 2 && g.ibeg == 0 && g.iend == g.N && (!partials || (st && nparts)))
+        return launch_apply2d(g, L.stream, sigma, wmode, wdiag, x, q, partials, st, nparts);
     if (nparts) *nparts = L.grid;
     const StencilK sk = make_stencil(g);
     return dispatch_p(g.p, [&](auto pc) {
