@@ -254,7 +254,7 @@ def slab_main(a):
                        "theta_solver": "spectral (distributed: all-to-all transposes of the last dimension)",
                        "parallelism": f"slab x{nranks} ({transport}: halo planes, all-to-all, 7-sum all-reduce)"},
             "roofline": roof, "kernels_rank0": per,
-            "residuals": {"r_norm": st["r_norm"], "s_norm": st["s_norm"]}, "cpu_baseline": None}), flush=True)
+            "residuals": {"r_norm": st["r_norm"], "s_norm": st["s_norm"]}, "cpu_baseline": None}), file=OUT, flush=True)
     D.close()
 
 
@@ -321,7 +321,7 @@ def cv_main(a):
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
                          "bytes_per_launch": tim[dom]["bytes_per_launch"], "avg_launch_ms": round(d_avg, 4),
                          "mall_resident": 8 * N * 7 < 256 * 2 ** 20},
-            "kernels": kern, "cpu_baseline": None}), flush=True)
+            "kernels": kern, "cpu_baseline": None}), file=OUT, flush=True)
     D.close()
 
 
@@ -457,9 +457,23 @@ def main():
                           "pcg_unconverged": int(n_unconv)},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=OUT, flush=True)
     D.close()
 
 
+# The stream of the one JSON line: fd 1 as the process started (main() below points fd 1 at stderr, so
+# what libraries print to stdout, e.g. RCCL's version banner when a communicator is created, cannot land
+# beside the line).
+OUT = sys.stdout
+
+
+def _json_stdout():
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 if __name__ == "__main__":
+    OUT = _json_stdout()
     main()
