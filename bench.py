@@ -11,12 +11,14 @@ Other BASELINE configs: ``--dims 2 --size 1024`` (config 2), ``--dims 3 --size 2
 ``--dims 4 --size 128`` (config 5 on one GPU) and ``--mode cv`` (config 4's work item: a CV fold's
 warm-started lambda chunk on 2048^2 with a 0/1 fold mask W, so the theta-solve is Jacobi-PCG).
 
-Multi-GPU (torchrun, one process per GPU): every rank fits its own independent
-512^3 mesh (noise seed + rank) — the embarrassingly parallel "independent mesh
-fits" sharding of the north star — so value = total iterations/s of all ranks
-and scaling is weak. torch.distributed (RCCL by default, MVTV_DIST_BACKEND=gloo
-for host scalars) provides the barriers, the max-over-ranks time and the final
-global residual all-reduce.
+Multi-GPU (one process per GPU; ``--gpus N`` starts the N rank processes itself when it is not run
+under torchrun). At N > 1 the headline is the metric's own definition: ONE 512^3 mesh
+slab-decomposed over the N GPUs (``scaling: strong``; the whole loop inside libmvtv with RCCL on the
+solver stream). Before it every rank also fits its own independent 512^3 mesh (noise seed + rank, the
+embarrassingly parallel sharding of the north star); that aggregate is reported beside the headline as
+``independent_fits`` (``scaling: weak``). One RCCL per process: torch.distributed runs on gloo (host
+barriers, max-over-ranks time, the 128-byte RCCL id) and every device collective goes through libmvtv's
+communicator (``rccl_ranks`` = its size), whose RCCL is the copy torch already mapped.
 """
 from __future__ import annotations
 
@@ -31,14 +33,72 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import multivartv_amd as mv  # noqa: E402  (load libmvtv before anything that brings its own HIP runtime)
-from multivartv_amd.synth import SEED, towers  # noqa: E402
-
+mv = None                  # multivartv_amd, imported by _import_mv() (after the rank launcher)
+SEED = towers = None
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def _import_mv():
+    """libmvtv is loaded before anything that brings its own HIP runtime; never in the launcher process."""
+    global mv, SEED, towers
+    import multivartv_amd
+    from multivartv_amd import synth
+    mv, SEED, towers = multivartv_amd, synth.SEED, synth.towers
+
+
+def _spawn_ranks(n, argv, dry_run=False):
+    """``--gpus N`` (N > 1) outside torchrun: start N rank processes of this script, one per GPU, with the
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* environment torchrun would give them. This process imports
+    nothing that touches HIP. Rank 0 inherits stdout (the one JSON line); the other ranks' stdout goes to
+    stderr. When a rank fails the others are ended (they would wait for it in a collective) and the launcher
+    exits non-zero."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out = None if (r == 0 or dry_run) else sys.stderr
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env, stdout=out))
+    rc = 0
+    while procs:
+        time.sleep(0.2)
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                log(f"bench.py launcher: a rank exited with status {code}; ending the others")
+                for q in procs:
+                    q.send_signal(signal.SIGTERM)
+                deadline = time.time() + 30
+                for q in procs:
+                    try:
+                        q.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+    return rc
+
+
+def _dry_run(a):
+    """--dry-run (CPU test of the launcher): report the rank plumbing, optionally fail one rank."""
+    env = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    print(json.dumps({"dry_run": True, "gpus": a.gpus, "mode": a.mode, "env": env,
+                      "mv_imported": "multivartv_amd" in sys.modules}), file=OUT, flush=True)
+    if a.dry_run_fail_rank >= 0 and int(env["RANK"] or 0) == a.dry_run_fail_rank:
+        sys.exit(3)
+    if a.dry_run_fail_rank >= 0:
+        time.sleep(60)   # a healthy rank waiting for its failed peer: the launcher must end it
 
 
 def parse():
@@ -56,19 +116,25 @@ def parse():
                          "spectral = the exact solve (--mode cv: the spectrally preconditioned PCG)")
     ap.add_argument("--pcg-steps", type=int, default=10,
                     help="steps of the secondary Jacobi-PCG leg reported beside the main one (0 = skip)")
-    ap.add_argument("--mode", choices=["independent", "slab", "cv"], default="independent",
-                    help="N > 1: independent fits per GPU (weak scaling, default) or one mesh slab-decomposed "
-                         "over the GPUs (strong scaling; RCCL halo exchange + all-to-all transposes)")
+    ap.add_argument("--mode", choices=["auto", "independent", "slab", "cv"], default="auto",
+                    help="auto: N = 1 one fit; N > 1 one mesh slab-decomposed over the GPUs (strong scaling, the "
+                         "metric) with the independent fits per GPU (weak scaling) reported beside it. "
+                         "independent / slab: only that one")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--slab-ranks", type=int, default=1,
                     help="--mode slab without torchrun: ranks of an in-process rehearsal on one GPU (1: RCCL, one rank)")
     ap.add_argument("--cpu-planes", type=int, default=0,
                     help="cpu_baseline sample: slowest-dim planes of the mesh (0 = a quarter of them)")
     ap.add_argument("--cpu-full", action="store_true", help="cpu_baseline on the whole mesh (no extrapolation)")
+    ap.add_argument("--dry-run", action="store_true", help="launcher test: ranks report their env and exit")
+    ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
 class Dist:
+    """Host-side plumbing of the ranks over torch.distributed on gloo (barriers, max-over-ranks time, the
+    RCCL id): no torch RCCL communicator, so the process's one RCCL is libmvtv's."""
+
     def __init__(self, backend="gloo"):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
@@ -117,6 +183,16 @@ def load_pmc(name):
         return None, None
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(m, lam, pcg_iters, planes, full=False):
     """The CPU oracle on the host cores, one ADMM iteration (variant B) of the same towers problem:
       * spectral (the headline's like-for-like): oracle/c/mvtv_oracle.c's loop with the exact theta-solve
@@ -160,6 +236,7 @@ def cpu_baseline(m, lam, pcg_iters, planes, full=False):
                                            f"{scale:.0f}")
     best_spec = t_spec <= t_pcg
     return dict(value=1.0 / (min(t_spec, t_pcg) * scale), unit="iters/s", cores=ncores, kind="port",
+                cpu_model=_cpu_model(), host_cpus=os.cpu_count(), omp_num_threads=os.environ.get("OMP_NUM_THREADS"),
                 algorithm="spectral" if best_spec else f"Jacobi-PCG x {int(pcg_iters)}",
                 sample=(f"1 ADMM iteration (variant B) of the same towers problem on {where}, "
                         f"{ncores} threads: oracle/c/mvtv_oracle.c loop with the faster of its two theta-solves "
@@ -171,24 +248,47 @@ def cpu_baseline(m, lam, pcg_iters, planes, full=False):
                 spectral_seconds=round(t_spec, 2))
 
 
-def slab_main(a):
-    """One mesh decomposed over the ranks: strong scaling. Every rank runs the whole
-    ADMM loop inside libmvtv (mvtv_slab_run) with RCCL collectives on its stream. World size 1 (no torchrun):
-    --slab-ranks R > 1 rehearses an R-rank decomposition on the one GPU with the in-process loopback
-    transport; R = 1 runs the slab loop over a one-rank RCCL communicator."""
+METRIC = "ADMM iters/sec on 512^3 fp64 mesh; achieved HBM GB/s vs peak at 1/2/4/8 GPUs"
+
+
+def _roofline(tim):
+    """The dominant kernel (by time) of a timing table and its achieved algorithmic GB/s."""
+    cand = [k for k in tim if tim[k]["bytes_per_launch"] > 0 and tim[k]["launches"]]
+    if not cand:
+        return None
+    dom = max(cand, key=lambda k: tim[k]["ms"])
+    d_avg = tim[dom]["ms"] / tim[dom]["launches"]
+    achieved = tim[dom]["bytes_per_launch"] / (d_avg * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "bytes_per_launch": tim[dom]["bytes_per_launch"], "avg_launch_ms": round(d_avg, 4)}
+
+
+def _rccl_comm(D, dev):
+    """libmvtv's RCCL communicator over the ranks (the 128-byte id broadcast over gloo)."""
+    from multivartv_amd import slab
+    return slab.Comm.rccl(dev) if D.dist else slab.Comm.rccl_single(dev)
+
+
+def slab_main(a, D, comm=None):
+    """One mesh decomposed over the ranks (the metric at 2/4/8 GPUs): strong scaling.
+    Every rank runs the whole ADMM loop inside libmvtv (mvtv_slab_run) with RCCL collectives on its stream.
+    World size 1: --slab-ranks R > 1 rehearses an R-rank decomposition on the one GPU with the in-process
+    loopback transport; R = 1 runs the slab loop over a one-rank RCCL communicator. Returns rank 0's line."""
     from multivartv_amd import slab
     m = [a.size] * a.dims
     lam = a.lam
     deltas = [(1.0 + 2e-4) / v for v in m]
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
-        D = Dist("nccl")
+    R = max(1, a.slab_ranks)
+    if D.world > 1 or R == 1:
         dev = D.local % max(1, mv.device_count())
+        own = comm is None
+        if own:
+            comm = _rccl_comm(D, dev)
         b = slab.plane_bounds(m[-1], D.world)
         pl = int(np.prod(m[:-1]))
         y = towers(m, start=int(b[D.rank]) * pl, count=int(b[D.rank + 1] - b[D.rank]) * pl)
         ysum, = D.allreduce([float(y.sum())], "sum")
-        comm = slab.Comm.rccl(dev)
         S = slab.SlabADMM(m, y, deltas, ysum / float(np.prod(m)), comm, device=dev)
         del y
         if a.warmup > 0:
@@ -196,69 +296,46 @@ def slab_main(a):
         D.barrier()
         S.P.timing(True)
         t0 = time.perf_counter()
-        st = S.run(lam, fixed_iters=a.steps)
+        st = S.run(lam, fixed_iters=a.steps)   # returns after the stream drained
         t1 = time.perf_counter()
         D.barrier()
         tim = S.P.timings()
         S.P.timing(False)
         g_elapsed, = D.allreduce([t1 - t0], "max")
-        rank, nranks, transport = D.rank, D.world, "RCCL"
+        nranks, rccl_ranks = D.world, comm.size
+        transport = "RCCL" if D.world > 1 else "RCCL (one rank)"
         S.close()
-        comm.close()
-    else:
-        D = Dist("gloo")
-        R = max(1, a.slab_ranks)
-        y = towers(m)
-        if R == 1:
-            comm = slab.Comm.rccl_single(0)
-            S = slab.SlabADMM(m, y, deltas, float(y.mean()), comm, device=0)
-            del y
-            if a.warmup > 0:
-                S.run(lam, fixed_iters=a.warmup)
-            S.P.timing(True)
-            t0 = time.perf_counter()
-            st = S.run(lam, fixed_iters=a.steps)
-            t1 = time.perf_counter()
-            tim = S.P.timings()
-            S.close()
+        if own:
             comm.close()
-            transport = "RCCL (one rank)"
-        else:
-            if a.warmup > 0:
-                slab.run_local_group(m, y, deltas, lam, R, fixed_iters=a.warmup)
-            t0 = time.perf_counter()
-            outs, _ = slab.run_local_group(m, y, deltas, lam, R, fixed_iters=a.steps)
-            t1 = time.perf_counter()
-            st, tim = outs[0], {}
-            transport = f"in-process loopback, {R} ranks on one GPU"
-        g_elapsed, rank, nranks = t1 - t0, 0, R
+    else:
+        y = towers(m)
+        if a.warmup > 0:
+            slab.run_local_group(m, y, deltas, lam, R, fixed_iters=a.warmup)
+        t0 = time.perf_counter()
+        outs, _ = slab.run_local_group(m, y, deltas, lam, R, fixed_iters=a.steps)
+        t1 = time.perf_counter()
+        st, tim = outs[0], {}
+        transport = f"in-process loopback, {R} ranks on one GPU"
+        g_elapsed, nranks, rccl_ranks = t1 - t0, R, 0
     per = {k: dict(avg_ms=round(v["ms"] / v["launches"], 4), launches=v["launches"]) for k, v in tim.items()
            if v["launches"]}
-    roof = None
-    if any(v["bytes_per_launch"] > 0 and v["launches"] for v in tim.values()):
-        dom = max((k for k in tim if tim[k]["bytes_per_launch"] > 0 and tim[k]["launches"]), key=lambda k: tim[k]["ms"])
-        d_avg = tim[dom]["ms"] / tim[dom]["launches"]
-        achieved = tim[dom]["bytes_per_launch"] / (d_avg * 1e-3) / 1e9
-        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                "bytes_per_launch": tim[dom]["bytes_per_launch"], "avg_launch_ms": round(d_avg, 4)}
-    if rank == 0:
-        print(json.dumps({
-            "metric": "ADMM iters/sec on 512^3 fp64 mesh; achieved HBM GB/s vs peak at 1/2/4/8 GPUs",
-            "value": round(a.steps / g_elapsed, 4), "unit": "iters/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(g_elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: towers + 0.5 N(0,1) (splitmix64/Box-Muller, seed 0x4D565456), O = I",
-            "config": {"workload": f"{a.dims}D {a.size}^{a.dims} fp64 mesh-TV ADMM, variant B, lambda={lam}, one mesh "
-                                   f"slab-decomposed along dim {a.dims - 1} over {nranks} ranks", "mesh": m,
-                       "theta_solver": "spectral (distributed: all-to-all transposes of the last dimension)",
-                       "parallelism": f"slab x{nranks} ({transport}: halo planes, all-to-all, 7-sum all-reduce)"},
-            "roofline": roof, "kernels_rank0": per,
-            "residuals": {"r_norm": st["r_norm"], "s_norm": st["s_norm"]}, "cpu_baseline": None}), file=OUT, flush=True)
-    D.close()
+    if D.rank != 0:
+        return None
+    return {
+        "metric": METRIC, "value": round(a.steps / g_elapsed, 4), "unit": "iters/s", "n_gpus": D.world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(g_elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: towers + 0.5 N(0,1) (splitmix64/Box-Muller, seed 0x4D565456), O = I",
+        "config": {"workload": f"{a.dims}D {a.size}^{a.dims} fp64 mesh-TV ADMM, variant B, lambda={lam}, one mesh "
+                               f"slab-decomposed along dim {a.dims - 1} over {nranks} ranks", "mesh": m,
+                   "theta_solver": "spectral (distributed: all-to-all transposes of the last dimension)",
+                   "parallelism": f"slab x{nranks} ({transport}: halo planes, all-to-all, 7-sum all-reduce)"},
+        "rccl_ranks": rccl_ranks, "rccl_library": slab.Comm.library() if rccl_ranks else None,
+        "roofline": _roofline(tim), "kernels_rank0": per,
+        "residuals": {"r_norm": st["r_norm"], "s_norm": st["s_norm"]}, "cpu_baseline": None}
 
 
-def cv_main(a):
+def cv_main(a, D):
     """Config 4's work item (BASELINE.json: 2D 2048^2, 32-lambda CV path batched over 8 GPUs): on each rank
     one CV fold's warm-started lambda chunk (rcpp…/solvers.cpp:340-353 -> mbs_path :204-222). Fold
     (rank % 5) of kfoldinds drops 1/5 of the lattice points, so W = O^T O is a 0/1 mask and the theta-solve
@@ -266,7 +343,6 @@ def cv_main(a):
     GPU, 1e-4 lambda_max .. lambda_max); rank r takes lambdas [4r, 4r+4) (mod 32) and runs steps/4 fixed ADMM
     iterations at each, theta / u / rho carried (one mvtv_path call). value = ADMM iterations/s of all ranks."""
     from multivartv_amd import cv as mcv
-    D = Dist(os.environ.get("MVTV_DIST_BACKEND", "nccl"))
     m = [a.size] * a.dims
     y = towers(m)
     fold = mcv.kfoldinds(y.size, 5, seed=0)
@@ -295,49 +371,34 @@ def cv_main(a):
     P.timing(False)
     g_elapsed, = D.allreduce([t1 - t0], "max")
     kbar = sum(st["pcg_iters"] for st in stats) / steps
-    dom = max((k for k in tim if tim[k]["bytes_per_launch"] > 0 and tim[k]["launches"]), key=lambda k: tim[k]["ms"])
-    d_avg = tim[dom]["ms"] / tim[dom]["launches"]
-    achieved = tim[dom]["bytes_per_launch"] / (d_avg * 1e-3) / 1e9
+    roof = _roofline(tim)
+    roof["mall_resident"] = 8 * P.N * 7 < 256 * 2 ** 20
     kern = {k: dict(avg_ms=round(v["ms"] / v["launches"], 4), launches=v["launches"],
                     share=round(v["ms"] / ((t1 - t0) * 1e3), 4)) for k, v in tim.items() if v["launches"]}
     N = P.N
     P.close()
-    if D.rank == 0:
-        print(json.dumps({
-            "metric": "ADMM iters/sec on 512^3 fp64 mesh; achieved HBM GB/s vs peak at 1/2/4/8 GPUs",
-            "value": round(D.world * steps / g_elapsed, 4), "unit": "iters/s", "n_gpus": D.world, "steps": steps,
-            "warmup": a.warmup, "ms_per_step": round(g_elapsed / steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: 2D towers + 0.5 N(0,1) on the lattice, CV fold mask W (kfoldinds seed 0), O = I on the "
-                    "training rows",
-            "config": {"workload": f"config 4 work item: {a.dims}D {a.size}^{a.dims} CV fold (rank % 5) lambda chunk, "
-                                   f"4 lambdas x {per} fixed iterations, warm-started, variant B",
-                       "mesh": m, "nodes": N, "lambdas": [float(v) for v in chunk],
-                       "theta_solver": {mv.SOLVER_PCG: "jacobi_pcg", mv.SOLVER_PCG_SPECTRAL: "pcg_spectral"}.get(
-                           stats[0]["theta_solver"], "?"),
-                       "pcg_rtol": a.pcg_rtol, "pcg_iters_mean": round(kbar, 2), "rho_out": [float(r) for r in rhos],
-                       "parallelism": f"fold / lambda-chunk work items, one per GPU (x{D.world})"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                         "bytes_per_launch": tim[dom]["bytes_per_launch"], "avg_launch_ms": round(d_avg, 4),
-                         "mall_resident": 8 * N * 7 < 256 * 2 ** 20},
-            "kernels": kern, "cpu_baseline": None}), file=OUT, flush=True)
-    D.close()
+    if D.rank != 0:
+        return None
+    return {
+        "metric": METRIC, "value": round(D.world * steps / g_elapsed, 4), "unit": "iters/s", "n_gpus": D.world,
+        "steps": steps, "warmup": a.warmup, "ms_per_step": round(g_elapsed / steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: 2D towers + 0.5 N(0,1) on the lattice, CV fold mask W (kfoldinds seed 0), O = I on the "
+                "training rows",
+        "config": {"workload": f"config 4 work item: {a.dims}D {a.size}^{a.dims} CV fold (rank % 5) lambda chunk, "
+                               f"4 lambdas x {per} fixed iterations, warm-started, variant B",
+                   "mesh": m, "nodes": N, "lambdas": [float(v) for v in chunk],
+                   "theta_solver": {mv.SOLVER_PCG: "jacobi_pcg", mv.SOLVER_PCG_SPECTRAL: "pcg_spectral"}.get(
+                       stats[0]["theta_solver"], "?"),
+                   "pcg_rtol": a.pcg_rtol, "pcg_iters_mean": round(kbar, 2), "rho_out": [float(r) for r in rhos],
+                   "parallelism": f"fold / lambda-chunk work items, one per GPU (x{D.world})"},
+        "roofline": roof, "kernels": kern, "cpu_baseline": None}
 
 
-def main():
-    a = parse()
-    if a.mode == "cv":
-        if a.size == 512 and a.dims == 3:   # config 4's shape unless given
-            a.dims, a.size = 2, 2048
-        return cv_main(a)
-    if a.mode == "slab":
-        return slab_main(a)
-    # the independent fits share nothing but the barrier, the max time and the final residual
-    # all-reduce: RCCL (device scalars) by default, MVTV_DIST_BACKEND=gloo for host scalars
-    D = Dist(os.environ.get("MVTV_DIST_BACKEND", "nccl"))
-    if mv.device_count() < 1:
-        raise SystemExit("bench.py: no HIP device")
+def independent_main(a, D, comm=None):
+    """Every rank fits its own 512^3 mesh (noise seed + rank): the north star's independent mesh fits,
+    weak scaling. The global residual all-reduce goes over libmvtv's RCCL communicator when there is one.
+    Returns rank 0's line."""
     m = [a.size] * a.dims
     lam = a.lam
     t_setup = time.perf_counter()
@@ -345,7 +406,6 @@ def main():
     deltas = [(1.0 + 2e-4) / v for v in m]
     P = mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP, device=D.local % max(1, mv.device_count()))
     P.state_set(np.full(y.size, y.mean()), None, lam / 5.0)
-    ymean = float(y.mean())
     del y
     log(f"[rank {D.rank}] setup {time.perf_counter() - t_setup:.1f}s: N={P.N} E={P.E} blocks={P.nb}")
 
@@ -387,24 +447,32 @@ def main():
                    "kernel_avg_ms": round(pk_ms, 4),
                    "kernel_GBps": round(fk["bytes_per_launch"] / (pk_ms * 1e-3) / 1e9, 1) if fk["launches"] else None}
     g_elapsed, = D.allreduce([elapsed], "max")
-    # global residual all-reduce over the independent fits
-    r2, s2, n_unconv = D.allreduce([st["r_norm"] ** 2, st["s_norm"] ** 2, float(st["pcg_unconverged"])], "sum")
-    kbar_all, = D.allreduce([kbar], "sum")
+    # global residual all-reduce over the independent fits (RCCL over xGMI through libmvtv's communicator)
+    red = [st["r_norm"] ** 2, st["s_norm"] ** 2, float(st["pcg_unconverged"]), kbar]
+    if comm is not None:
+        red = comm.allreduce_host(red).tolist()
+        red_via = f"RCCL ({comm.size} ranks, libmvtv communicator)"
+    else:
+        red = D.allreduce(red, "sum")
+        red_via = "host" if D.world == 1 else "gloo"
+    r2, s2, n_unconv, kbar_all = red
     kbar_all /= D.world
 
-    # dominant kernel (by time in the timed region) and its achieved HBM rate
-    dom = max((k for k in tim if tim[k]["bytes_per_launch"] > 0), key=lambda k: tim[k]["ms"])
+    roof = _roofline(tim)
+    dom = roof["kernel"]
     per = {}
     for k, v in tim.items():
         if v["launches"]:
             avg = v["ms"] / v["launches"]
             per[k] = dict(avg_ms=round(avg, 4), launches=v["launches"], share=round(v["ms"] / (elapsed * 1e3), 4),
                           GBps=round(v["bytes_per_launch"] / (avg * 1e-3) / 1e9, 1) if v["bytes_per_launch"] else None)
-    d_avg_ms = tim[dom]["ms"] / tim[dom]["launches"]
-    achieved = tim[dom]["bytes_per_launch"] / (d_avg_ms * 1e-3) / 1e9
     N, E = P.N, P.E
     iter_gbps = moved * a.steps / elapsed / 1e9                  # algorithmic bytes of every kernel launched
     pmc, pmc_src = load_pmc(dom) if (a.dims, a.size) == (3, 512) else (None, None)
+    roof.update(traffic=pmc, traffic_source=pmc_src,
+                # a mesh whose working set fits the 256 MiB Infinity Cache is served partly on-die:
+                # its "HBM" fraction is an upper bound, not an HBM measurement (SURVEY §7 hard part 7)
+                mall_resident=8 * N * 6 < 256 * 2 ** 20)
 
     cpu = None
     if D.world == 1 and not a.no_cpu:
@@ -419,45 +487,64 @@ def main():
         except Exception as e:  # the baseline is reported, never required
             log(f"cpu_baseline failed: {e}")
     P.close()
+    if D.rank != 0:
+        return None
+    value = D.world * a.steps / g_elapsed
+    return {
+        "metric": METRIC, "value": round(value, 4), "unit": "iters/s", "n_gpus": D.world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(g_elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: 3D towers + 0.5 N(0,1) (splitmix64/Box-Muller, seed 0x4D565456 + rank), O = I",
+        "config": {"workload": f"{a.dims}D {a.size}^{a.dims} fp64 mesh-TV ADMM, variant B (rcpp admm_update), "
+                               f"lambda={lam}, fixed-iteration mode",
+                   "theta_solver": used,
+                   "mesh": m, "nodes": N, "edges": E, "pcg_rtol": a.pcg_rtol, "pcg_iters_mean": round(kbar_all, 2),
+                   "parallelism": (f"independent mesh fits, one per GPU (gloo barrier / max-time, residual "
+                                   f"all-reduce over {red_via})") if D.world > 1 else "single GPU"},
+        "roofline": roof,
+        "iteration_hbm": {"bytes_per_iter": moved, "GBps": round(iter_gbps, 1),
+                          "frac": round(iter_gbps / HBM_PEAK_GBPS, 4),
+                          "survey_bytes_per_iter": 8.0 * (5 * E + 8 * N + 10 * kbar * N)},
+        "pcg_leg": pcg_leg,
+        "kernels": per,
+        "residuals": {"r_norm": float(np.sqrt(r2)), "s_norm": float(np.sqrt(s2)), "pcg_unconverged": int(n_unconv)},
+        "cpu_baseline": cpu,
+    }
 
-    if D.rank == 0:
-        value = D.world * a.steps / g_elapsed
-        out = {
-            "metric": "ADMM iters/sec on 512^3 fp64 mesh; achieved HBM GB/s vs peak at 1/2/4/8 GPUs",
-            "value": round(value, 4),
-            "unit": "iters/s",
-            "n_gpus": D.world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(g_elapsed / a.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic: 3D towers + 0.5 N(0,1) (splitmix64/Box-Muller, seed 0x4D565456 + rank), O = I",
-            "config": {"workload": f"{a.dims}D {a.size}^{a.dims} fp64 mesh-TV ADMM, variant B (rcpp admm_update), "
-                                   f"lambda={lam}, fixed-iteration mode",
-                       "theta_solver": used,
-                       "mesh": m, "nodes": N, "edges": E, "pcg_rtol": a.pcg_rtol, "pcg_iters_mean": round(kbar_all, 2),
-                       "parallelism": (f"independent mesh fits, one per GPU ({'RCCL' if D.backend == 'nccl' else D.backend} "
-                                       f"barrier / max-time / residual all-reduce)") if D.world > 1 else "single GPU"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": pmc, "traffic_source": pmc_src, "bytes_per_launch": tim[dom]["bytes_per_launch"],
-                         "avg_launch_ms": round(d_avg_ms, 4),
-                         # a mesh whose working set fits the 256 MiB Infinity Cache is served partly on-die:
-                         # its "HBM" fraction is an upper bound, not an HBM measurement (SURVEY §7 hard part 7)
-                         "mall_resident": 8 * N * 6 < 256 * 2 ** 20},
-            "iteration_hbm": {"bytes_per_iter": moved, "GBps": round(iter_gbps, 1),
-                              "frac": round(iter_gbps / HBM_PEAK_GBPS, 4),
-                              "survey_bytes_per_iter": 8.0 * (5 * E + 8 * N + 10 * kbar * N)},
-            "pcg_leg": pcg_leg,
-            "kernels": per,
-            "residuals": {"r_norm": float(np.sqrt(r2)), "s_norm": float(np.sqrt(s2)),
-                          "pcg_unconverged": int(n_unconv)},
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out), file=OUT, flush=True)
+
+def main():
+    a = parse()
+    if a.dry_run:
+        return _dry_run(a)
+    _import_mv()
+    if mv.device_count() < 1:
+        raise SystemExit("bench.py: no HIP device")
+    D = Dist("gloo")
+    line = None
+    if a.mode == "cv":
+        if a.size == 512 and a.dims == 3:   # config 4's shape unless given
+            a.dims, a.size = 2, 2048
+        line = cv_main(a, D)
+    elif a.mode == "slab":
+        line = slab_main(a, D)
+    elif a.mode == "independent" or D.world == 1:
+        comm = _rccl_comm(D, D.local % mv.device_count()) if D.world > 1 else None
+        line = independent_main(a, D, comm)
+        if comm is not None:
+            comm.close()
+    else:
+        # N > 1: the metric is one mesh over all GPUs (slab, strong); the independent fits (weak) beside it
+        comm = _rccl_comm(D, D.local % mv.device_count())
+        ind = independent_main(a, D, comm)
+        line = slab_main(a, D, comm)
+        comm.close()
+        if line is not None:
+            line["independent_fits"] = {k: ind[k] for k in ("value", "unit", "ms_per_step", "scaling", "roofline",
+                                                            "residuals")}
+            line["independent_fits"]["workload"] = (f"one {a.size}^{a.dims} fit per GPU (noise seed + rank), "
+                                                   f"{D.world} GPUs")
+    if line is not None:
+        print(json.dumps(line), file=OUT, flush=True)
     D.close()
 
 
@@ -475,5 +562,8 @@ def _json_stdout():
 
 
 if __name__ == "__main__":
+    _a = parse()
+    if _a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(_a.gpus, sys.argv[1:], dry_run=_a.dry_run))
     OUT = _json_stdout()
     main()

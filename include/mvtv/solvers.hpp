@@ -7,6 +7,7 @@
 // warm-started lambda path, MSE bookkeeping).
 #pragma once
 #include <cstdint>
+#include <limits>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -47,7 +48,11 @@ struct mbs_cache {
     vec oty, w;
     int64_t ntheta = 0, rowsD = 0;
     vec deltas;                     // block weights of D (empty: every weight 1, cpp-code mbs_one without cache)
-    double sp_sigma = 0.0;          // variant A: sp_crosses = crossO + sp_sigma * crossD (cpp-code/solvers.hpp:26)
+    // the solve matrix the cache holds, sp_crosses = crossO + sp_sigma * crossD (rcpp…/solvers.hpp:46,
+    // cpp-code/solvers.hpp:26); admm_update's FIRST theta-solve uses it (rcpp…/solvers.cpp:107,113;
+    // cpp-code/solvers.cpp:116). NaN: not set (B: rho_init, A: lambda). mbs_path (B) leaves the rho carried
+    // INTO its last lambda here (:213), which mbs_fit_optimal's refit then solves with (:273, :47).
+    double sp_sigma = std::numeric_limits<double>::quiet_NaN();
     mbs_cache() = default;
     mbs_cache(const mbs_cache&) = delete;
     mbs_cache& operator=(const mbs_cache&) = delete;
@@ -64,7 +69,8 @@ struct admm_out {
     mvtv_admm_stats stats{};
 };
 
-// B: rcpp…/solvers.hpp:100 (y is unused by the loop, kept for signature parity)
+// B: rcpp…/solvers.hpp:100 (y is unused by the loop, kept for signature parity). The first theta-solve uses
+// the cache's matrix (inits.sp_sigma; NaN: rho_init), every later one crossO + rho crossD (:126).
 void admm_update(const vec& y, mbs_cache& inits, vec& theta_init, double lambda, bool verbose, vec& u_init,
                  double& rho_init, admm_out& out);
 // A: cpp-code/solvers.hpp:85 — throws std::invalid_argument("Failed to converge!") past 2000 iterations;
@@ -107,7 +113,9 @@ std::vector<int> kfoldinds(int64_t n, int k, uint64_t seed = 0);
 vec create_lambdas(int n_lambda, mbs_cache& inits, const vec* lambdas, bool verbose = false);
 // test_mse (:278-288): MSE of each path model's predictions at (data, y)
 vec test_mse(const mat& data, const vec& y, const mbs_object& path, int n_lambda);
-// mbs_fit_optimal (:261-274): cold refit at the lambda of the smallest row mean of mse_mat
+// mbs_fit_optimal (:261-274): cold refit (theta = mean y, u = 0, rho = lambdas[0] / 5) at the lambda of the
+// smallest row mean of mse_mat, whose first theta-solve uses the matrix the preceding mbs_path left in the
+// cache (crossO + rho_in(last lambda) crossD, :213 -> :273 -> use_cache :47 -> :107, :113)
 void mbs_fit_optimal(const mat& data, const vec& y, const vec& m, mbs_one_object& best_model, const mat& mesh,
                      const vec& lambdas, const mat& mse_mat, mbs_cache& cache, bool verbose = false);
 

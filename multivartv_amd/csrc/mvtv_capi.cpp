@@ -680,7 +680,12 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
         // launches 2-4 % shorter at 512^3 on the same box (4.21 -> 4.13 ms, 5.2-5.36 -> 5.13 ms)
         const char* e = probe_env("MVTV_EAOS");
         const bool want = e ? std::atoi(e) != 0 : true;
-        g.eaos = (want && P->f3d && g.p == 3 && g.N % 64 == 0) ? 1u : 0u;
+        // a slab rank decides from its plane size, which every rank shares (its N counts its own ghost
+        // planes): the z halo moves whole planes, one contiguous run per plane only when planes are whole
+        // 64-node chunks, so every rank must pick the same layout
+        const uint64_t plane = g.N / g.m[g.p - 1];
+        const bool chunks = P->slab ? plane % 64 == 0 : g.N % 64 == 0;
+        g.eaos = (want && P->f3d && g.p == 3 && chunks) ? 1u : 0u;
     }
     if (s == MVTV_OK) s = mvtv_problem_set_data(P, d->oty, d->wdiag);
     if (s != MVTV_OK) {

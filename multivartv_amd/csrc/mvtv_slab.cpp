@@ -37,6 +37,9 @@
 // ============================================================================================ transports
 struct mvtv_comm {
     int rank = 0, size = 1;
+    int device = 0;                  // RCCL: the communicator's device
+    double* scratch = nullptr;       // mvtv_comm_allreduce_host's device staging (RCCL)
+    hipStream_t stream = nullptr;
     virtual ~mvtv_comm() = default;
     // point-to-point transfers between begin() and end() progress together (all-to-all, halos)
     virtual mvtv_status begin() = 0;
@@ -44,6 +47,9 @@ struct mvtv_comm {
     virtual mvtv_status recv(double* buf, size_t n, int peer, hipStream_t s) = 0;
     virtual mvtv_status end(hipStream_t s) = 0;
     virtual mvtv_status allreduce_sum(double* buf, size_t n, hipStream_t s) = 0;
+    // a rank whose loop failed tells its peers, so that they fail instead of waiting for it (loopback; an RCCL
+    // peer of a failed process is ended by the launcher)
+    virtual void abort() {}
 };
 
 namespace {
@@ -61,6 +67,7 @@ struct RcclApi {
     ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                               hipStream_t) = nullptr;
     const char* (*GetErrorString)(ncclResult_t) = nullptr;
+    std::string path;   // the file the functions came from
 };
 
 mvtv_status rccl_api(RcclApi** out) {
@@ -70,9 +77,15 @@ mvtv_status rccl_api(RcclApi** out) {
     std::lock_guard<std::mutex> lk(mu);
     if (!tried) {
         tried = true;
-        for (const char* name : {"/opt/rocm/lib/librccl.so.1", "librccl.so.1", "librccl.so"}) {
-            api.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+        // One RCCL per process: a copy already mapped (torch's librccl, soname librccl.so.1, is loaded by
+        // `import torch`) is reused; only a process without one loads ROCm's
+        for (const char* name : {"librccl.so.1", "librccl.so"}) {
+            api.h = dlopen(name, RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);
             if (api.h) break;
+        }
+        for (const char* name : {"/opt/rocm/lib/librccl.so.1", "librccl.so.1", "librccl.so"}) {
+            if (api.h) break;
+            api.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
         }
         if (api.h) {
             auto sym = [&](auto& fp, const char* n) { fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(api.h, n)); };
@@ -85,6 +98,9 @@ mvtv_status rccl_api(RcclApi** out) {
             sym(api.GroupEnd, "ncclGroupEnd");
             sym(api.AllReduce, "ncclAllReduce");
             sym(api.GetErrorString, "ncclGetErrorString");
+            Dl_info info{};
+            if (api.GetUniqueId && dladdr(reinterpret_cast<void*>(api.GetUniqueId), &info) && info.dli_fname)
+                api.path = info.dli_fname;
         }
     }
     if (!api.h || !api.GetUniqueId || !api.CommInitRank || !api.Send || !api.Recv || !api.GroupStart ||
@@ -119,6 +135,8 @@ struct RcclComm final : mvtv_comm {
     SelfCopy self;
     ~RcclComm() override {
         if (comm && api_->CommDestroy) api_->CommDestroy(comm);
+        if (scratch) (void)hipFree(scratch);
+        if (stream) (void)hipStreamDestroy(stream);
     }
     mvtv_status begin() override {
         NCCL_TRY(api_->GroupStart());
@@ -171,6 +189,7 @@ struct LocalHub {
     std::vector<double*> bufs;
     std::vector<hipEvent_t> bev, cev;
     std::vector<hipEvent_t> pool;   // events of finished transfers, reused (guarded by mu)
+    bool aborted = false;           // some rank's loop failed: every wait gives up
     explicit LocalHub(int g) : size(g), box(size_t(g) * size_t(g)), bufs(size_t(g)), bev(size_t(g)), cev(size_t(g)) {}
     ~LocalHub() {
         for (auto e : pool) (void)hipEventDestroy(e);
@@ -237,7 +256,8 @@ struct LocalComm final : mvtv_comm {
         {
             std::unique_lock<std::mutex> lk(hub->mu);
             auto& q = hub->box[size_t(peer) * size_t(size) + size_t(rank)];
-            hub->cv.wait(lk, [&] { return !q.empty(); });
+            hub->cv.wait(lk, [&] { return !q.empty() || hub->aborted; });
+            if (q.empty()) return fail(MVTV_HIP_ERROR, "loopback: a peer rank aborted");
             m = q.front();
             q.pop_front();
         }
@@ -255,10 +275,12 @@ struct LocalComm final : mvtv_comm {
     mvtv_status end(hipStream_t s) override {
         std::unique_lock<std::mutex> lk(hub->mu);
         hub->cv.wait(lk, [&] {
+            if (hub->aborted) return true;
             for (auto& pd : sent)
                 if (!pd.acked) return false;
             return true;
         });
+        if (hub->aborted) return fail(MVTV_HIP_ERROR, "loopback: a peer rank aborted");
         lk.unlock();
         for (auto& pd : sent) HIP_TRY(hipStreamWaitEvent(s, pd.done, 0));
         lk.lock();   // both events have been waited on by the streams that need them: reusable
@@ -269,16 +291,23 @@ struct LocalComm final : mvtv_comm {
         sent.clear();
         return MVTV_OK;
     }
-    // generation barrier on the hub
-    void barrier(std::unique_lock<std::mutex>& lk) {
+    // generation barrier on the hub; false when a peer aborted
+    bool barrier(std::unique_lock<std::mutex>& lk) {
+        if (hub->aborted) return false;
         const long g = hub->gen;
         if (++hub->arrive == size) {
             hub->arrive = 0;
             ++hub->gen;
             hub->cv.notify_all();
         } else {
-            hub->cv.wait(lk, [&] { return hub->gen != g; });
+            hub->cv.wait(lk, [&] { return hub->gen != g || hub->aborted; });
         }
+        return hub->gen != g;
+    }
+    void abort() override {
+        std::lock_guard<std::mutex> lk(hub->mu);
+        hub->aborted = true;
+        hub->cv.notify_all();
     }
     mvtv_status allreduce_sum(double* buf, size_t n, hipStream_t s) override {
         if (size == 1) return MVTV_OK;
@@ -294,7 +323,7 @@ struct LocalComm final : mvtv_comm {
         std::unique_lock<std::mutex> lk(hub->mu);
         hub->bufs[size_t(rank)] = buf;
         hub->bev[size_t(rank)] = ready;
-        barrier(lk);   // every rank's vector is posted
+        if (!barrier(lk)) return fail(MVTV_HIP_ERROR, "loopback: a peer rank aborted");   // every vector posted
         lk.unlock();
         for (int r = 0; r < size; ++r) {
             HIP_TRY(hipStreamWaitEvent(s, hub->bev[size_t(r)], 0));
@@ -304,14 +333,14 @@ struct LocalComm final : mvtv_comm {
         HIP_TRY(hipEventRecord(copied, s));
         lk.lock();
         hub->cev[size_t(rank)] = copied;
-        barrier(lk);   // every rank has enqueued its copies
+        if (!barrier(lk)) return fail(MVTV_HIP_ERROR, "loopback: a peer rank aborted");   // copies enqueued
         lk.unlock();
         for (int r = 0; r < size; ++r)   // nobody overwrites its vector before all copies of it are done
             if (r != rank) HIP_TRY(hipStreamWaitEvent(s, hub->cev[size_t(r)], 0));
         hipLaunchKernelGGL(k_rowsum, dim3(1), dim3(64), 0, s, stage, size, int(n), buf);
         HIP_TRY(hipGetLastError());
         lk.lock();
-        barrier(lk);   // the hub's slots may be reused
+        if (!barrier(lk)) return fail(MVTV_HIP_ERROR, "loopback: a peer rank aborted");   // slots reusable
         hub->pool.push_back(ready);
         hub->pool.push_back(copied);
         lk.unlock();
@@ -344,6 +373,7 @@ mvtv_status mvtv_comm_create_rccl(const uint8_t* id128, int32_t nranks, int32_t 
     c->api_ = api;
     c->rank = rank;
     c->size = nranks;
+    c->device = device;
     ncclUniqueId id;
     std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
     const ncclResult_t r = api->CommInitRank(&c->comm, nranks, id, rank);
@@ -370,6 +400,26 @@ mvtv_status mvtv_comm_create_local(int32_t nranks, mvtv_comm** out) {
 }
 
 void mvtv_comm_destroy(mvtv_comm* c) { delete c; }
+
+mvtv_status mvtv_comm_allreduce_host(mvtv_comm* c, double* vals, int32_t n) {
+    if (!c || (!vals && n > 0) || n < 0 || n > 64) return fail(MVTV_BAD_ARG, "bad argument (n <= 64)");
+    if (!dynamic_cast<RcclComm*>(c)) return fail(MVTV_BAD_ARG, "host all-reduce: RCCL communicators only");
+    if (c->size == 1 || n == 0) return MVTV_OK;
+    DeviceGuard dg(c->device);
+    if (!c->stream) HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (!c->scratch) MVTV_TRY(alloc(&c->scratch, 64));
+    HIP_TRY(hipMemcpyAsync(c->scratch, vals, size_t(n) * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    MVTV_TRY(c->allreduce_sum(c->scratch, size_t(n), c->stream));
+    HIP_TRY(hipMemcpyAsync(vals, c->scratch, size_t(n) * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MVTV_OK;
+}
+
+const char* mvtv_comm_library(void) {
+    RcclApi* api = nullptr;
+    if (rccl_api(&api) != MVTV_OK) return "";
+    return api->path.c_str();
+}
 int32_t mvtv_comm_rank(const mvtv_comm* c) { return c ? c->rank : -1; }
 int32_t mvtv_comm_size(const mvtv_comm* c) { return c ? c->size : 0; }
 
@@ -391,9 +441,9 @@ uint32_t ilog2(uint32_t v) {
 
 }  // namespace
 
-extern "C" mvtv_status mvtv_slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, double lambda,
-                                     double theta0, double rho0, mvtv_admm_stats* stats) {
-    if (!P || !C || !opts) return fail(MVTV_BAD_ARG, "null argument");
+namespace {
+mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, double lambda, double theta0,
+                     double rho0, mvtv_admm_stats* stats) {
     if (!P->slab) return fail(MVTV_BAD_ARG, "not a slab problem (mvtv_problem_create_slab)");
     if (opts->variant != MVTV_VARIANT_RCPP) return fail(MVTV_BAD_ARG, "the slab loop runs variant B");
     if (P->wmode != W_IDENTITY || !P->spec_pow2) return fail(MVTV_BAD_ARG, "slab loop: W = I, power-of-two m_j <= 4096");
@@ -420,6 +470,17 @@ extern "C" mvtv_status mvtv_slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_a
     for (int r = 0; r <= G; ++r) zbs[size_t(r)] = uint32_t(uint64_t(sg.mg) * uint64_t(r) / uint64_t(G));
     if (zbs[size_t(rk)] != sg.zb || zbs[size_t(rk) + 1] != sg.zb + sg.nz)
         return fail(MVTV_BAD_ARG, "slab plane range differs from the even split of the communicator");
+    {   // every rank must enqueue the same loop: the fused pass or not, and the same edge layout (the z halo
+        // moves whole planes in it). One sum of the flags; a mismatch fails on every rank alike
+        double flags[4] = {P->f3d ? 1.0 : 0.0, P->g.eaos ? 1.0 : 0.0, P->e3d ? 1.0 : 0.0, double(sg.plane)};
+        HIP_TRY(hipMemcpyAsync(P->red, flags, sizeof(flags), hipMemcpyHostToDevice, s));
+        MVTV_TRY(C->allreduce_sum(P->red, 4, s));
+        double sum[4];
+        HIP_TRY(hipMemcpyAsync(sum, P->red, sizeof(sum), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        for (int k = 0; k < 4; ++k)
+            if (sum[k] != double(G) * flags[k]) return fail(MVTV_BAD_ARG, "slab ranks disagree on the loop layout");
+    }
 
     const double tol = opts->tol > 0 ? opts->tol : 1e-4;
     const int max_counter = opts->max_counter > 0 ? opts->max_counter : 3000;
@@ -656,4 +717,14 @@ extern "C" mvtv_status mvtv_slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_a
     S.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (stats) *stats = S;
     return S.status == MVTV_OK ? MVTV_OK : MVTV_MAXITER;
+}
+}  // namespace
+
+extern "C" mvtv_status mvtv_slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, double lambda,
+                                     double theta0, double rho0, mvtv_admm_stats* stats) {
+    if (!C) return fail(MVTV_BAD_ARG, "null communicator");
+    const mvtv_status st =
+        (!P || !opts) ? fail(MVTV_BAD_ARG, "null argument") : slab_run(P, C, opts, lambda, theta0, rho0, stats);
+    if (st != MVTV_OK && st != MVTV_MAXITER) C->abort();
+    return st;
 }

@@ -239,6 +239,7 @@ void admm_update(const vec& /*y*/, mbs_cache& inits, vec& theta_init, double lam
     mvtv_admm_opts o;
     mvtv_default_opts(&o, MVTV_VARIANT_RCPP);
     o.verbose = verbose;
+    o.sigma = inits.sp_sigma;   // spcrosses = inits.sp_crosses for the first solve (:107, :113); NaN: rho
     out.theta = theta_init;
     out.u = u_init.empty() ? vec(size_t(inits.rowsD), 0.0) : u_init;
     out.rho = rho_init;
@@ -296,13 +297,15 @@ void mbs_path(const mat& data, const vec& y, const vec& m, const mat& mesh, cons
     // stays resident on the GPU between lambdas and is read back once per lambda for the model.
     const size_t n_lambda = lambdas.size();
     vec theta(size_t(cache.ntheta), mean(y));
-    check(mvtv_state_set(cache.prob, theta.data(), nullptr, lambdas.empty() ? 0.0 : lambdas[0] / 5.0));
+    double rho_in = lambdas.empty() ? 0.0 : lambdas[0] / 5.0;   // rho_init (:209)
+    check(mvtv_state_set(cache.prob, theta.data(), nullptr, rho_in));
     mvtv_admm_opts o;
     mvtv_default_opts(&o, MVTV_VARIANT_RCPP);
     o.verbose = verbose;
     output.models.clear();
     output.mses.assign(n_lambda, 0.0);
     for (size_t i = 0; i < n_lambda; ++i) {
+        cache.sp_sigma = rho_in;   // cache->sp_crosses = crossO + rho_init crossD (:213); o.sigma NaN = the same
         mvtv_admm_stats st;
         const int s = mvtv_admm_run(cache.prob, &o, lambdas[i], &st);
         if (s != MVTV_OK && s != MVTV_MAXITER) check(s);
@@ -317,6 +320,7 @@ void mbs_path(const mat& data, const vec& y, const vec& m, const mat& mesh, cons
         model.y = y;
         model.m = m;
         output.mses[i] = mbs_mse(model, ftrue);
+        rho_in = model.rhohat;   // :218 (the cache keeps the previous lambda's matrix after the loop)
         output.models.push_back(std::move(model));
     }
     // fill_output_mbs (:177-184): first minimum
@@ -384,6 +388,8 @@ void mbs_fit_optimal(const mat& data, const vec& y, const vec& m, mbs_one_object
             best = size_t(i);
         }
     }
+    // :266-268. mbs_one uses the cache (:273 -> use_cache :47), so admm_update's first solve takes
+    // cache.sp_sigma, the rho the preceding mbs_path carried into its last lambda (:213), not rho_init.
     vec theta(size_t(cache.ntheta), mean(y));
     vec u(size_t(cache.rowsD), 0.0);
     double rho = lambdas[0] / 5.0;

@@ -3,9 +3,10 @@
 Mirrors ``mbs_impl`` and its helpers in rcpp-code/MultivarTV/src/solvers.cpp:
   create_lambdas   :186-200   lambda grid from lam_max_pinv (GPU, ``Problem.lambda_max``)
   mbs_path         :204-222   warm-started path (theta, u, rho carried; resident on the GPU)
-  mbs_fit_optimal  :224-237   cold refit at the best lambda (folds == 1)
-  test_mse         :241-251   held-out MSE per lambda
-  mbs_impl         :302-376   folds, final path, best model, result list
+  mbs_fit_optimal  :261-274   cold refit at the best lambda (folds == 1), first solve on the
+                              matrix mbs_path left in the cache (:213 -> :273 -> :47 -> :107, :113)
+  test_mse         :278-288   held-out MSE per lambda
+  mbs_impl         :305-376   folds, final path, best model, result list
 with create_mesh (rcpp…/utils.cpp:234-254), create_deltas (:256-263) and kfoldinds (:367-376).
 
 Multi-GPU. One process per GPU (torch.distributed, any backend). The
@@ -136,7 +137,7 @@ def assign(n_items: int, world: int, rank: int):
 
 def mbs_impl(data, y, m, mesh=None, n_lambda=100, ftrue=None, lambdas=None, folds=1, verbose=False, seed=0,
              device=None, group=None, _runner=None):
-    """rcpp…/solvers.cpp:302-376. Returns the reference's result list as a dict (rank 0; other
+    """rcpp…/solvers.cpp:305-376. Returns the reference's result list as a dict (rank 0; other
     ranks return only 'cv.mses' and 'lambda_minmse_ind').
 
     ``_runner(kind, fold)`` replaces the GPU path computation (tests of the distribution logic):
@@ -210,10 +211,15 @@ def mbs_impl(data, y, m, mesh=None, n_lambda=100, ftrue=None, lambdas=None, fold
 
     thetas, fitted = final["thetas"], final["fitted"]
     if folds == 1 and _runner is None:
-        # mbs_fit_optimal (:224-237): cold start at the best lambda with rho_init = lambdas[0] / 5
+        # mbs_fit_optimal (:261-274): cold start at the best lambda with rho_init = lambdas[0] / 5 (:268), but
+        # mbs_one takes the cache (:273), whose sp_crosses mbs_path last set to crossO + rho crossD with the
+        # rho carried INTO the last lambda (:213); use_cache copies it (:47) and admm_update's first solve
+        # uses it (:107, :113), while b is formed with rho_init (:112).
         P, idx = problem_for(data, y)
+        st = final["stats"]
+        sigma0 = float(st[-2]["rho"]) if len(st) >= 2 else float(LAMBDAS[0]) / 5.0
         th, _, _, _ = P.admm(float(LAMBDAS[best]), np.full(P.N, y.mean()), u=None, rho=float(LAMBDAS[0]) / 5.0,
-                             return_u=False)
+                             return_u=False, sigma=sigma0)
         best_theta, best_fit = th, th[idx]
     else:
         best_theta, best_fit = thetas[best], fitted[best]

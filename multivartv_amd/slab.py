@@ -49,6 +49,8 @@ _SIGS = {
     "mvtv_slab_run": (_C.c_int, [_C.c_void_p, _C.c_void_p, _C.POINTER(_lib.AdmmOpts), _C.c_double, _C.c_double,
                                  _C.c_double, _C.POINTER(_lib.AdmmStats)]),
     "mvtv_sync": (_C.c_int, [_C.c_void_p]),
+    "mvtv_comm_allreduce_host": (_C.c_int, [_C.c_void_p, _dp, _C.c_int32]),
+    "mvtv_comm_library": (_C.c_char_p, []),
 }
 _lib.SIGNATURES.update(_SIGS)
 if _lib._LIB is not None:   # library already loaded: register the new signatures
@@ -102,6 +104,17 @@ class Comm:
         hs = (_C.c_void_p * n)()
         _lib._check(_L().mvtv_comm_create_local(n, hs))
         return [cls(_C.c_void_p(hs[i])) for i in range(n)]
+
+    def allreduce_host(self, vals):
+        """Sum of a few host doubles over the RCCL communicator (blocking)."""
+        v = np.ascontiguousarray(np.asarray(vals, dtype=np.float64).ravel())
+        _lib._check(_L().mvtv_comm_allreduce_host(self._h, v.ctypes.data_as(_dp), v.size))
+        return v
+
+    @staticmethod
+    def library():
+        """The file RCCL was resolved from (an already-mapped librccl.so.1 is reused: one RCCL per process)."""
+        return (_L().mvtv_comm_library() or b"").decode()
 
     def close(self):
         if getattr(self, "_h", None):

@@ -30,6 +30,26 @@ def test_create_mesh_column_major():
     assert mesh[0, 0] == pytest.approx(data[:, 0].min() - 1e-4)
 
 
+def test_oracle_folds1_refit_follows_stale_cache_matrix():
+    """The oracle's mbs_impl (folds = 1) refits as the reference's mbs_fit_optimal does: b with rho_init =
+    lambdas[0] / 5 (rcpp…/solvers.cpp:268, :112) but the first solve on crossO + rho crossD with the rho that
+    mbs_path carried INTO its last lambda (:213 -> :273 -> use_cache :47 -> :107, :113)."""
+    rng = np.random.default_rng(4)
+    x = rng.uniform(0, 1, size=(240, 2))
+    y = np.where(np.all(x > 0.6, axis=1), 1.0, 0.0) + 0.3 * rng.standard_normal(240)
+    m, lams = [10, 8], [2.0, 1.0, 0.5, 0.2, 0.05]
+    ref = O.mbs_impl_rcpp(x, y, m, lams, folds=1)
+    mesh, deltas = O.create_mesh_rcpp(x, m), O.create_deltas_rcpp(x, m)
+    D = O.build_D(m, O.block_table(2, deltas, "cpp"))
+    idx = O.nearest_index(x, mesh)
+    W, oty = np.bincount(idx, minlength=80).astype(float), np.bincount(idx, weights=y, minlength=80)
+    args = (D, oty, W, lams[ref["best"]], np.full(80, y.mean()), np.zeros(D.shape[0]), lams[0] / 5)
+    stale = O.admm_rcpp(*args, sigma0=ref["final"][-2].rho)
+    fresh = O.admm_rcpp(*args)
+    np.testing.assert_array_equal(ref["best_theta"], stale.theta)
+    assert stale.iters != fresh.iters
+
+
 def test_assign_round_robin():
     items = [cv.assign(7, 3, r) for r in range(3)]
     assert items == [[0, 3, 6], [1, 4], [2, 5]]

@@ -62,6 +62,48 @@ def test_mbs_impl_matches_oracle(folds):
         assert np.max(np.abs(out["models"][i]["theta_hat"] - r.theta)) <= 1e-7 * max(1.0, np.max(np.abs(r.theta)))
 
 
+def _refit_case(seed=4):
+    """A scattered 2-D problem on which mbs_fit_optimal's stale solve matrix changes the refit: the rho carried
+    into the last lambda (3.2) is not rho_init = lambdas[0] / 5 (0.4); 129 against 77 iterations (oracle)."""
+    m = [10, 8]
+    x, y = _scattered(240, 2, seed=seed)
+    mesh = O.create_mesh_rcpp(x, m)
+    deltas = O.create_deltas_rcpp(x, m)
+    idx = O.nearest_index(x, mesh)
+    N = int(np.prod(m))
+    W = np.bincount(idx, minlength=N).astype(float)
+    oty = np.bincount(idx, weights=y, minlength=N)
+    D = O.build_D(m, O.block_table(2, deltas, "cpp"))
+    return m, x, y, deltas, W, oty, D
+
+
+def test_folds1_refit_uses_stale_cache_matrix():
+    """mbs_impl(folds = 1): mbs_fit_optimal (rcpp…/solvers.cpp:261-274) refits through mbs_one with the cache,
+    whose sp_crosses mbs_path last set with the rho carried INTO the last lambda (:213); use_cache copies it
+    (:47) and admm_update's first theta-solve uses it (:107, :113) while b uses rho_init (:112). The refit with
+    that matrix takes a different trajectory than a sigma = rho restart; GPU: iterations and rho exact, theta
+    1e-8 against the oracle."""
+    m, x, y, deltas, W, oty, D = _refit_case()
+    ref = O.mbs_impl_rcpp(x, y, m, LAMS, folds=1)
+    best, fin = ref["best"], ref["final"]
+    sigma0 = fin[-2].rho
+    N, E = D.shape[1], D.shape[0]
+    stale = O.admm_rcpp(D, oty, W, LAMS[best], np.full(N, y.mean()), np.zeros(E), LAMS[0] / 5, sigma0=sigma0)
+    fresh = O.admm_rcpp(D, oty, W, LAMS[best], np.full(N, y.mean()), np.zeros(E), LAMS[0] / 5)
+    assert sigma0 != LAMS[0] / 5 and stale.iters != fresh.iters
+    scale = np.max(np.abs(stale.theta))
+    assert np.max(np.abs(stale.theta - fresh.theta)) > 1e-3 * scale
+    np.testing.assert_array_equal(ref["best_theta"], stale.theta)
+    with mv.Problem(m, oty, wdiag=W, deltas=deltas, order=mv.ORDER_CPP) as P:
+        th, _, rho, st = P.admm(LAMS[best], np.full(N, y.mean()), u=np.zeros(E), rho=LAMS[0] / 5, sigma=sigma0)
+    assert st["iters"] == stale.iters and rho == stale.rho
+    assert np.max(np.abs(th - stale.theta)) <= 1e-8 * scale
+    out = cv.mbs_impl(x, y, m, lambdas=LAMS, folds=1, group=False)
+    assert out["lambda_minmse_ind"] == best + 1
+    assert np.max(np.abs(out["theta_hat"] - stale.theta)) <= 1e-8 * scale
+    np.testing.assert_allclose(out["residuals"], y - out["fitted"], rtol=0, atol=0)
+
+
 def test_create_lambdas_grid():
     m = [16, 16]
     x, y = _scattered(500, 2, seed=5)

@@ -1,7 +1,12 @@
 """BASELINE.json configs at their real shapes, anchored to the CPU oracle where it finishes in seconds.
 
-* metric config, 3-D 512^3: the spectral solve and the Jacobi-PCG (rtol 1e-13) follow the same
-  variant-B trajectory (rcpp-code/MultivarTV/src/solvers.cpp:110-133) for 3 fixed iterations;
+* metric config, 3-D 512^3, against the C oracle (oracle/c/mvtv_oracle.c's variant-B loop with the exact
+  cosine-transform theta-solve by scipy.fft, pinned in tests/test_oracle_c.py): 2 fixed iterations of
+  rcpp-code/MultivarTV/src/solvers.cpp:110-133 on the same inputs, the GPU's whole bench path (fused
+  k_admm3a at 512^3's tiling, k_dct8 / k_tri, the device-side control) — rho exact, theta and u 1e-10,
+  r / s norms 1e-9; and the spectral solve against the Jacobi-PCG (rtol 1e-13) for 3 iterations;
+* config 5's tile shapes, 4-D 128 x 128 x 128 x 16, against the same C oracle (k_edge4d / k_gather4a/b on
+  128^3 hyperplanes);
 * config 5, 4-D 128^4 on one GPU: the same agreement for 2 iterations (one process holds the whole
   128^4 mesh: 15 edge blocks, 32 GB of edge state);
 * config 4's work item, 2-D 2048^2 with a 0/1 CV-fold mask W (rcpp…/solvers.cpp:340-353): a
@@ -43,6 +48,41 @@ def _two_solvers(m, iters):
     assert ss["r_norm"] == pytest.approx(sp["r_norm"], rel=1e-8)
     assert ss["s_norm"] == pytest.approx(sp["s_norm"], rel=1e-8)
     return ss, sp
+
+
+def _vs_c_oracle(m, iters):
+    """GPU (AUTO = the spectral solve, the bench's path) against the C oracle's spectral loop, same inputs."""
+    from oracle import c_oracle
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    lam, rho0 = 1.0, 0.2
+    th0 = np.full(y.size, y.mean())
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        P.state_set(th0, None, rho0)
+        st = P.run(lam, fixed_iters=iters)
+        assert st["theta_solver"] == mv.SOLVER_SPECTRAL and st["iters"] == iters
+        tg, ug, rg = P.state_get(want_u=True)
+    th, u = th0.copy(), np.zeros(c_oracle.num_edges(m))
+    assert u.size == ug.size
+    c_oracle.set_threads(min(16, c_oracle.threads()))
+    ref = c_oracle.admm_rcpp_spectral(m, y, lam, th, u, rho0, deltas, fixed_iters=iters,
+                                      workers=min(16, c_oracle.threads()))
+    del y
+    assert ref["iters"] == iters and rg == ref["rho"] and st["rho"] == ref["rho"]
+    assert np.max(np.abs(tg - th)) <= 1e-10 * np.max(np.abs(th))
+    assert np.max(np.abs(ug - u)) <= 1e-10 * np.max(np.abs(u))
+    assert st["r_norm"] == pytest.approx(ref["r_norm"], rel=1e-9)
+    assert st["s_norm"] == pytest.approx(ref["s_norm"], rel=1e-9)
+
+
+@pytest.mark.timeout(600)
+def test_metric_config_512_cubed_vs_c_oracle():
+    _vs_c_oracle([512, 512, 512], 2)
+
+
+@pytest.mark.timeout(300)
+def test_config5_tile_shapes_4d_vs_c_oracle():
+    _vs_c_oracle([128, 128, 128, 16], 2)
 
 
 def test_metric_config_512_cubed():

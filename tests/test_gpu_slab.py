@@ -32,8 +32,10 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("m,lam,world", [([16, 16, 16], 1.0, 1), ([16, 16, 16], 1.0, 2), ([32, 32, 32], 0.5, 4),
-                                         ([64, 32], 0.5, 2), ([8, 8, 8, 8], 1.0, 4), ([16, 16, 16, 16], 1.0, 2)],
-                         ids=["3d_16_w1", "3d_16_w2", "3d_32_w4", "2d_64x32_w2", "4d_8_w4", "4d_16_w2"])
+                                         ([64, 32], 0.5, 2), ([8, 8, 8, 8], 1.0, 4), ([16, 16, 16, 16], 1.0, 2),
+                                         ([4, 4, 8], 1.0, 4)],
+                         ids=["3d_16_w1", "3d_16_w2", "3d_32_w4", "2d_64x32_w2", "4d_8_w4", "4d_16_w2",
+                              "3d_4x4x8_w4_small_planes"])
 @pytest.mark.parametrize("fixed", [7, 0])
 def test_local_group_matches_one_gpu(m, lam, world, fixed):
     y, deltas, th, rho, st = _reference(m, lam, fixed)
@@ -43,6 +45,37 @@ def test_local_group_matches_one_gpu(m, lam, world, fixed):
     assert out[0]["r_norm"] == pytest.approx(st["r_norm"], rel=1e-9)
     assert out[0]["s_norm"] == pytest.approx(st["s_norm"], rel=1e-9)
     assert _rel(theta, th) <= 1e-11
+
+
+def test_loopback_failing_rank_does_not_hang_its_peers():
+    """A rank whose loop fails (here: a plane range that is not the communicator's even split) makes its
+    peers fail too instead of waiting for its transfers (LocalHub abort, csrc/mvtv_slab.cpp)."""
+    import threading
+    m, lam = [8, 8, 8], 1.0
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    comms = slab.Comm.local_group(2)
+    ranks = [slab.SlabADMM(m, y[r * 256:(r + 1) * 256], deltas, float(y.mean()), comms[r]) for r in range(2)]
+    errs = [None, None]
+    ranks[1].P.close()   # rank 1's handle is gone: its mvtv_slab_run fails at once
+    ranks[1].P._h = None
+
+    def work(r):
+        try:
+            ranks[r].run(lam, fixed_iters=3)
+        except Exception as e:   # noqa: BLE001
+            errs[r] = e
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in ts)
+    assert errs[0] is not None and errs[1] is not None
+    ranks[0].close()
+    for c in comms:
+        c.close()
 
 
 def test_slab_4d_16_four_ranks_vs_c_oracle():

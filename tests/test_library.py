@@ -75,3 +75,17 @@ def test_no_device_fails_loudly():
         pytest.skip("a GPU is visible")
     with pytest.raises(mv.MvtvError):
         mv.Problem([4, 4], np.zeros(16))
+
+
+def test_one_rccl_per_process():
+    """After `import torch` (whose libtorch_hip maps its own librccl.so, soname librccl.so.1) the library's
+    RCCL transport resolves to that copy instead of loading ROCm's: one RCCL runtime per process. Runs in a
+    child process, since the resolution is made once per process."""
+    code = ("import torch, multivartv_amd\n"
+            "from multivartv_amd import slab\n"
+            "print(slab.Comm.library())\n")
+    out = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stderr
+    import torch
+    torch_lib = os.path.realpath(os.path.join(os.path.dirname(torch.__file__), "lib"))
+    assert os.path.realpath(out.stdout.strip().splitlines()[-1]).startswith(torch_lib)

@@ -21,3 +21,22 @@ def test_c_oracle_matches_golden(name):
     assert st["rho"] == meta["rho"]
     assert np.max(np.abs(th - g["theta"])) <= 1e-8 * np.max(np.abs(g["theta"]))
     assert np.max(np.abs(u - g["u"])) <= 1e-8 * max(1.0, np.max(np.abs(g["u"])))
+
+
+@pytest.mark.parametrize("name", ["rcpp_1d_200", "rcpp_2d_32", "rcpp_2d_24x40", "rcpp_3d_12", "rcpp_3d_8x8x11",
+                                  "rcpp_4d_5"])
+def test_c_oracle_spectral_matches_golden(name):
+    """The C oracle's loop with the exact cosine-transform theta-solve (admm_rcpp_spectral: the checker of
+    the 512^3 metric config, tests/test_gpu_fullsize.py) against the SuperLU-driven fixtures (W = I meshes):
+    iterations and rho exact, theta and u to 1e-9."""
+    meta, g = load_golden(name)
+    if not np.all(g["W"] == 1.0):
+        pytest.skip("W != I")
+    E = c_oracle.num_edges(meta["m"])
+    th = g["theta0"].copy()
+    u = np.zeros(E)
+    st = c_oracle.admm_rcpp_spectral(meta["m"], g["Oty"], meta["lam"], th, u, meta["rho0"], meta["deltas"])
+    assert st["iters"] == meta["iters"]
+    assert st["rho"] == meta["rho"]
+    assert np.max(np.abs(th - g["theta"])) <= 1e-9 * np.max(np.abs(g["theta"]))
+    assert np.max(np.abs(u - g["u"])) <= 1e-9 * max(1.0, np.max(np.abs(g["u"])))
