@@ -137,6 +137,7 @@ void free_all(mvtv_problem* P) {
     }
     for (auto e : P->ev_pool) (void)hipEventDestroy(e);
     if (P->stream) (void)hipStreamDestroy(P->stream);
+    if (P->comm_stream) (void)hipStreamDestroy(P->comm_stream);
 }
 
 double variant_tol(const mvtv_admm_opts& o) {
@@ -1592,7 +1593,13 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
     if (!P || kid < 0 || kid >= MVTV_K_COUNT) return fail(MVTV_BAD_ARG, "kernel id");
     DeviceGuard dg(P->device);
     MVTV_TRY(P->sync());
-    const double N = double(P->g.N), E = double(P->E), w = P->wmode == W_DIAG ? 1.0 : 0.0;
+    double N = double(P->g.N), E = double(P->E);
+    const double w = P->wmode == W_DIAG ? 1.0 : 0.0;
+    if (P->slab) {   // a slab rank's kernels work on its owned planes (ghost planes are read only as halos)
+        const double own = double(P->ze - P->zb) / double(P->g.m[P->g.p - 1]);
+        N *= own;
+        E *= own;
+    }
     // algorithmic bytes per launch (each array element read or written once)
     double b = 0.0;
     switch (kid) {

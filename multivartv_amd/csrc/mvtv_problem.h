@@ -106,6 +106,7 @@ struct mvtv_problem {
     int g_lo = 0, g_hi = 0;
     double* slab_send = nullptr;   // mvtv_slab_run: the owned planes in the all-to-all's packed order
     double* slab_lines = nullptr;  // mvtv_slab_run: full last-dimension lines of this rank's line chunk
+    hipStream_t comm_stream = nullptr;   // mvtv_slab_run: the collectives' stream (overlapped with `stream`)
 
     // resident ADMM state
     bool have_state = false;

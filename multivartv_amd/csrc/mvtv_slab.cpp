@@ -540,29 +540,121 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     lg.m[p - 1] = sg.mg;
     lg.stride[p - 1] = sg.chunk;
     lg.N = sg.chunk * sg.mg;
-    DctPack pk_out{1, sg.lpl, sg.lch, sg.nz}, pk_in{2, sg.lpl, sg.lch, sg.nz};
+    // Pipelined transposes (p >= 3): the lines are cut into K pieces of w = m_0 / K adjacent dim-0 indices.
+    // Piece k's last local pass, its all-to-all, its last-dimension pass, its way back and its first inverse
+    // pass each depend only on piece k, so the transfers of piece k run on the collectives' stream while
+    // the compute stream transforms piece k + 1 (the line chunk must be whole dim-0 rows).
+    const uint32_t lm0 = ilog2(P->g.m[0]);
+    int K = 1;
+    if (!solo && p >= 3 && sg.lch >= lm0) {
+        K = 4;
+        const char* e = probe_env("MVTV_SLAB_PIECES");
+        if (e) K = std::max(1, std::atoi(e));
+        // a piece row keeps >= 16 lines (k_dct8's 128-B rows), the piece's line count >= 16 (k_tri tiles)
+        while (K > 1 && ((P->g.m[0] / uint32_t(K)) < 16u || (sg.chunk / uint32_t(K)) < 16u ||
+                         (uint32_t(K) & (uint32_t(K) - 1u)) != 0u))
+            K /= 2;
+    }
+    const uint32_t lk = ilog2(uint32_t(K)), lw = lm0 - lk, w = 1u << lw;
+    const size_t pch = sg.chunk / uint32_t(K);   // lines of a piece in this rank's chunk
+    DctPack pk_out{1, sg.lpl, sg.lch, sg.nz, lk, lm0}, pk_in{2, sg.lpl, sg.lch, sg.nz, lk, lm0};
     const double inv_n = 1.0 / (double(sg.lines) * double(sg.mg));
     double* th = P->theta + sg.off;
     double* sendbuf = solo ? th : P->slab_send;
     double* linebuf = solo ? th : P->slab_lines;
     const DctPack* pko = solo ? nullptr : &pk_out;
     const DctPack* pki = solo ? nullptr : &pk_in;
+    // LinePiece of piece k: for the local pass along dim p - 2 (lines over the owned planes) or for the
+    // last-dimension pass on the piece buffer (its chunk lines, eigenvalues from the global line index)
+    auto piece_pass = [&](int k) {
+        LinePiece pc;
+        pc.lw = lw;
+        pc.ls = lm0;
+        pc.xoff = uint32_t(k) * w;
+        pc.nlines = uint32_t(og.N / og.m[p - 2] / uint64_t(K));
+        return pc;
+    };
+    auto piece_mid = [&](int k) {
+        LinePiece pc;
+        pc.lw = lw;
+        pc.ls = lm0;
+        pc.xoff = uint32_t(k) * w;
+        pc.nlines = uint32_t(pch);
+        return pc;
+    };
+    Geom lgk = lg;   // the last-dimension pass on one piece buffer
+    lgk.stride[p - 1] = uint32_t(pch);
+    lgk.N = pch * sg.mg;
     double* gbuf[2] = {P->guprev, P->gu};
     double* ebuf[2] = {P->edges, fused ? P->edges2 : P->edges};
     const size_t pl = sg.plane;
     const size_t first_owned = size_t(P->g_lo) * pl, last_owned = first_owned + size_t(sg.nz - 1) * pl;
 
+    // The collectives run on their own stream sc, handed data by events, so the compute stream s goes on:
+    // with the transfers of other pieces, and with the z halo (needed by the next iteration's edge pass)
+    // during the next theta-solve. One rank: no transfers, everything on s.
+    hipStream_t sc = s;
+    if (!solo) {
+        if (!P->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&P->comm_stream, hipStreamNonBlocking));
+        sc = P->comm_stream;
+    }
+    struct Events {
+        std::vector<hipEvent_t> v;
+        ~Events() {
+            for (auto e : v) (void)hipEventDestroy(e);
+        }
+    } evs;
+    auto mkev = [&](size_t n) -> mvtv_status {
+        for (size_t i = evs.v.size(); i < n; ++i) {
+            hipEvent_t e = nullptr;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            evs.v.push_back(e);
+        }
+        return MVTV_OK;
+    };
+    // events: per piece ef (packed, s -> sc), er (received, sc -> s), et (solved, s -> sc), eb (back, sc -> s);
+    // then theta ready, theta halo done, sums ready, sums reduced, edges ready, z ghost in place, z halo done
+    enum { EV_TH = 0, EV_THD, EV_RED, EV_AR, EV_EDGE, EV_EDGED, EV_ZH, EV_FIXED };
+    MVTV_TRY(mkev(size_t(EV_FIXED) + 4 * size_t(K)));
+    hipEvent_t* ev = evs.v.data();
+    hipEvent_t *ef = ev + EV_FIXED, *er = ef + K, *et = er + K, *eb = et + K;
+    auto handoff = [&](hipEvent_t e, hipStream_t from, hipStream_t to) -> mvtv_status {
+        HIP_TRY(hipEventRecord(e, from));
+        HIP_TRY(hipStreamWaitEvent(to, e, 0));
+        return MVTV_OK;
+    };
+    bool zh_pending = false;   // a z halo was enqueued on sc that the next edge pass must wait for
+
     // edge plane e of buffer z (eaos: one contiguous run of nb * plane words; block-major: nb runs)
     auto edge_plane_xfer = [&](double* z, size_t e, int peer, bool is_send) -> mvtv_status {
         if (P->g.eaos) {
             double* ptr = z + e * pl * size_t(P->g.nb);
-            return is_send ? C->send(ptr, pl * size_t(P->g.nb), peer, s) : C->recv(ptr, pl * size_t(P->g.nb), peer, s);
+            return is_send ? C->send(ptr, pl * size_t(P->g.nb), peer, sc) : C->recv(ptr, pl * size_t(P->g.nb), peer, sc);
         }
         for (int k = 0; k < P->g.nb; ++k) {
             double* ptr = z + size_t(k) * nodes + e * pl;
-            MVTV_TRY(is_send ? C->send(ptr, pl, peer, s) : C->recv(ptr, pl, peer, s));
+            MVTV_TRY(is_send ? C->send(ptr, pl, peer, sc) : C->recv(ptr, pl, peer, sc));
         }
         return MVTV_OK;
+    };
+    // piece k of the forward transpose: my planes x rank r's lines -> rank r; rank r's planes x my lines <- r
+    auto a2a_fwd = [&](int k) -> mvtv_status {
+        MVTV_TRY(C->begin());
+        for (int r = 0; r < G; ++r)
+            MVTV_TRY(C->send(sendbuf + (size_t(k) * size_t(G) + size_t(r)) * sg.nz * pch, size_t(sg.nz) * pch, r, sc));
+        for (int r = 0; r < G; ++r)
+            MVTV_TRY(C->recv(linebuf + size_t(k) * sg.mg * pch + size_t(zbs[size_t(r)]) * pch,
+                             size_t(zbs[size_t(r) + 1] - zbs[size_t(r)]) * pch, r, sc));
+        return C->end(sc);
+    };
+    auto a2a_back = [&](int k) -> mvtv_status {
+        MVTV_TRY(C->begin());
+        for (int r = 0; r < G; ++r)
+            MVTV_TRY(C->send(linebuf + size_t(k) * sg.mg * pch + size_t(zbs[size_t(r)]) * pch,
+                             size_t(zbs[size_t(r) + 1] - zbs[size_t(r)]) * pch, r, sc));
+        for (int r = 0; r < G; ++r)
+            MVTV_TRY(C->recv(sendbuf + (size_t(k) * size_t(G) + size_t(r)) * sg.nz * pch, size_t(sg.nz) * pch, r, sc));
+        return C->end(sc);
     };
 
     auto enqueue = [&](int j) -> mvtv_status {
@@ -571,62 +663,74 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         double* gn = gbuf[(j + 1) & 1];
         double* zo = ebuf[j & 1];
         double* zn = ebuf[(j + 1) & 1];
-        // -- theta-solve: local forward passes, the last one into the packed send buffer
+        // -- theta-solve: forward passes along dims 0..p-3 in place; along dim p-2 by pieces into the
+        //    packed send buffer, each piece's all-to-all on sc as soon as it is written
         for (int d = 0; d <= p - 2; ++d) {
-            const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
             const bool last = d == p - 2;
-            if (d == 0)
-                HIP_TRY(launch_dct_pass(P->spec, og, s, 0, 0, P->oty + sg.off, P->ga + sg.off, 0.0, gp + sg.off, 0.0,
-                                        last ? sendbuf : th, 0.0, 1.0, P->ctl, 0, 0.0, nullptr,
-                                        last ? pko : nullptr));
-            else
-                HIP_TRY(launch_dct_pass(P->spec, og, s, 0, d, th, nullptr, 0.0, nullptr, 0.0,
-                                        last ? sendbuf : th, 0.0, 1.0, P->ctl, 0, 0.0, nullptr,
-                                        last ? pko : nullptr));
-            P->tstop(h);
+            const int npc = last ? K : 1;
+            for (int k = 0; k < npc; ++k) {
+                const LinePiece pc = piece_pass(k);
+                const LinePiece* pcp = (last && K > 1) ? &pc : nullptr;
+                const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
+                if (d == 0)
+                    HIP_TRY(launch_dct_pass(P->spec, og, s, 0, 0, P->oty + sg.off, P->ga + sg.off, 0.0, gp + sg.off, 0.0,
+                                            last ? sendbuf : th, 0.0, 1.0, P->ctl, 0, 0.0, nullptr,
+                                            last ? pko : nullptr));
+                else
+                    HIP_TRY(launch_dct_pass(P->spec, og, s, 0, d, th, nullptr, 0.0, nullptr, 0.0, last ? sendbuf : th,
+                                            0.0, 1.0, P->ctl, 0, 0.0, nullptr, last ? pko : nullptr, nullptr, pcp));
+                P->tstop(h);
+                if (last && !solo) {
+                    MVTV_TRY(handoff(ef[k], s, sc));
+                    MVTV_TRY(a2a_fwd(k));
+                    HIP_TRY(hipEventRecord(er[k], sc));
+                }
+            }
         }
-        // -- all-to-all: my planes x rank r's chunk -> rank r; rank r's planes x my chunk <- rank r
-        if (!solo) {
-            MVTV_TRY(C->begin());
-            for (int r = 0; r < G; ++r)
-                MVTV_TRY(C->send(sendbuf + size_t(r) * sg.nz * sg.chunk, size_t(sg.nz) * sg.chunk, r, s));
-            for (int r = 0; r < G; ++r)
-                MVTV_TRY(C->recv(linebuf + size_t(zbs[size_t(r)]) * sg.chunk,
-                                 size_t(zbs[size_t(r) + 1] - zbs[size_t(r)]) * sg.chunk, r, s));
-            MVTV_TRY(C->end(s));
-        }
-        {
+        // -- last dimension (forward / divide / inverse or the tridiagonal solve) per piece, then its way back
+        for (int k = 0; k < K; ++k) {
+            if (!solo) HIP_TRY(hipStreamWaitEvent(s, er[k], 0));
+            const LinePiece pc = piece_mid(k);
+            double* lb = linebuf + size_t(k) * sg.mg * pch;
             const int h = P->tstart(MVTV_K_DCT);
-            HIP_TRY(launch_dct_pass(P->spec, lg, s, 2, p - 1, linebuf, nullptr, 0.0, nullptr, 0.0, linebuf, 0.0, 1.0,
-                                    P->ctl, uint32_t(rk) * sg.chunk, inv_n));
+            HIP_TRY(launch_dct_pass(P->spec, K > 1 ? lgk : lg, s, 2, p - 1, lb, nullptr, 0.0, nullptr, 0.0, lb, 0.0, 1.0,
+                                    P->ctl, uint32_t(rk) * sg.chunk, inv_n, nullptr, nullptr, nullptr,
+                                    K > 1 ? &pc : nullptr));
             P->tstop(h);
+            if (!solo) {
+                MVTV_TRY(handoff(et[k], s, sc));
+                MVTV_TRY(a2a_back(k));
+                HIP_TRY(hipEventRecord(eb[k], sc));
+            }
         }
-        if (!solo) {
-            MVTV_TRY(C->begin());
-            for (int r = 0; r < G; ++r)
-                MVTV_TRY(C->send(linebuf + size_t(zbs[size_t(r)]) * sg.chunk,
-                                 size_t(zbs[size_t(r) + 1] - zbs[size_t(r)]) * sg.chunk, r, s));
-            for (int r = 0; r < G; ++r)
-                MVTV_TRY(C->recv(sendbuf + size_t(r) * sg.nz * sg.chunk, size_t(sg.nz) * sg.chunk, r, s));
-            MVTV_TRY(C->end(s));
-        }
-        // -- local inverse passes, the first one from the packed buffer
+        // -- inverse passes: dim p-2 by pieces from the packed buffer, then dims p-3..0 in place
         for (int d = p - 2; d >= 0; --d) {
-            const int h = P->tstart(MVTV_K_DCT);
             const bool first = d == p - 2;
-            HIP_TRY(launch_dct_pass(P->spec, og, s, 1, d, first ? sendbuf : th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0,
-                                    P->ctl, 0, 0.0, nullptr, first ? pki : nullptr));
-            P->tstop(h);
+            const int npc = first ? K : 1;
+            for (int k = 0; k < npc; ++k) {
+                if (first && !solo) HIP_TRY(hipStreamWaitEvent(s, eb[k], 0));
+                const LinePiece pc = piece_pass(k);
+                const int h = P->tstart(MVTV_K_DCT);
+                HIP_TRY(launch_dct_pass(P->spec, og, s, 1, d, first ? sendbuf : th, nullptr, 0.0, nullptr, 0.0, th, 0.0,
+                                        1.0, P->ctl, 0, 0.0, nullptr, first ? pki : nullptr, nullptr,
+                                        (first && K > 1) ? &pc : nullptr));
+                P->tstop(h);
+            }
         }
         // -- theta halo: both ghost planes
-        MVTV_TRY(C->begin());
-        if (rk > 0) MVTV_TRY(C->send(P->theta + first_owned, pl, rk - 1, s));
-        if (rk < G - 1) MVTV_TRY(C->send(P->theta + last_owned, pl, rk + 1, s));
-        if (rk > 0) MVTV_TRY(C->recv(P->theta, pl, rk - 1, s));
-        if (rk < G - 1) MVTV_TRY(C->recv(P->theta + last_owned + pl, pl, rk + 1, s));
-        MVTV_TRY(C->end(s));
+        if (!solo) {
+            MVTV_TRY(handoff(ev[EV_TH], s, sc));
+            MVTV_TRY(C->begin());
+            if (rk > 0) MVTV_TRY(C->send(P->theta + first_owned, pl, rk - 1, sc));
+            if (rk < G - 1) MVTV_TRY(C->send(P->theta + last_owned, pl, rk + 1, sc));
+            if (rk > 0) MVTV_TRY(C->recv(P->theta, pl, rk - 1, sc));
+            if (rk < G - 1) MVTV_TRY(C->recv(P->theta + last_owned + pl, pl, rk + 1, sc));
+            MVTV_TRY(C->end(sc));
+            MVTV_TRY(handoff(ev[EV_THD], sc, s));
+        }
         // -- edge update + gather on the owned planes, partial sums into P->red
         if (fused) {
+            if (zh_pending) HIP_TRY(hipStreamWaitEvent(s, ev[EV_ZH], 0));   // z_old's ghost plane is in place
             int h = P->tstart(MVTV_K_ADMM_FUSED);
             int npf = 0;
             HIP_TRY(launch_admm3d(P->g, P->order, um, s, P->theta, zo, zn, 0.0, 1.0, 0.0, 1.0, nullptr, P->ga, gn, gp,
@@ -645,10 +749,14 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
             P->tstop(h);
             HIP_TRY(launch_finalize(s, P->partials, npe, ER_N, 1, 0, P->red, P->st, 0.0, 0, P->ctl));
             // D^T at the first owned plane reads the new z of plane zb-1 (rank-1's last plane)
-            MVTV_TRY(C->begin());
-            if (rk < G - 1) MVTV_TRY(edge_plane_xfer(P->edges, last_owned / pl, rk + 1, true));
-            if (rk > 0) MVTV_TRY(edge_plane_xfer(P->edges, 0, rk - 1, false));
-            MVTV_TRY(C->end(s));
+            if (!solo) {
+                MVTV_TRY(handoff(ev[EV_EDGE], s, sc));
+                MVTV_TRY(C->begin());
+                if (rk < G - 1) MVTV_TRY(edge_plane_xfer(P->edges, last_owned / pl, rk + 1, true));
+                if (rk > 0) MVTV_TRY(edge_plane_xfer(P->edges, 0, rk - 1, false));
+                MVTV_TRY(C->end(sc));
+                MVTV_TRY(handoff(ev[EV_EDGED], sc, s));
+            }
             h = P->tstart(MVTV_K_GATHER);
             const int hb = P->tstart_b(MVTV_K_GATHER4B);
             int npg = P->grid;
@@ -663,20 +771,28 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
             HIP_TRY(launch_finalize(s, P->partials, npg, GR_N, 0, 0, P->red + ER_N, P->st, 0.0, 0, P->ctl));
         }
         // -- global sums, then every rank's identical decision
-        MVTV_TRY(C->allreduce_sum(P->red, ER_N + GR_N, s));
+        if (!solo) {
+            MVTV_TRY(handoff(ev[EV_RED], s, sc));
+            MVTV_TRY(C->allreduce_sum(P->red, ER_N + GR_N, sc));
+            MVTV_TRY(handoff(ev[EV_AR], sc, s));
+        }
         HIP_TRY(launch_admm_control(s, P->ctl, P->red));
-        // -- z halo for the next iteration's chunk-start recompute (fused): rank-1's last plane of z_new
-        if (fused) {
+        // -- z halo for the next iteration's chunk-start recompute (fused): rank-1's last plane of z_new, on sc
+        //    (z_new is complete: EV_RED was recorded after the fused pass) while s starts the next solve
+        if (fused && !solo) {
             MVTV_TRY(C->begin());
             if (rk < G - 1) MVTV_TRY(edge_plane_xfer(zn, last_owned / pl, rk + 1, true));
             if (rk > 0) MVTV_TRY(edge_plane_xfer(zn, 0, rk - 1, false));
-            MVTV_TRY(C->end(s));
+            MVTV_TRY(C->end(sc));
+            HIP_TRY(hipEventRecord(ev[EV_ZH], sc));
+            zh_pending = true;
         }
         return MVTV_OK;
     };
 
     // batches of iterations between polls: a schedule that depends only on the (identical) decisions, so
-    // every rank enqueues the same collectives
+    // every rank enqueues the same collectives. Iterations enqueued past convergence are no-ops in their
+    // kernels, but their collectives still move their buffers
     const int limit = opts->fixed_iters > 0 ? opts->fixed_iters : max_counter + 1;
     int target = opts->fixed_iters > 0 ? opts->fixed_iters : 16;
     int enq = 0;
@@ -691,6 +807,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         if (c.done || enq >= limit) break;
         target = enq + std::max(4, enq / 4);
     }
+    if (!solo) HIP_TRY(hipStreamSynchronize(sc));   // the last z halo
     const int it_done = c.it;
     if (P->timing && it_done < int(mark.size()))
         for (size_t e = mark[size_t(it_done)]; e < P->pending.size(); ++e) P->pending[e].kid = -1;

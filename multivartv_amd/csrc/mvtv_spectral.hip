@@ -73,6 +73,8 @@ struct SpecArgs {
     // (plane size 2^pk_lpl, chunk 2^pk_lch lines per rank, pk_nz owned planes)
     int32_t pk;
     uint32_t pk_lpl, pk_lch, pk_nz;
+    uint32_t pk_lk, pk_lm0;   // pieces of the pipelined transposes (DctPack)
+    uint32_t rm_lw, rm_ls, rm_xoff;   // LinePiece: local line -> mesh line (0 = identity)
     // mixed-radix lengths (k_dctg): the FFT's radices in stage order, division by the line stride
     int32_t nrad;
     int32_t rad[8];
@@ -88,7 +90,17 @@ struct SpecArgs {
 __device__ __forceinline__ uint32_t pack_index(const SpecArgs& a, uint32_t i) {
     const uint32_t z = i >> a.pk_lpl, q = i & ((1u << a.pk_lpl) - 1u);
     const uint32_t s = q >> a.pk_lch;
-    return ((s * a.pk_nz + z) << a.pk_lch) | (q & ((1u << a.pk_lch) - 1u));
+    if (!a.pk_lk) return ((s * a.pk_nz + z) << a.pk_lch) | (q & ((1u << a.pk_lch) - 1u));
+    // [piece][rank][plane][row of the chunk][dim-0 index in the piece]
+    const uint32_t lw = a.pk_lm0 - a.pk_lk, lrows = a.pk_lch - a.pk_lm0;
+    const uint32_t x = q & ((1u << a.pk_lm0) - 1u), yr = (q >> a.pk_lm0) & ((1u << lrows) - 1u);
+    const uint32_t k = x >> lw, G = 1u << (a.pk_lpl - a.pk_lch);
+    return (((((k * G + s) * a.pk_nz + z) << lrows) + yr) << lw) | (x & ((1u << lw) - 1u));
+}
+
+// mesh line of local line q of a piece pass (LinePiece), identity without pieces
+__device__ __forceinline__ uint32_t piece_line(const SpecArgs& a, uint32_t q) {
+    return a.rm_lw ? ((q >> a.rm_lw) << a.rm_ls) + a.rm_xoff + (q & ((1u << a.rm_lw) - 1u)) : q;
 }
 
 enum SpecMode { SPEC_FWD = 0, SPEC_INV = 1, SPEC_MID = 2 };
@@ -226,9 +238,9 @@ __global__ __launch_bounds__(spec::NT) void k_dct(const SpecArgs a) {
 
     if (MODE == SPEC_MID && threadIdx.x < uint32_t(tq)) {
         // line q indexes dims 0..p-2 column-major (d = p - 1): split mu into c0 + c1 * lam_d(k)
-        const uint32_t q = a.q_off + q0 + threadIdx.x;
+        const uint32_t ql = q0 + threadIdx.x;
         double lamv[kMaxDims] = {0, 0, 0, 0};
-        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
+        uint32_t rest = a.q_off + piece_line(a, ql < a.nlines ? ql : 0u);
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int j = 0; j < a.p; ++j) {
             if (j == a.d) continue;
@@ -538,9 +550,9 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
     const double2* __restrict__ tw = a.tw;
 
     for (int l = t; MODE == SPEC_MID && l < a.tq; l += S::NT) {
-        const uint32_t q = a.q_off + q0 + l;
+        const uint32_t ql = q0 + l;
         double lamv[kMaxDims] = {0, 0, 0, 0};
-        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
+        uint32_t rest = a.q_off + piece_line(a, ql < a.nlines ? ql : 0u);
         // line q enumerates the dims other than d, dim 0 fastest
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int jj = 0; jj < a.p; ++jj) {
@@ -564,8 +576,9 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
 
     // element k of real line ql (local) -> global offset
     auto gaddr = [&](int ql, uint32_t k) -> uint32_t {
-        const uint32_t q = q0 + uint32_t(ql);
+        uint32_t q = q0 + uint32_t(ql);
         if (D0) return (q << L) + k;
+        if (MODE != SPEC_MID) q = piece_line(a, q);   // a piece of the lines (pipelined slab transposes)
         return (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (k << a.ls);
     };
     auto ld2 = [&](uint32_t k) -> double2 {   // (line la, line lb) at position k, b formed if FORMB
@@ -904,9 +917,9 @@ __global__ __launch_bounds__(dctg::NT) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint32_t q0 = blockIdx.x * uint32_t(tq);
 
     if (MODE == SPEC_MID && threadIdx.x < uint32_t(tq)) {
-        const uint32_t q = a.q_off + q0 + threadIdx.x;
+        const uint32_t ql = q0 + threadIdx.x;
         double lamv[kMaxDims] = {0, 0, 0, 0};
-        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
+        uint32_t rest = a.q_off + piece_line(a, ql < a.nlines ? ql : 0u);
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int j = 0; j < a.p; ++j) {
             if (j == a.d) continue;
@@ -1134,8 +1147,7 @@ __global__ __launch_bounds__((tri::Shape<L, SEG, TQL>::NT)) void k_tri(const Spe
     double lamv[kMaxDims] = {0, 0, 0, 0};
     if (t < TQ) {
         // c0 + c1 T along d for this line (q indexes dims 0..p-2 column-major, as k_dct8's MID)
-        const uint32_t ql = a.q_off + (valid ? q : q0);
-        uint32_t rest = ql;
+        uint32_t rest = a.q_off + piece_line(a, valid ? q : q0);
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int jj = 0; jj < a.p; ++jj) {
             if (jj == a.d) continue;
@@ -1286,9 +1298,8 @@ __global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nse
         g[i] = (valid && i < sl) ? __builtin_nontemporal_load(a.in + base + uint32_t(i) * a.stride) : 0.0;
 
     if (t < TQ) {
-        const uint32_t ql = a.q_off + qq;
         double lamv[kMaxDims] = {0, 0, 0, 0};
-        uint32_t rest = ql;
+        uint32_t rest = a.q_off + piece_line(a, qq);
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int jj = 0; jj < a.p; ++jj) {
             if (jj == a.d) continue;
@@ -1568,6 +1579,7 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
     if (d0 && t0 > 0) want = t0;
     if (!d0 && t1 > 0) want = t1;
     if (!d0) want = std::min<int>(want, int(a.stride));
+    if (!d0 && a.rm_lw && mode != SPEC_MID) want = std::min<int>(want, 1 << a.rm_lw);   // tiles inside a piece row
     a.xcd = xcd_env >= 0 ? xcd_env : (xcd_def ? 1 : 0);
     if (try_tile<L, 2>(a, s, mode, d0, formb, want) || try_tile<L, 4>(a, s, mode, d0, formb, want) ||
         try_tile<L, 8>(a, s, mode, d0, formb, want) || try_tile<L, 16>(a, s, mode, d0, formb, want) ||
@@ -1592,13 +1604,21 @@ bool dct_pcg_fusable(const Geom& g, size_t partial_words) {
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
                            double w0, const AdmmCtl* ctl, uint32_t q_off, double inv_n, const int32_t* skip,
-                           const DctPack* pack, const PcgFuse* pf) {
+                           const DctPack* pack, const PcgFuse* pf, const LinePiece* piece) {
     SpecArgs a{};
     if (pack && pack->mode) {
         a.pk = pack->mode;
         a.pk_lpl = pack->lpl;
         a.pk_lch = pack->lch;
         a.pk_nz = pack->nz;
+        a.pk_lk = pack->lk;
+        a.pk_lm0 = pack->lm0;
+        if (a.pk_lk && (a.pk_lch < a.pk_lm0 || a.pk_lk > a.pk_lm0)) return hipErrorInvalidValue;
+    }
+    if (piece && piece->lw) {
+        a.rm_lw = piece->lw;
+        a.rm_ls = piece->ls;
+        a.rm_xoff = piece->xoff;
     }
     a.ctl = ctl;
     a.skip = skip;
@@ -1626,6 +1646,10 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     while ((1u << a.ls) < a.stride) ++a.ls;
     const uint32_t m = g.m[d];
     a.nlines = g.N / m;
+    if (a.rm_lw) {   // FWD / INV: a piece of the mesh's lines along d > 0; MID: the piece buffer's own lines
+        if (piece->nlines == 0 || (mode != SPEC_MID && d == 0)) return hipErrorInvalidValue;
+        a.nlines = piece->nlines;
+    }
     a.d = d;
     a.p = g.p;
     a.L = 0;
@@ -1639,7 +1663,7 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
         a.pf = *pf;
     }
     if ((1u << a.L) != m || (1u << a.ls) != a.stride) {   // mixed radix, or a power of two over a general stride
-        if (a.pk || !dct_radix_plan(m, a.rad, &a.nrad)) return hipErrorInvalidValue;
+        if (a.pk || (a.rm_lw && mode != SPEC_MID) || !dct_radix_plan(m, a.rad, &a.nrad)) return hipErrorInvalidValue;
         a.fds = FastDiv(a.stride);
         a.fm = FastDiv(m);
         for (int st = 0, L = 1; st < a.nrad; ++st) {
@@ -1664,7 +1688,9 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
         launch_dctg(a, s, mode, d == 0, formb);
         return hipGetLastError();
     }
-    if (a.pk && a.L < 3) return hipErrorInvalidValue;   // the packed layout is served by k_dct8 only
+    if ((a.pk || (a.rm_lw && mode != SPEC_MID)) && a.L < 3)
+        return hipErrorInvalidValue;   // packed layouts and piece addressing are served by k_dct8 only
+    if (a.rm_lw && mode != SPEC_MID && probe_env("MVTV_DCT_LDS")) return hipErrorInvalidValue;
     if (const int tq = tri_tiles(a, mode, formb)) {
         launch_tri(a, s, tq);
         return hipGetLastError();
