@@ -136,12 +136,15 @@ def assign(n_items: int, world: int, rank: int):
 
 
 def mbs_impl(data, y, m, mesh=None, n_lambda=100, ftrue=None, lambdas=None, folds=1, verbose=False, seed=0,
-             device=None, group=None, _runner=None):
+             device=None, group=None, _runner=None, concurrent=1):
     """rcpp…/solvers.cpp:305-376. Returns the reference's result list as a dict (rank 0; other
     ranks return only 'cv.mses' and 'lambda_minmse_ind').
 
     ``_runner(kind, fold)`` replaces the GPU path computation (tests of the distribution logic):
     it returns (mse_vector, final_models) exactly as the internal runner does.
+
+    ``concurrent``: work items of this rank run at once, each on its own problem (HIP stream) and host
+    thread; the items are independent, so results do not depend on it.
     """
     data = np.asarray(data, dtype=np.float64)
     if data.ndim == 1:
@@ -160,9 +163,16 @@ def mbs_impl(data, y, m, mesh=None, n_lambda=100, ftrue=None, lambdas=None, fold
     state = {}
     AXES = tensor_axes(MESH, m)
 
-    def problem_for(x, yy):
-        P, idx = _cache(MESH, m, deltas, x, yy, device, state.get("P"), AXES)
-        state["P"] = P
+    import threading
+    lock = threading.Lock()
+
+    def problem_for(x, yy, own=False):
+        """The rank's shared problem (set to this data), or with own=True a new one (concurrent items)."""
+        if own:
+            return _cache(MESH, m, deltas, x, yy, device, None, AXES)
+        with lock:
+            P, idx = _cache(MESH, m, deltas, x, yy, device, state.get("P"), AXES)
+            state["P"] = P
         return P, idx
 
     if lambdas is None or _runner is None:
@@ -172,20 +182,26 @@ def mbs_impl(data, y, m, mesh=None, n_lambda=100, ftrue=None, lambdas=None, fold
         LAMBDAS = np.asarray(lambdas, dtype=np.float64).ravel()
     nl = LAMBDAS.size
 
+    own = concurrent > 1
+
     def runner(kind, f):
         if kind == "final":
             # models' mse: mbs_mse against ftrue (folds == 1) or y (:214, :355); test_mse against y (:330)
-            P, idx = problem_for(data, y)
+            P, idx = problem_for(data, y, own)
             thetas, stats = mbs_path(P, LAMBDAS, y.mean())
+            if own:
+                P.close()
             fitted = [th[idx] for th in thetas]
             ref = FTRUE if folds == 1 else y
             model_mses = np.array([np.sum((ft - ref) ** 2) / ref.size for ft in fitted])
             test = np.array([np.sum((ft - y) ** 2) / y.size for ft in fitted])
             return test, dict(thetas=thetas, fitted=fitted, stats=stats, model_mses=model_mses)
         tr, te = foldinds != f, foldinds == f
-        P, _ = problem_for(data[tr], y[tr])
+        P, _ = problem_for(data[tr], y[tr], own)
         thetas, _ = mbs_path(P, LAMBDAS, y[tr].mean())
         ti = P.nearest(AXES, data[te]) if AXES is not None else nearest_index(data[te], MESH)
+        if own:
+            P.close()
         yt = y[te]
         return np.array([np.sum((th[ti] - yt) ** 2) / yt.size for th in thetas]), None
 
@@ -193,7 +209,9 @@ def mbs_impl(data, y, m, mesh=None, n_lambda=100, ftrue=None, lambdas=None, fold
     n_items = 1 + (folds if folds > 1 else 0)
     mse_mat = np.zeros((nl, max(folds, 1)))
     final = None
-    for item in assign(n_items, world, rank):
+
+    def do_item(item):
+        nonlocal final
         if item == 0:
             mses, final = run("final", None)
             if folds == 1:
@@ -202,6 +220,16 @@ def mbs_impl(data, y, m, mesh=None, n_lambda=100, ftrue=None, lambdas=None, fold
             mse_mat[:, item - 1], _ = run("fold", item - 1)
         if verbose:
             print(f"[rank {rank}] work item {item} done")
+
+    mine = assign(n_items, world, rank)
+    if concurrent > 1 and len(mine) > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=min(concurrent, len(mine))) as ex:
+            for fut in [ex.submit(do_item, it) for it in mine]:
+                fut.result()
+    else:
+        for item in mine:
+            do_item(item)
     if dist is not None and world > 1:
         mse_mat = _allreduce_sum(dist, group, mse_mat)
     cv = mse_mat[:, 0] if folds == 1 else mse_mat.mean(axis=1)

@@ -13,6 +13,7 @@ from oracle import mvtv_oracle as O
 
 mv = pytest.importorskip("multivartv_amd")
 from multivartv_amd import cv  # noqa: E402
+from multivartv_amd.synth import towers  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -124,6 +125,50 @@ def _rank_main(rank, world, port, q):
     q.put((rank, out["cv.mses"].tolist(), out["lambda_minmse_ind"],
            out["theta_hat"].tolist() if rank == 0 else None))
     dist.destroy_process_group()
+
+
+def test_mbs_impl_concurrent_items_match_serial():
+    """Work items on their own problems / HIP streams at once (host threads): bit-identical to one at a time."""
+    x, y = _scattered(240, 2, seed=3)
+    serial = cv.mbs_impl(x, y, [10, 8], lambdas=LAMS, folds=3, seed=11, group=False)
+    conc = cv.mbs_impl(x, y, [10, 8], lambdas=LAMS, folds=3, seed=11, group=False, concurrent=4)
+    assert np.array_equal(conc["cv.mses"], serial["cv.mses"])
+    assert conc["lambda_minmse_ind"] == serial["lambda_minmse_ind"]
+    assert np.array_equal(conc["theta_hat"], serial["theta_hat"])
+    for a, b in zip(conc["models"], serial["models"]):
+        assert np.array_equal(a["theta_hat"], b["theta_hat"])
+
+
+def test_concurrent_fold_paths_on_streams_2048():
+    """Config 4's batched work items as bench.py --mode cv runs them: 3 fold paths of 2048^2 at once (one
+    problem, stream and host thread each) give the same iterations, rho and theta as one at a time."""
+    import threading
+    m = [2048, 2048]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    fold = cv.kfoldinds(y.size, 5, seed=0)
+    lams = np.array([1.6, 1.2, 0.9, 0.7])
+    probs = []
+    for f in range(3):
+        W = (fold != f).astype(np.float64)
+        probs.append((mv.Problem(m, W * y, wdiag=W, deltas=deltas, order=mv.ORDER_CPP), float(y[W > 0].mean())))
+    seq = [P.path(lams, np.full(P.N, ym), lams[0] / 5.0, fixed_iters=3) for P, ym in probs]
+    out = [None] * 3
+
+    def work(i):
+        P, ym = probs[i]
+        out[i] = P.path(lams, np.full(P.N, ym), lams[0] / 5.0, fixed_iters=3)
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for (th_s, rh_s, st_s), (th_c, rh_c, st_c) in zip(seq, out):
+        np.testing.assert_array_equal(th_s, th_c)
+        np.testing.assert_array_equal(rh_s, rh_c)
+        assert [s["pcg_iters"] for s in st_s] == [s["pcg_iters"] for s in st_c]
+    for P, _ in probs:
+        P.close()
 
 
 def test_mbs_impl_two_ranks_match_serial():
