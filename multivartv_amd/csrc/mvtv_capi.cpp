@@ -116,7 +116,7 @@ mvtv_status pick_zpair(mvtv_problem* P, bool track_theta) {
 
 void free_all(mvtv_problem* P) {
     double** bufs[] = {&P->oty, &P->wdiag, &P->theta, &P->edges, &P->ga, &P->gu, &P->guprev, &P->r,
-                       &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->slab_send, &P->slab_lines,
+                       &P->p, &P->q, &P->thold, &P->p2, &P->partials, &P->red, &P->stage, &P->slab_iface,
                        &P->edges2, &P->pcg_b, &P->g4, &P->edges3, &P->pcg_s, &P->pcg_t};
     for (double** b : bufs)
         if (*b) {
@@ -430,7 +430,7 @@ mvtv_status pcgs_solve(mvtv_problem* P, double sigma, const double* oty, const d
             }
             const int hh = P->tstart(t == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
             HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, t == 0 ? r : z, nullptr, 0.0, nullptr, 0.0, z,
-                                    sigma, w0, nullptr, 0, 0.0, skip, nullptr, f.mode ? &f : nullptr));
+                                    sigma, w0, nullptr, 0, 0.0, skip, f.mode ? &f : nullptr));
             P->tstop(hh);
         }
         HIP_TRY(launch_finalize(P->stream, P->partials, np_last, 2, 0, 3, nullptr, P->st));        // beta, done

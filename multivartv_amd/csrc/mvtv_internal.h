@@ -243,24 +243,6 @@ struct SpecPlan {
     uint32_t* perm = nullptr; // per dim (at lam_off): position of sample k in the mixed-radix FFT's input order
     uint32_t tw_off[kMaxDims] = {0, 0, 0, 0}, twq_off[kMaxDims] = {0, 0, 0, 0}, lam_off[kMaxDims] = {0, 0, 0, 0};
 };
-// The slab-decomposed solve's all-to-all buffer layout (mode 1: the pass writes `out` packed, 2: it
-// reads `in` packed): [rank][owned plane][line mod chunk], plane = 2^lpl lines, chunk = 2^lch lines.
-// With 2^lk > 1 pieces (the pipelined transposes, chunk a whole number of dim-0 rows of 2^lm0 lines):
-// [piece][rank][owned plane][row of the chunk][dim-0 index in the piece], a piece = 2^(lm0 - lk)
-// adjacent dim-0 indices, so every (piece, rank) block is contiguous
-struct DctPack {
-    int32_t mode = 0;
-    uint32_t lpl = 0, lch = 0, nz = 0;
-    uint32_t lk = 0, lm0 = 0;
-};
-// A pass over one piece of the lines (pipelined slab transposes): local line q stands for line
-// ((q >> lw) << ls) + xoff + (q mod 2^lw), i.e. rows of 2^lw lines every 2^ls lines from xoff. FWD / INV
-// passes along d > 0 address the mesh through it; MID passes take the line's eigenvalues from it (plus
-// q_off), their own lines being a contiguous piece buffer.
-struct LinePiece {
-    uint32_t lw = 0, ls = 0, xoff = 0;
-    uint32_t nlines = 0;   // lines of the piece
-};
 // PCG vector work folded into the d = 0 passes of a preconditioner solve (spectrally preconditioned PCG,
 // power-of-two m_0 >= 64): mode 1, first pass (`in` = r): r -= alpha q and x += alpha p on load (r, x
 // written back, the transform taken of sinv * r); mode 2, last pass: out = sinv * transform, (r.z, |r|^2)
@@ -284,8 +266,16 @@ bool dct_radix_plan(uint32_t m, int* rad, int* nrad);
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
                            double w0, const AdmmCtl* ctl = nullptr, uint32_t q_off = 0, double inv_n = 0.0,
-                           const int32_t* skip = nullptr, const DctPack* pack = nullptr,
-                           const PcgFuse* pf = nullptr, const LinePiece* piece = nullptr);
+                           const int32_t* skip = nullptr, const PcgFuse* pf = nullptr);
+// Slab-decomposed last-dimension solve by substructuring (mvtv_spectral.hip, k_tris): og = the owned planes
+// (m[p-1] = their count, stride[p-1] = plane lines). phase 1: per line the first / last rows of G, H, K of
+// the local block into coef [chunk s][6][line in chunk]; phase 3: x = scale * (local solve with the
+// neighbours' values lr [chunk s][2][line in chunk]) in place. lo_ext / hi_ext: the lines continue on the
+// rank below / above. launch_tri_iface: the interface systems of one chunk's lines over the G ranks.
+hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, int phase, double* x, double* coef,
+                           const double* lr, uint32_t chunk, int lo_ext, int hi_ext, double scale,
+                           const AdmmCtl* ctl);
+hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint32_t chunk, int G, const AdmmCtl* ctl);
 // z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /
 // launch_gather, *nparts workgroup rows
 bool edge3d_ok(const Geom& g);

@@ -104,8 +104,7 @@ struct mvtv_problem {
     bool slab = false;
     int64_t m_global = 0, zb = 0, ze = 0;
     int g_lo = 0, g_hi = 0;
-    double* slab_send = nullptr;   // mvtv_slab_run: the owned planes in the all-to-all's packed order
-    double* slab_lines = nullptr;  // mvtv_slab_run: full last-dimension lines of this rank's line chunk
+    double* slab_iface = nullptr;  // mvtv_slab_run: interface numbers of the distributed line solves (16 per line)
     hipStream_t comm_stream = nullptr;   // mvtv_slab_run: the collectives' stream (overlapped with `stream`)
 
     // resident ADMM state

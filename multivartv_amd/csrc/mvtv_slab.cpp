@@ -4,11 +4,12 @@
 //
 // Rank r owns planes [zb, ze) of the last dimension plus one ghost plane below / above
 // (mvtv_problem_create_slab). Per iteration:
-//   theta-solve  cosine transforms along dims 0..p-2 on the owned planes, the last of them writing the
-//                all-to-all send buffer directly in [rank][plane][line chunk] order; all-to-all (grouped
-//                send / recv) -> each rank holds full dim-(p-1) lines for 1/G of the lines; forward /
-//                divide / inverse along dim p-1; all-to-all back; the first inverse pass reads the packed
-//                buffer straight into theta. No pack or unpack copies.
+//   theta-solve  cosine transforms along dims 0..p-2 on the owned planes, in place; the tridiagonal line
+//                solves along dim p-1 by substructuring (mvtv_spectral.hip k_tris): each rank reduces its
+//                block of every line to 6 numbers, an all-to-all brings each chunk of lines' numbers to
+//                one rank, which solves the lines' interface systems over the ranks and sends every rank
+//                its lines' 2 neighbour values back; each rank then solves its blocks; inverse transforms
+//                along dims p-2..0 in place. 8 numbers per line cross the ranks instead of the mesh twice.
 //   theta halo   first owned plane -> rank-1's upper ghost, last -> rank+1's lower ghost.
 //   edge update  p = 3: the fused pass (k_admm3a) on the owned planes: its chunk-start recompute of
 //   + gather     plane zb-1 reads theta's lower ghost and z_old's lower ghost plane, which rank-1 sent
@@ -16,9 +17,10 @@
 //   reductions   one all-reduce of the 7 partial sums into the device control block; k_admm_control
 //                then takes adapt_step / stopping on every rank from bit-identical inputs.
 //   z halo       (p = 3) last owned plane of z_new -> rank+1's ghost plane of the same buffer.
-// Transports (mvtv_comm): RCCL over xGMI (one process per GPU; librccl is opened at run time, so the
-// library has no link-time dependency on it) or an in-process loopback group (every rank on its own host
-// thread, device-to-device copies between the ranks' buffers): the same loop, testable on one GPU.
+// The collectives run on a stream of their own, handed their inputs by events, so the z halo overlaps the
+// next iteration's theta-solve. Transports (mvtv_comm): RCCL over xGMI (one process per GPU; librccl is
+// resolved at run time, reusing a copy already mapped) or an in-process loopback group (every rank on its
+// own host thread, device-to-device copies between the ranks' buffers): the same loop, testable on one GPU.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -429,15 +431,9 @@ int32_t mvtv_comm_size(const mvtv_comm* c) { return c ? c->size : 0; }
 namespace {
 
 struct SlabGeom {
-    uint32_t plane = 0, nz = 0, zb = 0, mg = 0, lines = 0, chunk = 0, lpl = 0, lch = 0;
+    uint32_t plane = 0, nz = 0, zb = 0, mg = 0, lines = 0, chunk = 0;
     size_t off = 0;   // first owned node
 };
-
-uint32_t ilog2(uint32_t v) {
-    uint32_t l = 0;
-    while ((1u << l) < v) ++l;
-    return l;
-}
 
 }  // namespace
 
@@ -461,9 +457,6 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     sg.off = size_t(P->g_lo) * sg.plane;
     if (sg.lines % uint32_t(G) != 0) return fail(MVTV_BAD_ARG, "lines must split evenly over the ranks");
     sg.chunk = sg.lines / uint32_t(G);
-    if (sg.chunk < 2 || (sg.chunk & (sg.chunk - 1))) return fail(MVTV_BAD_ARG, "line chunk must be a power of two >= 2");
-    sg.lpl = ilog2(sg.plane);
-    sg.lch = ilog2(sg.chunk);
     // every rank's plane range, floor(m_global r / G) as plane_bounds (multivartv_amd/slab.py): the
     // all-to-all counts
     std::vector<uint32_t> zbs(size_t(G) + 1);
@@ -485,12 +478,11 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     const double tol = opts->tol > 0 ? opts->tol : 1e-4;
     const int max_counter = opts->max_counter > 0 ? opts->max_counter : 3000;
     const bool fused = P->f3d;
-    // buffers of the distributed solve: send = the owned planes in packed order, lines = m_global x chunk.
-    // One rank: the packed order is the natural one and the lines are the owned planes, so the whole
-    // solve runs in place on theta with no transfers
+    // interface buffers of the distributed line solves (16 numbers per line): the 6 coefficients of this
+    // rank's blocks by chunk, the chunk's coefficients from every rank, the (L, R) values by rank, and the
+    // values of this rank's lines by chunk. One rank: the line solves are local, no buffers, no transfers
     const bool solo = G == 1;
-    if (!solo && !P->slab_send) MVTV_TRY(alloc(&P->slab_send, size_t(sg.nz) * sg.lines));
-    if (!solo && !P->slab_lines) MVTV_TRY(alloc(&P->slab_lines, size_t(sg.mg) * sg.chunk));
+    if (!solo && !P->slab_iface) MVTV_TRY(alloc(&P->slab_iface, 16 * size_t(sg.lines)));
     if (fused && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
     const size_t nodes = P->g.N, ebytes = size_t(P->g.nb) * nodes * sizeof(double);
 
@@ -536,63 +528,21 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     og.N = sg.plane * sg.nz;
     og.ibeg = 0;
     og.iend = og.N;
-    Geom lg = P->g;
-    lg.m[p - 1] = sg.mg;
-    lg.stride[p - 1] = sg.chunk;
-    lg.N = sg.chunk * sg.mg;
-    // Pipelined transposes (p >= 3): the lines are cut into K pieces of w = m_0 / K adjacent dim-0 indices.
-    // Piece k's last local pass, its all-to-all, its last-dimension pass, its way back and its first inverse
-    // pass each depend only on piece k, so the transfers of piece k run on the collectives' stream while
-    // the compute stream transforms piece k + 1 (the line chunk must be whole dim-0 rows).
-    const uint32_t lm0 = ilog2(P->g.m[0]);
-    int K = 1;
-    if (!solo && p >= 3 && sg.lch >= lm0) {
-        K = 4;
-        const char* e = probe_env("MVTV_SLAB_PIECES");
-        if (e) K = std::max(1, std::atoi(e));
-        // a piece row keeps >= 16 lines (k_dct8's 128-B rows), the piece's line count >= 16 (k_tri tiles)
-        while (K > 1 && ((P->g.m[0] / uint32_t(K)) < 16u || (sg.chunk / uint32_t(K)) < 16u ||
-                         (uint32_t(K) & (uint32_t(K) - 1u)) != 0u))
-            K /= 2;
-    }
-    const uint32_t lk = ilog2(uint32_t(K)), lw = lm0 - lk, w = 1u << lw;
-    const size_t pch = sg.chunk / uint32_t(K);   // lines of a piece in this rank's chunk
-    DctPack pk_out{1, sg.lpl, sg.lch, sg.nz, lk, lm0}, pk_in{2, sg.lpl, sg.lch, sg.nz, lk, lm0};
-    const double inv_n = 1.0 / (double(sg.lines) * double(sg.mg));
     double* th = P->theta + sg.off;
-    double* sendbuf = solo ? th : P->slab_send;
-    double* linebuf = solo ? th : P->slab_lines;
-    const DctPack* pko = solo ? nullptr : &pk_out;
-    const DctPack* pki = solo ? nullptr : &pk_in;
-    // LinePiece of piece k: for the local pass along dim p - 2 (lines over the owned planes) or for the
-    // last-dimension pass on the piece buffer (its chunk lines, eigenvalues from the global line index)
-    auto piece_pass = [&](int k) {
-        LinePiece pc;
-        pc.lw = lw;
-        pc.ls = lm0;
-        pc.xoff = uint32_t(k) * w;
-        pc.nlines = uint32_t(og.N / og.m[p - 2] / uint64_t(K));
-        return pc;
-    };
-    auto piece_mid = [&](int k) {
-        LinePiece pc;
-        pc.lw = lw;
-        pc.ls = lm0;
-        pc.xoff = uint32_t(k) * w;
-        pc.nlines = uint32_t(pch);
-        return pc;
-    };
-    Geom lgk = lg;   // the last-dimension pass on one piece buffer
-    lgk.stride[p - 1] = uint32_t(pch);
-    lgk.N = pch * sg.mg;
+    const size_t ln = sg.lines, ch = sg.chunk;
+    double* co_send = P->slab_iface;          // [chunk s][6][line in chunk]
+    double* co_recv = co_send + 6 * ln;       // [rank r][6][line in my chunk]
+    double* lr_send = co_recv + 6 * ln;       // [rank r][2][line in my chunk]
+    double* lr_recv = lr_send + 2 * ln;       // [chunk s][2][line in chunk]
+    const double scale = 1.0 / double(sg.lines);   // the forward transforms along dims 0..p-2 (unnormalised)
     double* gbuf[2] = {P->guprev, P->gu};
     double* ebuf[2] = {P->edges, fused ? P->edges2 : P->edges};
     const size_t pl = sg.plane;
     const size_t first_owned = size_t(P->g_lo) * pl, last_owned = first_owned + size_t(sg.nz - 1) * pl;
 
-    // The collectives run on their own stream sc, handed data by events, so the compute stream s goes on:
-    // with the transfers of other pieces, and with the z halo (needed by the next iteration's edge pass)
-    // during the next theta-solve. One rank: no transfers, everything on s.
+    // The collectives run on their own stream sc, handed data by events, so the compute stream s goes on
+    // (the z halo, needed by the next iteration's edge pass, runs during the next theta-solve). One rank: no
+    // transfers, everything on s.
     hipStream_t sc = s;
     if (!solo) {
         if (!P->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&P->comm_stream, hipStreamNonBlocking));
@@ -604,20 +554,15 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
             for (auto e : v) (void)hipEventDestroy(e);
         }
     } evs;
-    auto mkev = [&](size_t n) -> mvtv_status {
-        for (size_t i = evs.v.size(); i < n; ++i) {
-            hipEvent_t e = nullptr;
-            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            evs.v.push_back(e);
-        }
-        return MVTV_OK;
-    };
-    // events: per piece ef (packed, s -> sc), er (received, sc -> s), et (solved, s -> sc), eb (back, sc -> s);
-    // then theta ready, theta halo done, sums ready, sums reduced, edges ready, z ghost in place, z halo done
-    enum { EV_TH = 0, EV_THD, EV_RED, EV_AR, EV_EDGE, EV_EDGED, EV_ZH, EV_FIXED };
-    MVTV_TRY(mkev(size_t(EV_FIXED) + 4 * size_t(K)));
+    // coefficients ready / gathered, neighbour values ready / delivered, theta ready / halo done, sums ready /
+    // reduced, edges ready / halo done, z halo done
+    enum { EV_CO = 0, EV_COD, EV_LR, EV_LRD, EV_TH, EV_THD, EV_RED, EV_AR, EV_EDGE, EV_EDGED, EV_ZH, EV_N };
+    for (int i = 0; i < EV_N; ++i) {
+        hipEvent_t e = nullptr;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        evs.v.push_back(e);
+    }
     hipEvent_t* ev = evs.v.data();
-    hipEvent_t *ef = ev + EV_FIXED, *er = ef + K, *et = er + K, *eb = et + K;
     auto handoff = [&](hipEvent_t e, hipStream_t from, hipStream_t to) -> mvtv_status {
         HIP_TRY(hipEventRecord(e, from));
         HIP_TRY(hipStreamWaitEvent(to, e, 0));
@@ -637,23 +582,11 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         }
         return MVTV_OK;
     };
-    // piece k of the forward transpose: my planes x rank r's lines -> rank r; rank r's planes x my lines <- r
-    auto a2a_fwd = [&](int k) -> mvtv_status {
+    // all-to-all of k numbers per line: block r of `send` (k x chunk) -> rank r, rank r's -> block r of `recv`
+    auto a2a = [&](const double* send, double* recv, size_t k) -> mvtv_status {
         MVTV_TRY(C->begin());
-        for (int r = 0; r < G; ++r)
-            MVTV_TRY(C->send(sendbuf + (size_t(k) * size_t(G) + size_t(r)) * sg.nz * pch, size_t(sg.nz) * pch, r, sc));
-        for (int r = 0; r < G; ++r)
-            MVTV_TRY(C->recv(linebuf + size_t(k) * sg.mg * pch + size_t(zbs[size_t(r)]) * pch,
-                             size_t(zbs[size_t(r) + 1] - zbs[size_t(r)]) * pch, r, sc));
-        return C->end(sc);
-    };
-    auto a2a_back = [&](int k) -> mvtv_status {
-        MVTV_TRY(C->begin());
-        for (int r = 0; r < G; ++r)
-            MVTV_TRY(C->send(linebuf + size_t(k) * sg.mg * pch + size_t(zbs[size_t(r)]) * pch,
-                             size_t(zbs[size_t(r) + 1] - zbs[size_t(r)]) * pch, r, sc));
-        for (int r = 0; r < G; ++r)
-            MVTV_TRY(C->recv(sendbuf + (size_t(k) * size_t(G) + size_t(r)) * sg.nz * pch, size_t(sg.nz) * pch, r, sc));
+        for (int r = 0; r < G; ++r) MVTV_TRY(C->send(send + size_t(r) * k * ch, k * ch, r, sc));
+        for (int r = 0; r < G; ++r) MVTV_TRY(C->recv(recv + size_t(r) * k * ch, k * ch, r, sc));
         return C->end(sc);
     };
 
@@ -663,59 +596,44 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         double* gn = gbuf[(j + 1) & 1];
         double* zo = ebuf[j & 1];
         double* zn = ebuf[(j + 1) & 1];
-        // -- theta-solve: forward passes along dims 0..p-3 in place; along dim p-2 by pieces into the
-        //    packed send buffer, each piece's all-to-all on sc as soon as it is written
+        // -- theta-solve: forward passes along dims 0..p-2 on the owned planes, in place
         for (int d = 0; d <= p - 2; ++d) {
-            const bool last = d == p - 2;
-            const int npc = last ? K : 1;
-            for (int k = 0; k < npc; ++k) {
-                const LinePiece pc = piece_pass(k);
-                const LinePiece* pcp = (last && K > 1) ? &pc : nullptr;
-                const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
-                if (d == 0)
-                    HIP_TRY(launch_dct_pass(P->spec, og, s, 0, 0, P->oty + sg.off, P->ga + sg.off, 0.0, gp + sg.off, 0.0,
-                                            last ? sendbuf : th, 0.0, 1.0, P->ctl, 0, 0.0, nullptr,
-                                            last ? pko : nullptr));
-                else
-                    HIP_TRY(launch_dct_pass(P->spec, og, s, 0, d, th, nullptr, 0.0, nullptr, 0.0, last ? sendbuf : th,
-                                            0.0, 1.0, P->ctl, 0, 0.0, nullptr, last ? pko : nullptr, nullptr, pcp));
-                P->tstop(h);
-                if (last && !solo) {
-                    MVTV_TRY(handoff(ef[k], s, sc));
-                    MVTV_TRY(a2a_fwd(k));
-                    HIP_TRY(hipEventRecord(er[k], sc));
-                }
-            }
-        }
-        // -- last dimension (forward / divide / inverse or the tridiagonal solve) per piece, then its way back
-        for (int k = 0; k < K; ++k) {
-            if (!solo) HIP_TRY(hipStreamWaitEvent(s, er[k], 0));
-            const LinePiece pc = piece_mid(k);
-            double* lb = linebuf + size_t(k) * sg.mg * pch;
-            const int h = P->tstart(MVTV_K_DCT);
-            HIP_TRY(launch_dct_pass(P->spec, K > 1 ? lgk : lg, s, 2, p - 1, lb, nullptr, 0.0, nullptr, 0.0, lb, 0.0, 1.0,
-                                    P->ctl, uint32_t(rk) * sg.chunk, inv_n, nullptr, nullptr, nullptr,
-                                    K > 1 ? &pc : nullptr));
+            const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
+            if (d == 0)
+                HIP_TRY(launch_dct_pass(P->spec, og, s, 0, 0, P->oty + sg.off, P->ga + sg.off, 0.0, gp + sg.off, 0.0,
+                                        th, 0.0, 1.0, P->ctl));
+            else
+                HIP_TRY(launch_dct_pass(P->spec, og, s, 0, d, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl));
             P->tstop(h);
-            if (!solo) {
-                MVTV_TRY(handoff(et[k], s, sc));
-                MVTV_TRY(a2a_back(k));
-                HIP_TRY(hipEventRecord(eb[k], sc));
-            }
         }
-        // -- inverse passes: dim p-2 by pieces from the packed buffer, then dims p-3..0 in place
+        // -- the line solves along dim p-1
+        if (solo) {   // the whole lines are here: the single-GPU pass (tridiagonal solve or DCT / divide / inverse)
+            const int h = P->tstart(MVTV_K_DCT);
+            HIP_TRY(launch_dct_pass(P->spec, og, s, 2, p - 1, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl, 0,
+                                    1.0 / (double(sg.lines) * double(sg.mg))));
+            P->tstop(h);
+        } else {
+            int h = P->tstart(MVTV_K_DCT);
+            HIP_TRY(launch_tri_slab(P->spec, og, s, 1, th, co_send, nullptr, uint32_t(ch), rk > 0, rk < G - 1, scale,
+                                    P->ctl));
+            P->tstop(h);
+            MVTV_TRY(handoff(ev[EV_CO], s, sc));
+            MVTV_TRY(a2a(co_send, co_recv, 6));
+            MVTV_TRY(handoff(ev[EV_COD], sc, s));
+            HIP_TRY(launch_tri_iface(s, co_recv, lr_send, uint32_t(ch), G, P->ctl));
+            MVTV_TRY(handoff(ev[EV_LR], s, sc));
+            MVTV_TRY(a2a(lr_send, lr_recv, 2));
+            MVTV_TRY(handoff(ev[EV_LRD], sc, s));
+            h = P->tstart(MVTV_K_DCT);
+            HIP_TRY(launch_tri_slab(P->spec, og, s, 3, th, nullptr, lr_recv, uint32_t(ch), rk > 0, rk < G - 1, scale,
+                                    P->ctl));
+            P->tstop(h);
+        }
+        // -- inverse passes along dims p-2..0, in place
         for (int d = p - 2; d >= 0; --d) {
-            const bool first = d == p - 2;
-            const int npc = first ? K : 1;
-            for (int k = 0; k < npc; ++k) {
-                if (first && !solo) HIP_TRY(hipStreamWaitEvent(s, eb[k], 0));
-                const LinePiece pc = piece_pass(k);
-                const int h = P->tstart(MVTV_K_DCT);
-                HIP_TRY(launch_dct_pass(P->spec, og, s, 1, d, first ? sendbuf : th, nullptr, 0.0, nullptr, 0.0, th, 0.0,
-                                        1.0, P->ctl, 0, 0.0, nullptr, first ? pki : nullptr, nullptr,
-                                        (first && K > 1) ? &pc : nullptr));
-                P->tstop(h);
-            }
+            const int h = P->tstart(MVTV_K_DCT);
+            HIP_TRY(launch_dct_pass(P->spec, og, s, 1, d, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl));
+            P->tstop(h);
         }
         // -- theta halo: both ghost planes
         if (!solo) {

@@ -65,16 +65,9 @@ struct SpecArgs {
     uint32_t nlines;         // N / m
     int32_t d, p, L, tq;     // line dimension, dims, log2 m, lines per workgroup
     int32_t ls;              // log2 stride
-    uint32_t q_off;          // MID: global index of line 0 (slab-decomposed solve works on a line chunk)
+    uint32_t q_off;          // MID: global index of line 0
     const int32_t* skip;     // != nullptr and *skip: return at once (preconditioner of a converged PCG)
     const AdmmCtl* ctl;      // asynchronous ADMM loop: sigma, ca = rho, cb = rho c_prev from the device
-    // slab decomposition: `out` (pk = 1) or `in` (pk = 2) is the all-to-all buffer of the distributed
-    // solve, packed as [rank s][owned plane z][line q mod chunk] with line q = the index over dims 0..p-2
-    // (plane size 2^pk_lpl, chunk 2^pk_lch lines per rank, pk_nz owned planes)
-    int32_t pk;
-    uint32_t pk_lpl, pk_lch, pk_nz;
-    uint32_t pk_lk, pk_lm0;   // pieces of the pipelined transposes (DctPack)
-    uint32_t rm_lw, rm_ls, rm_xoff;   // LinePiece: local line -> mesh line (0 = identity)
     // mixed-radix lengths (k_dctg): the FFT's radices in stage order, division by the line stride
     int32_t nrad;
     int32_t rad[8];
@@ -85,23 +78,6 @@ struct SpecArgs {
     int32_t xcd;              // k_dct8: tiles dealt to the XCDs in contiguous runs (grid a multiple of 8)
     PcgFuse pf;               // k_dct8 PC = 1 / 2: the PCG vector work of the preconditioner's d = 0 passes
 };
-
-// element offset in a packed all-to-all buffer of the element at offset i of the owned planes
-__device__ __forceinline__ uint32_t pack_index(const SpecArgs& a, uint32_t i) {
-    const uint32_t z = i >> a.pk_lpl, q = i & ((1u << a.pk_lpl) - 1u);
-    const uint32_t s = q >> a.pk_lch;
-    if (!a.pk_lk) return ((s * a.pk_nz + z) << a.pk_lch) | (q & ((1u << a.pk_lch) - 1u));
-    // [piece][rank][plane][row of the chunk][dim-0 index in the piece]
-    const uint32_t lw = a.pk_lm0 - a.pk_lk, lrows = a.pk_lch - a.pk_lm0;
-    const uint32_t x = q & ((1u << a.pk_lm0) - 1u), yr = (q >> a.pk_lm0) & ((1u << lrows) - 1u);
-    const uint32_t k = x >> lw, G = 1u << (a.pk_lpl - a.pk_lch);
-    return (((((k * G + s) * a.pk_nz + z) << lrows) + yr) << lw) | (x & ((1u << lw) - 1u));
-}
-
-// mesh line of local line q of a piece pass (LinePiece), identity without pieces
-__device__ __forceinline__ uint32_t piece_line(const SpecArgs& a, uint32_t q) {
-    return a.rm_lw ? ((q >> a.rm_lw) << a.rm_ls) + a.rm_xoff + (q & ((1u << a.rm_lw) - 1u)) : q;
-}
 
 enum SpecMode { SPEC_FWD = 0, SPEC_INV = 1, SPEC_MID = 2 };
 
@@ -238,9 +214,9 @@ __global__ __launch_bounds__(spec::NT) void k_dct(const SpecArgs a) {
 
     if (MODE == SPEC_MID && threadIdx.x < uint32_t(tq)) {
         // line q indexes dims 0..p-2 column-major (d = p - 1): split mu into c0 + c1 * lam_d(k)
-        const uint32_t ql = q0 + threadIdx.x;
+        const uint32_t q = a.q_off + q0 + threadIdx.x;
         double lamv[kMaxDims] = {0, 0, 0, 0};
-        uint32_t rest = a.q_off + piece_line(a, ql < a.nlines ? ql : 0u);
+        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int j = 0; j < a.p; ++j) {
             if (j == a.d) continue;
@@ -550,9 +526,9 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
     const double2* __restrict__ tw = a.tw;
 
     for (int l = t; MODE == SPEC_MID && l < a.tq; l += S::NT) {
-        const uint32_t ql = q0 + l;
+        const uint32_t q = a.q_off + q0 + l;
         double lamv[kMaxDims] = {0, 0, 0, 0};
-        uint32_t rest = a.q_off + piece_line(a, ql < a.nlines ? ql : 0u);
+        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
         // line q enumerates the dims other than d, dim 0 fastest
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int jj = 0; jj < a.p; ++jj) {
@@ -576,9 +552,8 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
 
     // element k of real line ql (local) -> global offset
     auto gaddr = [&](int ql, uint32_t k) -> uint32_t {
-        uint32_t q = q0 + uint32_t(ql);
+        const uint32_t q = q0 + uint32_t(ql);
         if (D0) return (q << L) + k;
-        if (MODE != SPEC_MID) q = piece_line(a, q);   // a piece of the lines (pipelined slab transposes)
         return (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (k << a.ls);
     };
     auto ld2 = [&](uint32_t k) -> double2 {   // (line la, line lb) at position k, b formed if FORMB
@@ -586,17 +561,17 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
         if (D0) {
             if (va) {
                 const uint32_t g = gaddr(la, k);
-                v.x = __builtin_nontemporal_load(a.in + (a.pk == 2 ? pack_index(a, g) : g));
+                v.x = __builtin_nontemporal_load(a.in + g);
                 if (FORMB) v.x += ca * __builtin_nontemporal_load(a.ga + g) + cb * __builtin_nontemporal_load(a.gb + g);
             }
             if (vb) {
                 const uint32_t g = gaddr(lb, k);
-                v.y = __builtin_nontemporal_load(a.in + (a.pk == 2 ? pack_index(a, g) : g));
+                v.y = __builtin_nontemporal_load(a.in + g);
                 if (FORMB) v.y += ca * __builtin_nontemporal_load(a.ga + g) + cb * __builtin_nontemporal_load(a.gb + g);
             }
         } else if (va) {   // d > 0: lines la, lb are adjacent words (vb == va)
             const uint32_t g = gaddr(la, k);
-            v = ldnt2(a.in + (a.pk == 2 ? pack_index(a, g) : g));
+            v = ldnt2(a.in + g);
             if (FORMB) {
                 const double2 x1 = ldnt2(a.ga + g);
                 const double2 x2 = ldnt2(a.gb + g);
@@ -606,13 +581,12 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
         }
         return v;
     };
-    auto po = [&](uint32_t g) -> uint32_t { return a.pk == 1 ? pack_index(a, g) : g; };
     auto st2 = [&](uint32_t k, double2 v) {
         if (D0) {
-            if (va) __builtin_nontemporal_store(v.x, a.out + po(gaddr(la, k)));
-            if (vb) __builtin_nontemporal_store(v.y, a.out + po(gaddr(lb, k)));
+            if (va) __builtin_nontemporal_store(v.x, a.out + gaddr(la, k));
+            if (vb) __builtin_nontemporal_store(v.y, a.out + gaddr(lb, k));
         } else if (va) {
-            stnt2(a.out + po(gaddr(la, k)), v);
+            stnt2(a.out + gaddr(la, k), v);
         }
     };
 
@@ -645,7 +619,7 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
                         }
                         return rv;
                     } else {
-                        double2 v = ldnt2(a.in + (a.pk == 2 ? pack_index(a, g) : g));
+                        double2 v = ldnt2(a.in + g);
                         if (FORMB) {
                             const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
                             v.x += ca * g1.x + cb * g2.x;
@@ -764,7 +738,7 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
                         rr = fma(rv.y, rv.y, rr);
                         stnt2(a.out + g, v);
                     } else {
-                        stnt2(a.out + po(g), v);
+                        stnt2(a.out + g, v);
                     }
                 };
                 if (va) st_out(gaddr(la, uint32_t(2 * n)), make_double2(v0.x, v1.x));
@@ -917,9 +891,9 @@ __global__ __launch_bounds__(dctg::NT) __attribute__((amdgpu_waves_per_eu(4))) v
     const uint32_t q0 = blockIdx.x * uint32_t(tq);
 
     if (MODE == SPEC_MID && threadIdx.x < uint32_t(tq)) {
-        const uint32_t ql = q0 + threadIdx.x;
+        const uint32_t q = a.q_off + q0 + threadIdx.x;
         double lamv[kMaxDims] = {0, 0, 0, 0};
-        uint32_t rest = a.q_off + piece_line(a, ql < a.nlines ? ql : 0u);
+        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int j = 0; j < a.p; ++j) {
             if (j == a.d) continue;
@@ -1147,7 +1121,8 @@ __global__ __launch_bounds__((tri::Shape<L, SEG, TQL>::NT)) void k_tri(const Spe
     double lamv[kMaxDims] = {0, 0, 0, 0};
     if (t < TQ) {
         // c0 + c1 T along d for this line (q indexes dims 0..p-2 column-major, as k_dct8's MID)
-        uint32_t rest = a.q_off + piece_line(a, valid ? q : q0);
+        const uint32_t ql = a.q_off + (valid ? q : q0);
+        uint32_t rest = ql;
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int jj = 0; jj < a.p; ++jj) {
             if (jj == a.d) continue;
@@ -1298,8 +1273,9 @@ __global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nse
         g[i] = (valid && i < sl) ? __builtin_nontemporal_load(a.in + base + uint32_t(i) * a.stride) : 0.0;
 
     if (t < TQ) {
+        const uint32_t ql = a.q_off + qq;
         double lamv[kMaxDims] = {0, 0, 0, 0};
-        uint32_t rest = a.q_off + piece_line(a, qq);
+        uint32_t rest = ql;
         const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
         for (int jj = 0; jj < a.p; ++jj) {
             if (jj == a.d) continue;
@@ -1411,6 +1387,303 @@ __global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nse
             __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + uint32_t(i) * a.stride);
 }
 
+// =============================================================================================
+// The last dimension of a slab-decomposed mesh (mvtv_slab.cpp): the same tridiagonal line solves, with
+// every line cut at the rank boundaries, solved by substructuring instead of transposing the mesh.
+//
+// Rank r holds rows [zb_r, ze_r) of every line (its owned planes). Its local block of the line's
+// operator, with the neighbours x[zb_r - 1] = L and x[ze_r] = R as unknowns (a mirror at the mesh's own
+// ends), has the solution x = G + L H + R K (G: the data with L = R = 0; H, K: the responses to L = 1 and
+// R = 1). Phase 1 (k_tris<1>) computes, per line, the first and last rows of G, H and K (6 numbers) without
+// writing the mesh; the interface system that couples the ranks' (first, last) rows of a line is solved
+// where the line's chunk lives (k_tris_iface: one thread per line, O(G)); phase 3 (k_tris<3>) solves the
+// local block again with the now known L and R and writes x. The ranks exchange 6 + 2 numbers per line
+// instead of the 2 x (owned planes) numbers per line of two transposes: at 512^3 over 8 ranks 15 MB
+// instead of 235 MB per rank per iteration. Within a rank the block is cut into nseg segments of sl rows,
+// one thread each, as k_trig (Toeplitz interior: the segment constants are line constants in LDS).
+namespace tris {
+constexpr int NSMAX = 64, TQ = 16;
+}
+
+template <int PHASE, int SMAX>
+__global__ __launch_bounds__(1024) void k_tris(const SpecArgs a, int sl, int nseg, double* __restrict__ x,
+                                               double* __restrict__ coef, const double* __restrict__ lr,
+                                               uint32_t chunk, int lo_ext, int hi_ext, double scale) {
+    constexpr int TQ = tris::TQ, NS = tris::NSMAX;
+    double sigma = a.sigma;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+    }
+    __shared__ double t_id[SMAX][TQ], t_e[SMAX][TQ], t_h[SMAX][TQ], t_k[SMAX][TQ];
+    __shared__ double s_a[TQ];
+    __shared__ double s_u[NS][TQ], s_v[NS][TQ], s_bu[NS][TQ];
+    // phase 1: the forward-eliminated u of the L- and R-response tracks; phase 3: the slopes of v_j on u_{j+1}
+    __shared__ double s_u1[PHASE == 1 ? NS : 1][TQ], s_u2[PHASE == 1 ? NS : 1][TQ], s_bv[PHASE == 3 ? NS : 1][TQ];
+    const int t = threadIdx.x, c = t % TQ, sj = t / TQ;
+    const uint32_t q0 = blockIdx.x * uint32_t(TQ);
+    const uint32_t q = q0 + uint32_t(c);
+    const bool valid = q < a.nlines;
+    const uint32_t qq = valid ? q : q0;
+    const size_t base = size_t(qq) + size_t(sj * sl) * a.stride;   // lines are contiguous: stride = plane
+
+    double g[SMAX];
+#pragma unroll
+    for (int i = 0; i < SMAX; ++i)
+        g[i] = (valid && i < sl) ? __builtin_nontemporal_load(x + base + size_t(i) * a.stride) : 0.0;
+    double lx = 0.0, rx = 0.0;   // phase 3: the neighbours' values (the interface solve's result)
+    if (PHASE == 3 && t < TQ) {
+        const uint32_t s = qq / chunk, l = qq - s * chunk;
+        if (lo_ext) lx = lr[(size_t(s) * 2) * chunk + l];
+        if (hi_ext) rx = lr[(size_t(s) * 2 + 1) * chunk + l];
+    }
+
+    if (t < TQ) {   // c0 + c1 T along the last dim for line qq (dims 0..p-2 column-major)
+        double lamv[kMaxDims] = {0, 0, 0, 0};
+        uint32_t rest = qq;
+        for (int jj = 0; jj < a.p - 1; ++jj) {
+            const uint32_t qd = (jj < a.p - 2) ? a.fd[jj].div(rest) : 0u;
+            lamv[jj] = a.lam[a.lam_off[jj] + (rest - qd * a.m[jj])];
+            rest = qd;
+        }
+        double c0 = a.w0, c1 = 0.0;
+        for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
+            if (a.cS[Sm] == 0.0) continue;
+            double prod = sigma * a.cS[Sm];
+            for (int jj = 0; jj < a.p - 1; ++jj)
+                if ((Sm >> jj) & 1) prod *= lamv[jj];
+            if ((Sm >> (a.p - 1)) & 1) c1 += prod;
+            else c0 += prod;
+        }
+        const double A = -c1, B = c0 + 2.0 * c1;
+        double e = 0.0, h = 1.0;
+#pragma unroll 1
+        for (int i = 0; i < sl; ++i) {
+            const double id = 1.0 / (B - A * e);
+            e = A * id;
+            h = -A * h * id;
+            t_id[i][c] = id;
+            t_e[i][c] = e;
+            t_h[i][c] = h;
+        }
+        double H = t_h[sl - 1][c], K = -t_e[sl - 1][c];
+        t_k[sl - 1][c] = K;
+#pragma unroll 1
+        for (int i = sl - 2; i >= 0; --i) {
+            const double ei = t_e[i][c];
+            H = t_h[i][c] - ei * H;
+            K = -ei * K;
+            t_h[i][c] = H;
+            t_k[i][c] = K;
+        }
+        s_a[c] = A;
+    }
+    __syncthreads();
+
+    {   // this segment with zero neighbours
+        const double A = s_a[c];
+        g[0] *= t_id[0][c];
+#pragma unroll
+        for (int i = 1; i < SMAX; ++i)
+            if (i < sl) g[i] = (g[i] - A * g[i - 1]) * t_id[i][c];
+        double last = 0.0;
+#pragma unroll
+        for (int i = SMAX - 1; i >= 0; --i) {
+            if (i == sl - 1) last = g[i];
+            if (i < sl - 1) g[i] -= t_e[i][c] * g[i + 1];
+        }
+        s_u[sj][c] = g[0];
+        s_v[sj][c] = last;
+    }
+    __syncthreads();
+
+    if (t < TQ) {
+        // segments' interface system as k_trig, with the block's ends either the mesh's mirror (v_{-1} = u_0,
+        // R_last = v_last) or a neighbour rank's value. Eliminated forward to v_{j-1} = av + bv u_j (bv is the
+        // same for every right-hand side: phase 1 carries three, the data and the responses to L = 1, R = 1).
+        const double H0 = t_h[0][c], K0 = t_k[0][c], H1 = t_h[sl - 1][c], K1 = t_k[sl - 1][c];
+        constexpr int NR = PHASE == 1 ? 3 : 1;
+        double av[NR], bv = lo_ext ? 0.0 : 1.0;
+        av[0] = lo_ext ? lx : 0.0;
+        if constexpr (NR == 3) {
+            av[1] = lo_ext ? 1.0 : 0.0;
+            av[2] = 0.0;
+        }
+#pragma unroll 1
+        for (int j = 0; j < nseg - 1; ++j) {
+            const double id = 1.0 / (1.0 - H0 * bv);
+            const double bu = K0 * id;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const double g0 = r == 0 ? s_u[j][c] : 0.0, g1 = r == 0 ? s_v[j][c] : 0.0;
+                const double au = (g0 + H0 * av[r]) * id;
+                av[r] = g1 + H1 * av[r] + H1 * bv * au;
+                if (r == 0) s_u[j][c] = au;
+                if constexpr (NR == 3) {
+                    if (r == 1) s_u1[j][c] = au;
+                    if (r == 2) s_u2[j][c] = au;
+                }
+                if (r == 0) s_v[j][c] = av[0];
+            }
+            bv = K1 + H1 * bv * bu;
+            s_bu[j][c] = bu;
+            if constexpr (PHASE == 3) s_bv[j][c] = bv;
+        }
+        // last segment: R_J = cr v_J + Rx (mirror: cr = 1, Rx = 0; neighbour: cr = 0, Rx = its value)
+        const int J = nseg - 1;
+        const double cr = hi_ext ? 0.0 : 1.0;
+        const double a11 = 1.0 - H0 * bv, a12 = -K0 * cr, a21 = -H1 * bv, a22 = 1.0 - K1 * cr;
+        const double idet = 1.0 / (a11 * a22 - a12 * a21);
+        double uJ[NR], vJ[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const double gJ0 = r == 0 ? s_u[J][c] : 0.0, gJ1 = r == 0 ? s_v[J][c] : 0.0;
+            const double rxr = r == 0 ? (hi_ext ? rx : 0.0) : (r == 2 && hi_ext ? 1.0 : 0.0);
+            const double b1 = gJ0 + H0 * av[r] + K0 * rxr, b2 = gJ1 + H1 * av[r] + K1 * rxr;
+            uJ[r] = (b1 * a22 - a12 * b2) * idet;
+            vJ[r] = (a11 * b2 - a21 * b1) * idet;
+        }
+        if constexpr (PHASE == 1) {
+            // first row of the block: back-substitute u_j = au_j + bu_j u_{j+1} down to u_0 for each track
+            double u[3] = {uJ[0], uJ[1], uJ[2]};
+#pragma unroll 1
+            for (int j = J - 1; j >= 0; --j) {
+                const double bu = s_bu[j][c];
+                u[0] = s_u[j][c] + bu * u[0];
+                u[1] = s_u1[j][c] + bu * u[1];
+                u[2] = s_u2[j][c] + bu * u[2];
+            }
+            if (valid) {   // [chunk s][6][line in chunk]: Gf Gl Hf Hl Kf Kl
+                const uint32_t s = q / chunk, l = q - s * chunk;
+                double* o = coef + size_t(s) * 6 * chunk + l;
+                o[0] = u[0];
+                o[size_t(chunk)] = vJ[0];
+                o[2 * size_t(chunk)] = u[1];
+                o[3 * size_t(chunk)] = vJ[1];
+                o[4 * size_t(chunk)] = u[2];
+                o[5 * size_t(chunk)] = vJ[2];
+            }
+        } else {
+            // every segment's (u_j, v_j) by back substitution
+            s_u[J][c] = uJ[0];
+            s_v[J][c] = vJ[0];
+            double un = uJ[0];
+#pragma unroll 1
+            for (int j = J - 1; j >= 0; --j) {
+                const double u = s_u[j][c] + s_bu[j][c] * un;
+                s_v[j][c] = s_v[j][c] + s_bv[j][c] * un;
+                s_u[j][c] = u;
+                un = u;
+            }
+        }
+    }
+    if constexpr (PHASE == 3) {
+        __shared__ double s_lx[TQ], s_rx[TQ];
+        if (t < TQ) {
+            s_lx[c] = lx;
+            s_rx[c] = rx;
+        }
+        __syncthreads();
+        const double Lj = sj == 0 ? (lo_ext ? s_lx[c] : s_u[0][c]) : s_v[sj - 1][c];
+        const double Rj = sj == nseg - 1 ? (hi_ext ? s_rx[c] : s_v[nseg - 1][c]) : s_u[sj + 1][c];
+        if (!valid) return;
+#pragma unroll
+        for (int i = 0; i < SMAX; ++i)
+            if (i < sl)
+                __builtin_nontemporal_store(scale * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), x + base + size_t(i) * a.stride);
+    }
+}
+
+// the interface systems of the lines of one chunk (on the rank that owns the chunk): from every rank r's
+// (Gf, Gl, Hf, Hl, Kf, Kl) [r][6][chunk] the first row u_r and last row v_r of each rank's block,
+//   u_r = Gf_r + Hf_r v_{r-1} + Kf_r u_{r+1},  v_r = Gl_r + Hl_r v_{r-1} + Kl_r u_{r+1}
+// (Hf_0 = Hl_0 = 0, Kf_{G-1} = Kl_{G-1} = 0: the mesh's ends), eliminated forward to
+// u_r = ga_r + de_r u_{r+1}, v_r = al_r + be_r u_{r+1} (kept in the input's first four rows), then
+// substituted back. Out [r][2][chunk]: (L, R) of rank r = (v_{r-1}, u_{r+1}).
+__global__ __launch_bounds__(256) void k_tris_iface(double* __restrict__ co, double* __restrict__ lr, uint32_t chunk,
+                                                    int G, const AdmmCtl* ctl) {
+    if (ctl && ctl->done) return;
+    const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= chunk) return;
+    const size_t C = chunk;
+    double al = 0.0, be = 0.0;
+    for (int r = 0; r < G; ++r) {
+        double* c = co + size_t(r) * 6 * C + l;
+        const double Gf = c[0], Gl = c[C], Hf = c[2 * C], Hl = c[3 * C], Kf = c[4 * C], Kl = c[5 * C];
+        const double id = 1.0 / (1.0 - Hf * be);
+        const double ga = (Gf + Hf * al) * id, de = Kf * id;
+        const double nal = Gl + Hl * al + Hl * be * ga, nbe = Kl + Hl * be * de;
+        c[0] = ga;
+        c[C] = de;
+        c[2 * C] = nal;
+        c[3 * C] = nbe;
+        al = nal;
+        be = nbe;
+    }
+    double un = 0.0;   // u_{r+1}
+    for (int r = G - 1; r >= 0; --r) {
+        const double* c = co + size_t(r) * 6 * C + l;
+        const double u = c[0] + c[C] * un, v = c[2 * C] + c[3 * C] * un;
+        lr[(size_t(r) * 2 + 1) * C + l] = r < G - 1 ? un : 0.0;          // R of rank r
+        if (r + 1 < G) lr[(size_t(r + 1) * 2) * C + l] = v;               // L of rank r + 1
+        un = u;
+    }
+    lr[l] = 0.0;   // L of rank 0 (the mesh's end)
+}
+
+static void tris_seg(uint32_t n, int* sl, int* nseg) {
+    // >= 4 segments when the block allows it, segments of <= 16 rows (32 past 1024 rows), <= 64 segments
+    uint32_t s = std::max<uint32_t>(1u, std::min<uint32_t>(n > 1024u ? 32u : 16u, n / 4u));
+    while (s > 1 && n % s) --s;
+    *sl = int(s);
+    *nseg = int(n / s);
+}
+
+hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, int phase, double* x, double* coef,
+                           const double* lr, uint32_t chunk, int lo_ext, int hi_ext, double scale,
+                           const AdmmCtl* ctl) {
+    const int p = og.p, d = p - 1;
+    SpecArgs a{};
+    a.ctl = ctl;
+    a.sigma = 1.0;
+    a.w0 = 1.0;
+    a.lam = sp.lam;
+    for (int j = 0; j < kMaxDims; ++j) {
+        a.lam_off[j] = sp.lam_off[j];
+        a.m[j] = og.m[j];
+    }
+    for (int j = 0; j < kMaxDims - 1; ++j) a.fd[j] = og.fd[j];
+    for (int S = 0; S < 16; ++S) a.cS[S] = og.cS[S];
+    a.d = d;
+    a.p = p;
+    a.stride = og.stride[d];
+    a.nlines = og.stride[d];
+    const uint32_t n = og.m[d];
+    int sl = 0, nseg = 0;
+    tris_seg(n, &sl, &nseg);
+    if (n < 1 || sl > 32 || nseg > tris::NSMAX || chunk == 0 || a.nlines % chunk != 0)
+        return hipErrorInvalidValue;
+    const dim3 grid((a.nlines + uint32_t(tris::TQ) - 1) / uint32_t(tris::TQ)), block(uint32_t(tris::TQ * nseg));
+    // segments of <= 16 rows (blocks up to 1024 planes) keep the row registers at 16
+    if (phase == 1 && sl <= 16)
+        klaunch((k_tris<1, 16>), grid, block, 0, s, a, sl, nseg, x, coef, lr, chunk, lo_ext, hi_ext, scale);
+    else if (phase == 1)
+        klaunch((k_tris<1, 32>), grid, block, 0, s, a, sl, nseg, x, coef, lr, chunk, lo_ext, hi_ext, scale);
+    else if (phase == 3 && sl <= 16)
+        klaunch((k_tris<3, 16>), grid, block, 0, s, a, sl, nseg, x, coef, lr, chunk, lo_ext, hi_ext, scale);
+    else if (phase == 3)
+        klaunch((k_tris<3, 32>), grid, block, 0, s, a, sl, nseg, x, coef, lr, chunk, lo_ext, hi_ext, scale);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint32_t chunk, int G, const AdmmCtl* ctl) {
+    if (G < 1 || chunk == 0) return hipErrorInvalidValue;
+    klaunch(k_tris_iface, dim3((chunk + 255) / 256), dim3(256), 0, s, coef_in, lr_out, chunk, G, ctl);
+    return hipGetLastError();
+}
+
 // segment length for k_trig: the smallest divisor of m in [16, 32], else the largest in [4, 16),
 // with at most 64 segments; 0 when there is none
 static int trig_seg(uint32_t m) {
@@ -1428,7 +1701,7 @@ static int trig_seg(uint32_t m) {
 // FFT pass stays faster: 9866 against 9381 with 8-line and 9050 with 4-line tiles, profiles/r02/v19_tri2d).
 // Probe builds: MVTV_DCT_TRI2D=0 / 4 / 8 forces the 2-D choice.
 static int tri_tiles(const SpecArgs& a, int mode, bool formb) {
-    if (mode != SPEC_MID || a.d == 0 || formb || a.pk) return 0;
+    if (mode != SPEC_MID || a.d == 0 || formb) return 0;
     const char* e = probe_env("MVTV_DCT_TRI");
     if (e && std::atoi(e) == 0) return 0;
     if (a.L < 6 || a.L > 11 || a.stride < 4u) return 0;
@@ -1579,7 +1852,6 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
     if (d0 && t0 > 0) want = t0;
     if (!d0 && t1 > 0) want = t1;
     if (!d0) want = std::min<int>(want, int(a.stride));
-    if (!d0 && a.rm_lw && mode != SPEC_MID) want = std::min<int>(want, 1 << a.rm_lw);   // tiles inside a piece row
     a.xcd = xcd_env >= 0 ? xcd_env : (xcd_def ? 1 : 0);
     if (try_tile<L, 2>(a, s, mode, d0, formb, want) || try_tile<L, 4>(a, s, mode, d0, formb, want) ||
         try_tile<L, 8>(a, s, mode, d0, formb, want) || try_tile<L, 16>(a, s, mode, d0, formb, want) ||
@@ -1604,22 +1876,8 @@ bool dct_pcg_fusable(const Geom& g, size_t partial_words) {
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
                            double w0, const AdmmCtl* ctl, uint32_t q_off, double inv_n, const int32_t* skip,
-                           const DctPack* pack, const PcgFuse* pf, const LinePiece* piece) {
+                           const PcgFuse* pf) {
     SpecArgs a{};
-    if (pack && pack->mode) {
-        a.pk = pack->mode;
-        a.pk_lpl = pack->lpl;
-        a.pk_lch = pack->lch;
-        a.pk_nz = pack->nz;
-        a.pk_lk = pack->lk;
-        a.pk_lm0 = pack->lm0;
-        if (a.pk_lk && (a.pk_lch < a.pk_lm0 || a.pk_lk > a.pk_lm0)) return hipErrorInvalidValue;
-    }
-    if (piece && piece->lw) {
-        a.rm_lw = piece->lw;
-        a.rm_ls = piece->ls;
-        a.rm_xoff = piece->xoff;
-    }
     a.ctl = ctl;
     a.skip = skip;
     a.q_off = q_off;
@@ -1646,10 +1904,6 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     while ((1u << a.ls) < a.stride) ++a.ls;
     const uint32_t m = g.m[d];
     a.nlines = g.N / m;
-    if (a.rm_lw) {   // FWD / INV: a piece of the mesh's lines along d > 0; MID: the piece buffer's own lines
-        if (piece->nlines == 0 || (mode != SPEC_MID && d == 0)) return hipErrorInvalidValue;
-        a.nlines = piece->nlines;
-    }
     a.d = d;
     a.p = g.p;
     a.L = 0;
@@ -1657,13 +1911,13 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     const bool formb = ga != nullptr;
     if (m > 4096) return hipErrorInvalidValue;
     if (pf && pf->mode) {   // PCG-fused d = 0 pass (dct_pcg_fusable meshes): k_dct8 only
-        if (d != 0 || formb || pack || (1u << a.L) != m || a.L < 6 || mode != (pf->mode == 1 ? SPEC_FWD : SPEC_INV) ||
+        if (d != 0 || formb || (1u << a.L) != m || a.L < 6 || mode != (pf->mode == 1 ? SPEC_FWD : SPEC_INV) ||
             (pf->mode == 2 && !pf->nparts))
             return hipErrorInvalidValue;
         a.pf = *pf;
     }
     if ((1u << a.L) != m || (1u << a.ls) != a.stride) {   // mixed radix, or a power of two over a general stride
-        if (a.pk || (a.rm_lw && mode != SPEC_MID) || !dct_radix_plan(m, a.rad, &a.nrad)) return hipErrorInvalidValue;
+        if (!dct_radix_plan(m, a.rad, &a.nrad)) return hipErrorInvalidValue;
         a.fds = FastDiv(a.stride);
         a.fm = FastDiv(m);
         for (int st = 0, L = 1; st < a.nrad; ++st) {
@@ -1688,9 +1942,6 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
         launch_dctg(a, s, mode, d == 0, formb);
         return hipGetLastError();
     }
-    if ((a.pk || (a.rm_lw && mode != SPEC_MID)) && a.L < 3)
-        return hipErrorInvalidValue;   // packed layouts and piece addressing are served by k_dct8 only
-    if (a.rm_lw && mode != SPEC_MID && probe_env("MVTV_DCT_LDS")) return hipErrorInvalidValue;
     if (const int tq = tri_tiles(a, mode, formb)) {
         launch_tri(a, s, tq);
         return hipGetLastError();

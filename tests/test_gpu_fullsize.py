@@ -125,6 +125,23 @@ def test_config4_fold_path_2048_vs_c_oracle(solver):
         assert stats[k]["s_norm"] == pytest.approx(st["s_norm"], rel=1e-8)
 
 
+def test_metric_512_cubed_eight_rank_decomposition():
+    """The metric at 8 GPUs as bench.py runs it (one 512^3 mesh, 64 planes per rank), rehearsed with the
+    loopback transport on one GPU: 2 fixed iterations against the one-GPU run, rho exact, theta 1e-11."""
+    from multivartv_amd import slab
+    m, lam, iters = [512, 512, 512], 1.0, 2
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        P.state_set(np.full(y.size, y.mean()), None, lam / 5.0)
+        st = P.run(lam, fixed_iters=iters)
+        th, _, rho = P.state_get(want_u=False)
+    out, theta = slab.run_local_group(m, y, deltas, lam, 8, fixed_iters=iters)
+    assert all(o["iters"] == iters and o["rho"] == rho for o in out)
+    assert out[0]["r_norm"] == pytest.approx(st["r_norm"], rel=1e-9)
+    assert np.max(np.abs(theta - th)) <= 1e-11 * np.max(np.abs(th))
+
+
 def test_config5_128_4d_eight_rank_decomposition():
     """Config 5 at its shape: 128^4 slab-decomposed over 8 ranks (16 planes of dim 3 each), the ranks'
     mvtv_slab_run loops on one GPU over the in-process loopback transport, against the one-GPU run:

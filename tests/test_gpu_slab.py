@@ -1,8 +1,8 @@
 """Slab-decomposed single mesh (csrc/mvtv_slab.cpp, multivartv_amd/slab.py).
 
-The transposes are pipelined in pieces of the dim-0 index (2 pieces at 32^3 over 4 ranks and 32^3 x 8 over
-2, 4 at 64^3 over 4; one below m_0 = 32) with the collectives on their own stream, so these cases cover
-the piece-packed layout, the per-piece last-dimension pass and the event hand-offs between the streams.
+The last dimension's line solves are substructured over the ranks (k_tris phase 1, the interface systems
+k_tris_iface, phase 3) with the collectives on their own stream: these cases cover blocks of 1 (4 x 4 x 8
+over 4 ranks: 2 planes each) to 32 planes per rank, 2-D to 4-D, and the event hand-offs between the streams.
 
 The decomposition changes where planes live and the summation order of the 7 global sums, so the
 iteration count and rho must match the one-GPU run exactly and theta to 1e-11 relative. Several ranks
@@ -38,8 +38,8 @@ def _rel(a, b):
 @pytest.mark.parametrize("m,lam,world", [([16, 16, 16], 1.0, 1), ([16, 16, 16], 1.0, 2), ([32, 32, 32], 0.5, 4),
                                          ([64, 32], 0.5, 2), ([8, 8, 8, 8], 1.0, 4), ([16, 16, 16, 16], 1.0, 2),
                                          ([4, 4, 8], 1.0, 4), ([64, 64, 64], 1.0, 4), ([32, 32, 32, 8], 1.0, 2)],
-                         ids=["3d_16_w1", "3d_16_w2", "3d_32_w4_2pieces", "2d_64x32_w2", "4d_8_w4", "4d_16_w2",
-                              "3d_4x4x8_w4_small_planes", "3d_64_w4_4pieces", "4d_32x32x32x8_w2_2pieces"])
+                         ids=["3d_16_w1", "3d_16_w2", "3d_32_w4", "2d_64x32_w2", "4d_8_w4", "4d_16_w2",
+                              "3d_4x4x8_w4_small_planes", "3d_64_w4", "4d_32x32x32x8_w2"])
 @pytest.mark.parametrize("fixed", [7, 0])
 def test_local_group_matches_one_gpu(m, lam, world, fixed):
     y, deltas, th, rho, st = _reference(m, lam, fixed)
