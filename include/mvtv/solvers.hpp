@@ -157,7 +157,7 @@ void mbs_one(const mat& data, const vec& y, const vec& m, mbs_one_object& output
 
 // mbs (cpp-code/solvers.hpp:129, solvers.cpp:277-310): k-fold CV over a lambda path, refit at the best lambda.
 // The reference's CV differs from a textbook CV in three ways, all reproduced when reference_cv is set
-// (the default, so results match the reference's code):
+// (the default):
 //   1. the cache (O, O^T y, O^T O) is built once on the FULL data and never rebuilt per fold (:288-301): each
 //      fold's path fits all n points and differs from the others only through mean(y_train) (theta_0 and
 //      theta_old, :199, :103);
@@ -167,9 +167,12 @@ void mbs_one(const mat& data, const vec& y, const vec& m, mbs_one_object& output
 //      last path left in the cache, crossO + lambdas[n_lambda-1] crossD (:209).
 // reference_cv = false: each fold's path runs on its own training cache, test MSEs use that fold's models,
 // and the refit solves with crossO + best_lambda crossD from mean(y).
-// kfold (cpp-code/utils.cpp:417-436) shuffles rows with Armadillo's RNG, which cannot be reproduced outside
-// that build; here the row order is the seeded permutation kfold_perm(n, seed), then fold i tests rows
-// [i n/k, (i+1) n/k) of it and trains on the others in permuted order, as the reference.
+// Fold assignment is NOT the reference's (parity unpinned): kfold (cpp-code/utils.cpp:417-436) calls
+// shuffle(join_horiz(data, y), 1), and Armadillo's shuffle(X, dim = 1) permutes the COLUMNS of X (per its
+// documentation; no Armadillo source is in this image), so the reference's folds are unshuffled contiguous
+// row blocks of a matrix whose p + 1 predictor / response columns were randomly reordered by Armadillo's RNG.
+// Neither that RNG nor the column scramble is reproduced: here rows are permuted by the seeded
+// kfold_perm(n, seed), fold i tests rows [i n/k, (i+1) n/k) of that order and trains on the rest.
 struct mbs_cpp_options {
     uint64_t seed = 0;
     bool reference_cv = true;
