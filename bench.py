@@ -17,8 +17,9 @@ slab-decomposed over the N GPUs (``scaling: strong``; the whole loop inside libm
 solver stream). Before it every rank also fits its own independent 512^3 mesh (noise seed + rank, the
 embarrassingly parallel sharding of the north star); that aggregate is reported beside the headline as
 ``independent_fits`` (``scaling: weak``). One RCCL per process: torch.distributed runs on gloo (host
-barriers, max-over-ranks time, the 128-byte RCCL id) and every device collective goes through libmvtv's
-communicator (``rccl_ranks`` = its size), whose RCCL is the copy torch already mapped.
+barriers, max-over-ranks time, the 128-byte RCCL id; torch's own RCCL is never initialised) and every
+device collective goes through libmvtv's communicator (``rccl_ranks`` = its size; ROCm's librccl on
+libmvtv's HIP runtime).
 """
 from __future__ import annotations
 

@@ -222,8 +222,8 @@ int32_t mvtv_comm_size(const mvtv_comm* comm);
 /* sum of n <= 64 host doubles over an RCCL communicator, in place (the global residual all-reduce of
  * independent fits); blocking */
 mvtv_status mvtv_comm_allreduce_host(mvtv_comm* comm, double* vals, int32_t n);
-/* the file RCCL was resolved from: an already-mapped librccl.so.1 (torch's) is reused, so a process holds
- * one RCCL; otherwise ROCm's. "" when RCCL is unavailable */
+/* the file RCCL was resolved from (ROCm's librccl, which shares libmvtv's HIP runtime); "" when RCCL is
+ * unavailable */
 const char* mvtv_comm_library(void);
 /* admm_update B from theta = theta0 on every node, u = 0, rho = rho0 (rcpp…/solvers.cpp:207-209); collective
  * over the communicator. stats hold the global norms; theta of the owned planes: mvtv_state_get (ghosts

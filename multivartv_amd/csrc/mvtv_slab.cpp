@@ -79,15 +79,13 @@ mvtv_status rccl_api(RcclApi** out) {
     std::lock_guard<std::mutex> lk(mu);
     if (!tried) {
         tried = true;
-        // One RCCL per process: a copy already mapped (torch's librccl, soname librccl.so.1, is loaded by
-        // `import torch`) is reused; only a process without one loads ROCm's
-        for (const char* name : {"librccl.so.1", "librccl.so"}) {
-            api.h = dlopen(name, RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);
-            if (api.h) break;
-        }
+        // ROCm's librccl, which shares libmvtv's HIP runtime (/opt/rocm). A librccl that `import torch` maps
+        // is NOT reused: torch's links torch's own copy of the HIP runtime, on which libmvtv's streams are
+        // invalid ("unhandled cuda error" at ncclCommInitRank). Callers keep one RCCL *running* per process
+        // by giving torch.distributed the gloo backend (bench.py), so torch's copy is never initialised.
         for (const char* name : {"/opt/rocm/lib/librccl.so.1", "librccl.so.1", "librccl.so"}) {
-            if (api.h) break;
             api.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (api.h) break;
         }
         if (api.h) {
             auto sym = [&](auto& fp, const char* n) { fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(api.h, n)); };

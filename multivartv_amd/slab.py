@@ -113,7 +113,7 @@ class Comm:
 
     @staticmethod
     def library():
-        """The file RCCL was resolved from (an already-mapped librccl.so.1 is reused: one RCCL per process)."""
+        """The file RCCL was resolved from (ROCm's librccl, on libmvtv's HIP runtime)."""
         return (_L().mvtv_comm_library() or b"").decode()
 
     def close(self):

@@ -77,10 +77,11 @@ def test_no_device_fails_loudly():
         mv.Problem([4, 4], np.zeros(16))
 
 
-def test_one_rccl_per_process():
-    """After `import torch` (whose libtorch_hip maps its own librccl.so, soname librccl.so.1) the library's
-    RCCL transport resolves to that copy instead of loading ROCm's: one RCCL runtime per process. Runs in a
-    child process, since the resolution is made once per process."""
+def test_rccl_resolves_to_rocm_not_torch():
+    """libmvtv's RCCL is ROCm's librccl (on libmvtv's HIP runtime) even after `import torch` has mapped
+    torch's librccl: torch's links torch's own HIP runtime copy, on which libmvtv's streams are invalid (a
+    GPU run of the NOLOAD reuse failed at ncclCommInitRank with "unhandled cuda error"). One RCCL *runs* per
+    bench rank because torch.distributed is given gloo there. Child process: the resolution is per process."""
     code = ("import torch, multivartv_amd\n"
             "from multivartv_amd import slab\n"
             "print(slab.Comm.library())\n")
@@ -88,4 +89,6 @@ def test_one_rccl_per_process():
     assert out.returncode == 0, out.stderr
     import torch
     torch_lib = os.path.realpath(os.path.join(os.path.dirname(torch.__file__), "lib"))
-    assert os.path.realpath(out.stdout.strip().splitlines()[-1]).startswith(torch_lib)
+    path = os.path.realpath(out.stdout.strip().splitlines()[-1])
+    assert path and not path.startswith(torch_lib)
+    assert "rccl" in os.path.basename(path)
