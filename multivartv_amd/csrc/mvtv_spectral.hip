@@ -1736,8 +1736,18 @@ static void launch_tri(SpecArgs& a, hipStream_t s, int tq) {
             const char* e = probe_env("MVTV_TRI_SEG");
             return e && std::atoi(e) == 32 ? 32 : 16;
         }();
-        if (seg == 32) launch_tri_seg<32, tri::TQ>(a, s);
-        else launch_tri_seg<16, tri::TQ>(a, s);
+        static const int tq32 = [] {   // probe: 32-line tiles (256-B rows)
+            const char* e = probe_env("MVTV_TRI_TQ");
+            return e && std::atoi(e) == 32 ? 1 : 0;
+        }();
+        if (tq32 && seg == 16 && a.stride >= 32u) {
+            a.tq = 32;
+            launch_tri_seg<16, 32>(a, s);
+        } else if (seg == 32) {
+            launch_tri_seg<32, tri::TQ>(a, s);
+        } else {
+            launch_tri_seg<16, tri::TQ>(a, s);
+        }
         return;
     }
     a.xcd = 1;   // 2-D: narrow tiles in XCD runs (grid a multiple of 8, tri_tiles)

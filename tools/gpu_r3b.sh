@@ -7,4 +7,8 @@ mkdir -p $O
 export MVTV_LIB_PATH=$GRAFT_REPO_ROOT/multivartv_amd/lib_p/libmvtv.so
 timeout -k 10 200 python tools/zchunk_probe.py 256 3952 1976 1520 1216 988 760 608 > $O/z256.txt 2>&1 && \
 timeout -k 10 300 python tools/zchunk_probe.py 512 4736 2368 3848 7696 9472 1184 > $O/z512.txt 2>&1 && \
-timeout -k 10 200 python tools/zchunk_probe.py 512x512x64 3848 2368 1184 592 > $O/z512x64.txt 2>&1
+timeout -k 10 200 python tools/zchunk_probe.py 512x512x64 3848 2368 1184 592 > $O/z512x64.txt 2>&1 && \
+for v in 16 32 16 32; do
+  MVTV_TRI_TQ=$v timeout -k 10 200 python bench.py --no-cpu --pcg-steps 0 --steps 30 --warmup 3 > $O/tri_tq$v.json 2> $O/tri_tq$v.err || exit 1
+  python -c "import json;d=json.load(open('$O/tri_tq$v.json'));print('tq $v', d['ms_per_step'], d['kernels']['dct'], d['kernels']['dct_first'])" >> $O/tri.txt
+done
