@@ -340,7 +340,9 @@ def slab_main(a, D, comm=None):
 
 def cv_main(a, D):
     """Config 4's work items (BASELINE.json: 2D 2048^2, 32-lambda CV path batched over 8 GPUs): CV fold paths
-    over lambda chunks (rcpp…/solvers.cpp:340-353 -> mbs_path :204-222). Work item (fold f, chunk c): the
+    over lambda chunks (rcpp…/solvers.cpp:340-353 -> mbs_path :204-222). Rank r's items are folds
+    (r B + i) % 5 over the rank's lambda chunk c = r % 8 (so --cv-batch changes the work per GPU, not its
+    mix: the same chunk, the same PCG counts). Work item (fold f, chunk c): the
     lattice minus fold f of kfoldinds (W = O^T O a 0/1 mask, so the theta-solve is the spectrally
     preconditioned PCG, rtol 1e-10, warm-started), lambdas [4c, 4c+4) of create_lambdas' 32-lambda grid
     (lam_max_pinv on the GPU, 1e-4 lambda_max .. lambda_max), steps/4 fixed ADMM iterations at each, theta /
@@ -355,7 +357,7 @@ def cv_main(a, D):
     fold = mcv.kfoldinds(y.size, 5, seed=0)
     deltas = [(1.0 + 2e-4) / v for v in m]
     B = max(1, a.cv_batch)
-    items = [D.rank * B + i for i in range(B)]
+    items = [D.rank * B + i for i in range(B)]   # item: fold (item % 5); lambda chunk: the rank's (rank % 8)
     dev = D.local % max(1, mv.device_count())
     probs, ymeans = [], []
     for it in items:
@@ -365,7 +367,7 @@ def cv_main(a, D):
     del y, fold
     lmax, _ = probs[0].lambda_max()
     grid = np.exp(np.linspace(np.log(lmax * 1e-4), np.log(lmax), 32))[::-1]
-    chunks = [grid[(4 * (it % 8) + np.arange(4)) % 32] for it in items]
+    chunks = [grid[(4 * (D.rank % 8) + np.arange(4)) % 32] for _ in items]
     per = max(1, a.steps // 4)
     steps = 4 * per
     solver = {"auto": mv.SOLVER_AUTO, "pcg": mv.SOLVER_PCG, "spectral": mv.SOLVER_PCG_SPECTRAL}[a.solver]

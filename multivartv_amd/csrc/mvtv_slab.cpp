@@ -627,14 +627,8 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
                                     P->ctl));
             P->tstop(h);
         }
-        // -- inverse passes along dims p-2..0, in place
-        for (int d = p - 2; d >= 0; --d) {
-            const int h = P->tstart(MVTV_K_DCT);
-            HIP_TRY(launch_dct_pass(P->spec, og, s, 1, d, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl));
-            P->tstop(h);
-        }
-        // -- theta halo: both ghost planes
-        if (!solo) {
+        // -- theta halo (both ghost planes) on sc, started as soon as the planes it sends are final
+        auto theta_halo = [&]() -> mvtv_status {
             MVTV_TRY(handoff(ev[EV_TH], s, sc));
             MVTV_TRY(C->begin());
             if (rk > 0) MVTV_TRY(C->send(P->theta + first_owned, pl, rk - 1, sc));
@@ -642,8 +636,39 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
             if (rk > 0) MVTV_TRY(C->recv(P->theta, pl, rk - 1, sc));
             if (rk < G - 1) MVTV_TRY(C->recv(P->theta + last_owned + pl, pl, rk + 1, sc));
             MVTV_TRY(C->end(sc));
-            MVTV_TRY(handoff(ev[EV_THD], sc, s));
+            HIP_TRY(hipEventRecord(ev[EV_THD], sc));
+            return MVTV_OK;
+        };
+        // -- inverse passes along dims p-2..0, in place. The last one (dim 0) works plane by plane, so it
+        //    transforms the first and last owned planes first and the halo carrying them overlaps the interior
+        for (int d = p - 2; d >= 0; --d) {
+            if (d == 0 && !solo && sg.nz >= 3) {
+                Geom one = og, mid = og;
+                one.m[p - 1] = 1;
+                one.N = sg.plane;
+                one.iend = one.N;
+                mid.m[p - 1] = sg.nz - 2;
+                mid.N = sg.plane * (sg.nz - 2);
+                mid.iend = mid.N;
+                double* edge_planes[2] = {th, th + size_t(sg.nz - 1) * pl};
+                for (double* ep : edge_planes) {
+                    const int h = P->tstart(MVTV_K_DCT);
+                    HIP_TRY(launch_dct_pass(P->spec, one, s, 1, 0, ep, nullptr, 0.0, nullptr, 0.0, ep, 0.0, 1.0, P->ctl));
+                    P->tstop(h);
+                }
+                MVTV_TRY(theta_halo());
+                const int h = P->tstart(MVTV_K_DCT);
+                HIP_TRY(launch_dct_pass(P->spec, mid, s, 1, 0, th + pl, nullptr, 0.0, nullptr, 0.0, th + pl, 0.0, 1.0,
+                                        P->ctl));
+                P->tstop(h);
+            } else {
+                const int h = P->tstart(MVTV_K_DCT);
+                HIP_TRY(launch_dct_pass(P->spec, og, s, 1, d, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl));
+                P->tstop(h);
+                if (d == 0 && !solo) MVTV_TRY(theta_halo());
+            }
         }
+        if (!solo) HIP_TRY(hipStreamWaitEvent(s, ev[EV_THD], 0));
         // -- edge update + gather on the owned planes, partial sums into P->red
         if (fused) {
             if (zh_pending) HIP_TRY(hipStreamWaitEvent(s, ev[EV_ZH], 0));   // z_old's ghost plane is in place
