@@ -393,18 +393,26 @@ def cv_main(a, D):
     if a.warmup > 0:
         run_items(lambda i: probs[i].path(chunks[i][:1], np.full(probs[i].N, ymeans[i]), chunks[i][0] / 5.0,
                                           want_thetas=False, fixed_iters=a.warmup, **opts))
-    D.barrier()
-    for P in probs:
-        P.timing(True)
-    t0 = time.perf_counter()
-    run_items(lambda i: probs[i].path(chunks[i], np.full(probs[i].N, ymeans[i]), chunks[i][0] / 5.0,
-                                      want_thetas=False, fixed_iters=per, **opts))
-    t1 = time.perf_counter()
-    D.barrier()
-    tims = [P.timings() for P in probs]
-    for P in probs:
-        P.timing(False)
-    g_elapsed, = D.allreduce([t1 - t0], "max")
+    # the value: the timed region without per-launch events (this work item's launches are 20-50 us, the
+    # event pairs around each would be part of what is timed); then the same region again with them, for
+    # the kernels' durations (roofline)
+    def timed(events):
+        D.barrier()
+        for P in probs:
+            P.timing(events)
+        t0 = time.perf_counter()
+        run_items(lambda i: probs[i].path(chunks[i], np.full(probs[i].N, ymeans[i]), chunks[i][0] / 5.0,
+                                          want_thetas=False, fixed_iters=per, **opts))
+        t1 = time.perf_counter()
+        D.barrier()
+        tm = [P.timings() for P in probs] if events else None
+        for P in probs:
+            P.timing(False)
+        return t1 - t0, tm
+    elapsed, _ = timed(False)
+    elapsed_ev, tims = timed(True)
+    t0, t1 = 0.0, elapsed_ev
+    g_elapsed, = D.allreduce([elapsed], "max")
     stats = [o[2] for o in out]
     kbar = sum(st["pcg_iters"] for sts in stats for st in sts) / (steps * B)
     tim = {k: dict(ms=sum(t[k]["ms"] for t in tims), launches=sum(t[k]["launches"] for t in tims),
@@ -437,9 +445,11 @@ def cv_main(a, D):
                    "pcg_rtol": a.pcg_rtol, "pcg_iters_mean": round(kbar, 2), "rho_out": rhos,
                    "parallelism": f"(fold, lambda-chunk) work items, {B} concurrent per GPU (x{D.world})"},
         "roofline": roof,
-        "aggregate_hbm": {"bytes": moved, "GBps": round(moved / (t1 - t0) / 1e9, 1),
-                          "frac": round(moved / (t1 - t0) / 1e9 / HBM_PEAK_GBPS, 4),
+        "aggregate_hbm": {"bytes": moved, "GBps": round(moved / elapsed / 1e9, 1),
+                          "frac": round(moved / elapsed / 1e9 / HBM_PEAK_GBPS, 4),
                           "note": "algorithmic bytes of every launch of the rank's items / the rank's wall time"},
+        "with_kernel_events": {"ms_per_step": round(elapsed_ev / steps * 1e3, 3),
+                               "note": "the same region timed with HIP events around every launch (roofline)"},
         "kernels": kern, "cpu_baseline": None}
 
 

@@ -661,6 +661,18 @@ __global__ __launch_bounds__(f3a::NT) void k_admm3a(const Fused3dArgs a) {
 }
 
 namespace {
+// compute units of the current device (the fused kernel's concurrent workgroups: one per CU)
+int device_cus() {
+    static thread_local int dev = -1, cus = 256;
+    int d = 0;
+    if (hipGetDevice(&d) == hipSuccess && d != dev) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+        dev = d;
+    }
+    return cus;
+}
+
 Fused3dArgs f3d_args(const Geom& g) {
     Fused3dArgs a{};
     a.g = g;
@@ -672,18 +684,38 @@ Fused3dArgs f3d_args(const Geom& g) {
     a.tiles_y = int((int(g.m[1]) + f3a::TY - 1) / f3a::TY);
     a.tpz = a.tiles_x * a.tiles_y;
     const int tiles = a.tpz;
-    // dim-2 chunks: ~4096 workgroups, or up to ~8192 while a chunk keeps >= 32 planes (each chunk
-    // recomputes one plane). 512^3: 6 -> 13 chunks, fused kernel -2 % on two boxes, each setting
-    // timed in one process (tools/zchunk_probe.py, profiles/r01/v10_zchunk_probe.txt)
+    // dim-2 chunks. A workgroup (1024 threads, 94 KB of LDS: one per CU) marches zc planes and recomputes
+    // one at its start, so the launch costs ~ waves x (zc + 1 + c0), waves = ceil(workgroups / CUs). Among
+    // chunkings of <= 32 planes that give >= 2.5 waves (fewer leave the tail of the last wave exposed; longer
+    // chunks measured slower at 512^3: 6 chunks of 86 planes 2 % behind 16 of 32, round 1) the one minimising
+    // that cost with c0 = 1; tiny meshes: the cheapest of all. Measured per setting in one process
+    // (tools/zchunk_probe.py, profiles/r03/v2_zchunk): 256^3 0.549 ms at the old ~4096-workgroup target
+    // (5-plane chunks) -> 0.488 ms (26 planes, 760 workgroups); a 512^3 slab rank of 64 planes (8 GPUs)
+    // 0.59 -> 0.513 ms (16 planes); 512^3 unchanged (32 planes, 3.53 ms, the best of six settings).
     const char* wge = probe_env("MVTV_F3D_WG");   // read per launch set-up: the probe varies it
     const int nzp = std::max(1, a.zhi - a.zlo);
-    int nz;
+    int nz = 1;
     if (wge) {
         nz = std::max(1, std::min(nzp, std::atoi(wge) / std::max(1, tiles)));
     } else {
-        const int nz4 = std::max(1, std::min(nzp, 4096 / std::max(1, tiles)));
-        const int nz8 = std::min(std::min(nzp, 8192 / std::max(1, tiles)), nzp / 32);
-        nz = std::max(nz4, nz8);
+        const int cus = device_cus();
+        auto cost_of = [&](int nzr, int zc) { return ((long(tiles) * nzr + cus - 1) / cus) * (zc + 2); };
+        for (int pass = 0; pass < 2 && nz == 1; ++pass) {
+            auto ok = [&](int nzr, int zc) { return pass == 1 || (zc <= 32 && 2L * tiles * nzr >= 5L * cus); };
+            long best = -1;
+            for (int c = 1; c <= nzp; ++c) {
+                const int zc = (nzp + c - 1) / c, nzr = (nzp + zc - 1) / zc;
+                if (nzr == c && ok(nzr, zc) && (best < 0 || cost_of(nzr, zc) < best)) best = cost_of(nzr, zc);
+            }
+            // the longest chunks within 2 % of the cheapest (the model's resolution)
+            for (int c = 1; c <= nzp && best >= 0; ++c) {
+                const int zc = (nzp + c - 1) / c, nzr = (nzp + zc - 1) / zc;
+                if (nzr == c && ok(nzr, zc) && 50 * cost_of(nzr, zc) <= 51 * best) {
+                    nz = nzr;
+                    break;
+                }
+            }
+        }
     }
     while (nz > 1 && ((nz * tiles + 7) / 8 * 8) * 7 > kMaxCgBlocks * kMaxRed) --nz;
     a.zchunk = (nzp + nz - 1) / nz;

@@ -12,3 +12,7 @@ for v in 16 32 16 32; do
   MVTV_TRI_TQ=$v timeout -k 10 200 python bench.py --no-cpu --pcg-steps 0 --steps 30 --warmup 3 > $O/tri_tq$v.json 2> $O/tri_tq$v.err || exit 1
   python -c "import json;d=json.load(open('$O/tri_tq$v.json'));print('tq $v', d['ms_per_step'], d['kernels']['dct'], d['kernels']['dct_first'])" >> $O/tri.txt
 done
+unset MVTV_LIB_PATH
+timeout -k 10 300 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_slab.py > $O/slab_tests.log 2>&1 && \
+timeout -k 10 300 python bench.py --mode cv --steps 40 --warmup 5 > $O/cv4.json 2> $O/cv4.err && \
+timeout -k 10 300 python bench.py --mode cv --steps 40 --warmup 5 --cv-batch 2 > $O/cv2.json 2> $O/cv2.err

@@ -4,6 +4,12 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r3c
 mkdir -p $O
+cd $R
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_fused3d.py tests/test_gpu_parity.py \
+  tests/test_gpu_slab.py > $O/tests.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --dims 3 --size 256 > $O/b256.json 2> $O/b256.err || exit 1
+timeout -k 10 300 python bench.py --no-cpu > $O/b512.json 2> $O/b512.err || exit 1
+timeout -k 10 300 python bench.py --mode cv --steps 40 --warmup 5 > $O/cv4.json 2> $O/cv4.err || exit 1
 cd /tmp && export TMPDIR=/tmp
 pmc() {  # name counter args...
   local n=$1 c=$2; shift 2
