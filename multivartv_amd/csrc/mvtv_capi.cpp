@@ -187,6 +187,15 @@ mvtv_status export_edges(mvtv_problem* P, const double* padded, double* host_u, 
     return MVTV_OK;
 }
 
+// PCG iterations enqueued before the first poll: the last solve's count plus this (probe: MVTV_PCG_AHEAD)
+int pcg_ahead() {
+    static const int v = [] {
+        const char* e = probe_env("MVTV_PCG_AHEAD");
+        return e ? std::atoi(e) : -2;
+    }();
+    return v;
+}
+
 // Solve (W + sigma D^T D) x = b, b = oty + ca*ga + cb*gb, by Jacobi-PCG warm-started at x.
 mvtv_status pcg_solve(mvtv_problem* P, double sigma, const double* oty, const double* ga, double ca,
                       const double* gb, double cb, double* x, double rtol, int maxit, int* iters, double* relres) {
@@ -246,7 +255,7 @@ mvtv_status pcg_solve(mvtv_problem* P, double sigma, const double* oty, const do
     // so the first poll comes just before it and later polls every 2 iterations.
     std::vector<size_t> mark;   // first timing entry of each enqueued iteration
     int enq = 0;
-    int batch = P->pcg_hint > 0 ? std::max(2, P->pcg_hint - 2) : kPcgPoll;
+    int batch = P->pcg_hint > 0 ? std::max(2, P->pcg_hint + pcg_ahead()) : kPcgPoll;
     for (;;) {
         for (int b = 0; b < batch && enq < maxit; ++b, ++enq) {
             mark.push_back(P->pending.size());
@@ -466,7 +475,7 @@ mvtv_status pcgs_solve(mvtv_problem* P, double sigma, const double* oty, const d
     };
     std::vector<size_t> mark;
     int enq = 0;
-    int batch = P->pcg_hint > 0 ? std::max(2, P->pcg_hint - 2) : kPcgPoll;
+    int batch = P->pcg_hint > 0 ? std::max(2, P->pcg_hint + pcg_ahead()) : kPcgPoll;
     for (;;) {
         for (int bb = 0; bb < batch && enq < maxit; ++bb, ++enq) {
             mark.push_back(P->pending.size());
