@@ -127,7 +127,7 @@ def parse():
     ap.add_argument("--cpu-planes", type=int, default=0,
                     help="cpu_baseline sample: slowest-dim planes of the mesh (0 = a quarter of them)")
     ap.add_argument("--cpu-full", action="store_true", help="cpu_baseline on the whole mesh (no extrapolation)")
-    ap.add_argument("--cv-batch", type=int, default=4,
+    ap.add_argument("--cv-batch", type=int, default=8,
                     help="--mode cv: work items (fold, lambda chunk) run at once per GPU, one HIP stream each")
     ap.add_argument("--dry-run", action="store_true", help="launcher test: ranks report their env and exit")
     ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)

@@ -869,7 +869,7 @@ __global__ __launch_bounds__(e4d::NT) void k_edge4d(const Edge4dArgs a) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
                 const double d = g.w[k] * v[S];
-                double* ep = a.edges + uint64_t(k) * g.N + i;
+                double* ep = a.edges + eix(g, k, i);
                 const double stored = __builtin_nontemporal_load(ep);
                 const double uo = (UM == U_EXPLICIT) ? stored : -c_old * clampd(stored, t_old);
                 const double z = d - uo;
@@ -920,13 +920,13 @@ __global__ __launch_bounds__(e4d::NT) void k_gather4d(const Edge4dArgs a) {
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
             constexpr int SI = S & 7;
-            const double* eb = a.edges + uint64_t(k) * g.N + uint32_t(w) * pl + base;
+            const uint32_t ib = uint32_t(w) * pl + base;
             qa = 0.0;
             qu = 0.0;
 #pragma unroll
             for (int q = 0; q < PC; ++q) {
                 if ((q & ~SI) != 0) continue;
-                const double vv = *(eb - qoff[q]);
+                const double vv = a.edges[eix(g, k, ib - qoff[q])];
                 const double v = qok[q] ? vv : 0.0;
                 const bool neg = __builtin_popcount(q) & 1;
                 if constexpr (UM == U_FROM_Z) {
@@ -1129,13 +1129,13 @@ __global__ __launch_bounds__(64 * TYV) void k_gather4a(const Gather4Args a) {
         constexpr int k = decltype(kc)::value;
         constexpr int S = sprime_mask(block_code(k, P, ORD), P);
         constexpr int SI = S & 3;
-        const double* eb = a.edges + uint64_t(k) * g.N + uint32_t(e) * m01 + base;
+        const uint32_t ib = uint32_t(e) * m01 + base;
         qa = 0.0;
         qu = 0.0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if ((q & ~SI) != 0) continue;
-            const double vv = *(eb - qoff[q]);
+            const double vv = a.edges[eix(g, k, ib - qoff[q])];
             const double v = qok[q] ? vv : 0.0;
             const bool neg = __builtin_popcount(q) & 1;
             if constexpr (UM == U_FROM_Z) {

@@ -187,11 +187,13 @@ mvtv_status export_edges(mvtv_problem* P, const double* padded, double* host_u, 
     return MVTV_OK;
 }
 
-// PCG iterations enqueued before the first poll: the last solve's count plus this (probe: MVTV_PCG_AHEAD)
+// PCG iterations enqueued before the first poll: the last solve's count plus this (probe: MVTV_PCG_AHEAD).
+// Config 4's work item (2048^2 fold, one stream): -2 327, 0 335, +2 326, +4 325 ADMM it/s on one box
+// (profiles/r03/v5_cv_tuning)
 int pcg_ahead() {
     static const int v = [] {
         const char* e = probe_env("MVTV_PCG_AHEAD");
-        return e ? std::atoi(e) : -2;
+        return e ? std::atoi(e) : 0;
     }();
     return v;
 }
@@ -695,7 +697,7 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
         // 64-node chunks, so every rank must pick the same layout
         const uint64_t plane = g.N / g.m[g.p - 1];
         const bool chunks = P->slab ? plane % 64 == 0 : g.N % 64 == 0;
-        g.eaos = (want && P->f3d && g.p == 3 && chunks) ? 1u : 0u;
+        g.eaos = (want && ((P->f3d && g.p == 3) || (P->e3d && g.p == 4)) && chunks) ? 1u : 0u;
     }
     if (s == MVTV_OK) s = mvtv_problem_set_data(P, d->oty, d->wdiag);
     if (s != MVTV_OK) {
