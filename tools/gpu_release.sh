@@ -3,17 +3,18 @@
 # PMC calibration copies. Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-mkdir -p $R/gpurun_out/rel
+O=${REL_OUT:-gpurun_out/rel}
+mkdir -p $R/$O
 cd $R
-timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/rel/gpu_tests.log 2>&1
-rc=$?; tail -2 gpurun_out/rel/gpu_tests.log
+timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1
+rc=$?; tail -2 $O/gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests rc=$rc: stopping"; exit $rc; fi
-timeout -k 10 60 tools/bin/stream_bench > gpurun_out/rel/stream.txt 2>&1 &&
-timeout -k 10 600 python bench.py > gpurun_out/rel/bench.json 2> gpurun_out/rel/bench.err &&
+timeout -k 10 60 tools/bin/stream_bench > $O/stream.txt 2>&1 &&
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err &&
 cd /tmp && export TMPDIR=/tmp &&
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/rel/prof_kt -o run --output-format csv -- python3 $R/bench.py --no-cpu --steps 10 --warmup 2 > $R/gpurun_out/rel/prof_kt.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $R/gpurun_out/rel/prof_fetch -o run --output-format csv -- python3 $R/bench.py --no-cpu --pcg-steps 2 --steps 2 --warmup 1 > $R/gpurun_out/rel/prof_fetch.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $R/gpurun_out/rel/prof_write -o run --output-format csv -- python3 $R/bench.py --no-cpu --pcg-steps 2 --steps 2 --warmup 1 > $R/gpurun_out/rel/prof_write.log 2>&1 &&
-timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $R/gpurun_out/rel/calib_fetch -o run --output-format csv -- $R/tools/bin/pmc_calib > $R/gpurun_out/rel/calib_fetch.log 2>&1 &&
-timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $R/gpurun_out/rel/calib_write -o run --output-format csv -- $R/tools/bin/pmc_calib > $R/gpurun_out/rel/calib_write.log 2>&1
-rc2=$?; cd $R; [ $rc2 -eq 0 ] && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/rel/smoke.log 2>&1; echo "tests rc=$rc release rc=$rc2 smoke rc=$?"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof_kt -o run --output-format csv -- python3 $R/bench.py --no-cpu --steps 10 --warmup 2 > $R/$O/prof_kt.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $R/$O/prof_fetch -o run --output-format csv -- python3 $R/bench.py --no-cpu --pcg-steps 2 --steps 2 --warmup 1 > $R/$O/prof_fetch.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $R/$O/prof_write -o run --output-format csv -- python3 $R/bench.py --no-cpu --pcg-steps 2 --steps 2 --warmup 1 > $R/$O/prof_write.log 2>&1 &&
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $R/$O/calib_fetch -o run --output-format csv -- $R/tools/bin/pmc_calib > $R/$O/calib_fetch.log 2>&1 &&
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $R/$O/calib_write -o run --output-format csv -- $R/tools/bin/pmc_calib > $R/$O/calib_write.log 2>&1
+rc2=$?; cd $R; [ $rc2 -eq 0 ] && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; echo "tests rc=$rc release rc=$rc2 smoke rc=$?"
