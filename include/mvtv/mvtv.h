@@ -202,7 +202,10 @@ mvtv_status mvtv_solve_spectral(mvtv_problem* prob, double sigma, const double* 
  * mvtv_slab_run is the whole variant-B loop of one rank (rcpp…/solvers.cpp:110-133) with its
  * collectives on the problem's stream: all-to-all transposes of the distributed cosine-transform solve,
  * halo planes of theta and of the edge state, one 7-value all-reduce per iteration feeding the device-side
- * adapt_step / stopping decision. Supported: variant B, W = I, power-of-two m_j, u0 = 0. */
+ * adapt_step / stopping decision. Supported: variant B, W = I, u0 = 0, m_j <= 4096 a product of 2, 3, 5, 7
+ * for j < p - 1; the last dimension any length when G >= 2 (its line solves are substructured over the ranks;
+ * each rank's plane count must be 1..64 segments of <= 32 rows, e.g. any count <= 64 or with a divisor in
+ * 2..32 giving <= 64 segments), a 2-3-5-7 length <= 4096 when G = 1. */
 typedef struct mvtv_slab_desc {
     int64_t m_global;          /* planes of dim p-1 in the whole mesh */
     int64_t z_begin, z_end;    /* owned planes */

@@ -676,15 +676,20 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
         return s;
     }
     P->host_st = reinterpret_cast<PcgState*>(P->host_red + 16);
-    P->spec_mesh = P->spec_pow2 = true;
+    P->spec_mesh = P->spec_pow2 = P->spec_lead = true;
     for (int j = 0; j < p; ++j) {
         const uint32_t mj = uint32_t(mg[j]);
         int rad[8], nrad = 0;
-        if (mj > 4096 || !dct_radix_plan(mj, rad, &nrad)) P->spec_mesh = false;
+        if (mj > 4096 || !dct_radix_plan(mj, rad, &nrad)) {
+            P->spec_mesh = false;
+            if (j < p - 1) P->spec_lead = false;
+        }
         if ((mj & (mj - 1)) != 0) P->spec_pow2 = false;
     }
     if (!P->spec_mesh) P->spec_pow2 = false;
-    if (P->spec_mesh) s = spectral_plan(P);
+    // a slab problem's last dimension is solved by the substructured line solves (any length): the tables
+    // are needed for the transforms along dims 0..p-2 only
+    if (P->spec_mesh || (P->slab && P->spec_lead && p >= 2)) s = spectral_plan(P);
     P->e3d = edge3d_ok(g);
     if (s == MVTV_OK && P->e3d && g.p == 4 && gather4_ok(g)) s = alloc(&P->g4, 4 * size_t(N));
     P->f3d = fused3d_ok(g);   // slab problems too: the fused pass runs on the owned planes (Geom.ibeg/iend)

@@ -80,7 +80,8 @@ struct mvtv_problem {
     PcgState* host_st = nullptr;
     SpecPlan spec;                // spectral theta-solve tables (allocated when the mesh allows it)
     bool spec_mesh = false;       // every m_j <= 4096 a product of 2, 3, 5, 7 (spectral solve)
-    bool spec_pow2 = false;       // ... and a power of two (slab decomposition, k_dct8 / k_tri passes)
+    bool spec_pow2 = false;       // ... and a power of two (k_dct8 / k_tri passes)
+    bool spec_lead = false;       // dims 0..p-2 are (the slab loop: the last dimension may have any length)
     bool e3d = false;             // z-marching 3-D edge kernels
     bool f3d = false;             // fused 3-D edge update + gather (needs the second edge buffer)
     double* edges2 = nullptr;     // ping-pong partner of edges for the fused kernel

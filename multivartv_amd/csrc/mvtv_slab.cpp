@@ -440,7 +440,10 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
                      double rho0, mvtv_admm_stats* stats) {
     if (!P->slab) return fail(MVTV_BAD_ARG, "not a slab problem (mvtv_problem_create_slab)");
     if (opts->variant != MVTV_VARIANT_RCPP) return fail(MVTV_BAD_ARG, "the slab loop runs variant B");
-    if (P->wmode != W_IDENTITY || !P->spec_pow2) return fail(MVTV_BAD_ARG, "slab loop: W = I, power-of-two m_j <= 4096");
+    if (P->wmode != W_IDENTITY || !P->spec_lead || P->g.p < 2)
+        return fail(MVTV_BAD_ARG, "slab loop: W = I, p >= 2, m_j <= 4096 products of 2, 3, 5, 7 for j < p - 1");
+    if (C->size == 1 && !P->spec_mesh)
+        return fail(MVTV_BAD_ARG, "slab loop on one rank: the last dimension too must be <= 4096 and 2-3-5-7");
     if (!(lambda >= 0.0) || !(rho0 > 0.0)) return fail(MVTV_BAD_ARG, "lambda >= 0 and rho0 > 0");
     const auto t0 = std::chrono::steady_clock::now();
     DeviceGuard dg(P->device);

@@ -82,6 +82,36 @@ def test_loopback_failing_rank_does_not_hang_its_peers():
         c.close()
 
 
+@pytest.mark.parametrize("m,world", [([60, 60, 45], 3), ([24, 24, 37], 2), ([48, 48, 130], 4), ([40, 100], 4)],
+                         ids=["3d_60x60x45_w3_mixed_radix", "3d_24x24x37_w2_prime_last", "3d_48x48x130_w4",
+                              "2d_40x100_w4"])
+def test_slab_any_last_dimension_vs_c_oracle(m, world):
+    """The last dimension's line solves are substructured over the ranks, so it may have any length (37 is
+    prime; 45, 130 not powers of two) and the leading dims any 2-3-5-7 length (k_dctg passes): 12 fixed
+    iterations against the C oracle's loop with the exact scipy.fft solve, rho exact, theta 1e-9."""
+    from oracle import c_oracle
+    lam, fixed = 0.7, 12
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    th = np.full(y.size, y.mean())
+    u = np.zeros(c_oracle.num_edges(m))
+    ref = c_oracle.admm_rcpp_spectral(m, y, lam, th, u, lam / 5.0, deltas, fixed_iters=fixed)
+    out, theta = slab.run_local_group(m, y, deltas, lam, world, fixed_iters=fixed)
+    assert all(o["iters"] == fixed and o["rho"] == ref["rho"] for o in out)
+    assert _rel(theta, th) <= 1e-9
+    assert out[0]["r_norm"] == pytest.approx(ref["r_norm"], rel=1e-8)
+
+
+def test_slab_one_rank_needs_a_spectral_last_dimension():
+    y = towers([24, 24, 37])
+    comm = slab.Comm.local_group(1)[0]
+    S = slab.SlabADMM([24, 24, 37], y, [(1.0 + 2e-4) / v for v in (24, 24, 37)], y.mean(), comm)
+    with pytest.raises(mv.MvtvError):
+        S.run(1.0, fixed_iters=2)
+    S.close()
+    comm.close()
+
+
 def test_slab_4d_16_four_ranks_vs_c_oracle():
     """Config 5's decomposition (4-D, dim 3 split, 4 planes per rank) against the C oracle rather than
     the one-GPU HIP path: 20 fixed iterations of variant B from theta0 = mean y, u0 = 0."""
