@@ -2,9 +2,12 @@
 # one bench line per BASELINE config (with cpu_baseline), then a kernel trace of each shorter run
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/cfg
+O=$R/${CFG_OUT:-gpurun_out/cfg}
 mkdir -p $O
 cd $R
+if [ -n "$CFG_TESTS" ]; then
+  timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread $CFG_TESTS > $O/tests.log 2>&1 || exit 1
+fi
 run() {  # name, args...
   local n=$1; shift
   echo "== $n $*" >> $O/progress.log
@@ -12,6 +15,7 @@ run() {  # name, args...
 }
 run b512 && run b1024 --dims 2 --size 1024 && run b2048 --dims 2 --size 2048 && run b256 --dims 3 --size 256 && \
 run b128_4d --dims 4 --size 128 --pcg-steps 4 && run bcv --mode cv --steps 40 --warmup 5 && \
+run bslab1 --mode slab --no-cpu && \
 run b500 --dims 3 --size 500 --steps 10 --warmup 2 --pcg-steps 5 && run b1000 --dims 2 --size 1000 --pcg-steps 20 || exit 1
 cd /tmp && export TMPDIR=/tmp
 kt() {
@@ -19,7 +23,5 @@ kt() {
   echo "== kt $n $*" >> $O/progress.log
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_$n -o run --output-format csv -- python3 $R/bench.py --no-cpu "$@" > $O/kt_$n.log 2>&1
 }
-kt b512 --steps 10 --warmup 2 && kt b1024 --dims 2 --size 1024 --pcg-steps 2 && kt b256 --dims 3 --size 256 --pcg-steps 2 && \
-kt b128_4d --dims 4 --size 128 --pcg-steps 2 --steps 6 && kt bcv --mode cv --steps 20 --warmup 2 && \
-kt b500 --dims 3 --size 500 --steps 5 --warmup 1 --pcg-steps 2
+kt b1024 --dims 2 --size 1024 --pcg-steps 2 && kt bcv --mode cv --steps 20 --warmup 2 --cv-batch 1
 echo "rc=$?"
