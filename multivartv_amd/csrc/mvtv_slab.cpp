@@ -129,10 +129,12 @@ struct SelfCopy {
     }
 };
 
+// Every transfer goes through RCCL, the rank's own ones too (send / recv to self in the group), and the
+// all-reduce runs at one rank as well: one-GPU runs of the distributed loop (MVTV_SLAB_DISTRIBUTED=1 at
+// world size 1) execute the same RCCL calls as the 8-GPU runs.
 struct RcclComm final : mvtv_comm {
     RcclApi* api_ = nullptr;
     ncclComm_t comm = nullptr;
-    SelfCopy self;
     ~RcclComm() override {
         if (comm && api_->CommDestroy) api_->CommDestroy(comm);
         if (scratch) (void)hipFree(scratch);
@@ -143,15 +145,10 @@ struct RcclComm final : mvtv_comm {
         return MVTV_OK;
     }
     mvtv_status send(const double* buf, size_t n, int peer, hipStream_t s) override {
-        if (peer == rank) {
-            self.q.emplace_back(buf, n);
-            return MVTV_OK;
-        }
         NCCL_TRY(api_->Send(buf, n, ncclFloat64, peer, comm, s));
         return MVTV_OK;
     }
     mvtv_status recv(double* buf, size_t n, int peer, hipStream_t s) override {
-        if (peer == rank) return self.recv(buf, n, s);
         NCCL_TRY(api_->Recv(buf, n, ncclFloat64, peer, comm, s));
         return MVTV_OK;
     }
@@ -160,7 +157,6 @@ struct RcclComm final : mvtv_comm {
         return MVTV_OK;
     }
     mvtv_status allreduce_sum(double* buf, size_t n, hipStream_t s) override {
-        if (size == 1) return MVTV_OK;
         NCCL_TRY(api_->AllReduce(buf, buf, n, ncclFloat64, ncclSum, comm, s));
         return MVTV_OK;
     }
@@ -404,7 +400,7 @@ void mvtv_comm_destroy(mvtv_comm* c) { delete c; }
 mvtv_status mvtv_comm_allreduce_host(mvtv_comm* c, double* vals, int32_t n) {
     if (!c || (!vals && n > 0) || n < 0 || n > 64) return fail(MVTV_BAD_ARG, "bad argument (n <= 64)");
     if (!dynamic_cast<RcclComm*>(c)) return fail(MVTV_BAD_ARG, "host all-reduce: RCCL communicators only");
-    if (c->size == 1 || n == 0) return MVTV_OK;
+    if (n == 0) return MVTV_OK;
     DeviceGuard dg(c->device);
     if (!c->stream) HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     if (!c->scratch) MVTV_TRY(alloc(&c->scratch, 64));
@@ -481,8 +477,11 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     const bool fused = P->f3d;
     // interface buffers of the distributed line solves (16 numbers per line): the 6 coefficients of this
     // rank's blocks by chunk, the chunk's coefficients from every rank, the (L, R) values by rank, and the
-    // values of this rank's lines by chunk. One rank: the line solves are local, no buffers, no transfers
-    const bool solo = G == 1;
+    // values of this rank's lines by chunk. One rank: the line solves are local, no buffers, no transfers,
+    // unless MVTV_SLAB_DISTRIBUTED=1 asks for the distributed path at one rank (its transfers to itself),
+    // which runs every collective call of the G-rank loop on one GPU
+    const char* force = std::getenv("MVTV_SLAB_DISTRIBUTED");
+    const bool solo = G == 1 && !(force && std::atoi(force) != 0);
     if (!solo && !P->slab_iface) MVTV_TRY(alloc(&P->slab_iface, 16 * size_t(sg.lines)));
     if (fused && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
     const size_t nodes = P->g.N, ebytes = size_t(P->g.nb) * nodes * sizeof(double);

@@ -142,6 +142,25 @@ def test_rccl_single_rank(fixed):
     comm.close()
 
 
+@pytest.mark.parametrize("transport", ["rccl", "loopback"])
+@pytest.mark.parametrize("m", [[32, 32, 32], [16, 16, 16, 16]], ids=["3d_32", "4d_16"])
+def test_distributed_path_at_one_rank(transport, m, monkeypatch):
+    """MVTV_SLAB_DISTRIBUTED=1 at world size 1: the G-rank loop (substructured line solves with their
+    all-to-alls, the collectives' stream and its events, the all-reduce) on one GPU; over RCCL every
+    ncclSend / ncclRecv / ncclAllReduce call the multi-GPU runs make, to the rank itself. Converged run:
+    iterations and rho exact against the one-GPU path, theta 1e-11."""
+    monkeypatch.setenv("MVTV_SLAB_DISTRIBUTED", "1")
+    lam = 1.0
+    y, deltas, th, rho, st = _reference(m, lam, 0)
+    comm = slab.Comm.rccl_single(0) if transport == "rccl" else slab.Comm.local_group(1)[0]
+    S = slab.SlabADMM(m, y, deltas, y.mean(), comm, device=0)
+    o = S.run(lam, fixed_iters=0)
+    assert o["iters"] == st["iters"] and o["rho"] == rho
+    assert _rel(S.theta_owned(), th) <= 1e-11
+    S.close()
+    comm.close()
+
+
 def _rccl_rank_main(port, q):
     import torch
     import torch.distributed as dist
