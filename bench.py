@@ -412,8 +412,16 @@ def cv_main(a, D):
     N = probs[0].N
     roof["mall_resident"] = 8 * N * 7 < 256 * 2 ** 20
     moved = sum(v["bytes_per_launch"] * v["launches"] for v in tim.values())
-    roof["note"] = ("per-launch time of the dominant kernel while the rank's items run concurrently" if B > 1 else
-                    "per-launch time of the dominant kernel")
+    if B > 1:
+        # the items' launches overlap, so a launch's duration is shared with other items' kernels: the roofline
+        # object is the whole GPU's, the algorithmic bytes of every launch of the event-free region over its time
+        per_kernel = dict(roof, note="dominant kernel's launch time while the items run concurrently")
+        ach = moved / elapsed / 1e9
+        roof = {"bound": "hbm", "kernel": f"all launches of the {B} concurrent items", "achieved": round(ach, 1),
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                "mall_resident": per_kernel["mall_resident"], "dominant_kernel_concurrent": per_kernel}
+    else:
+        roof["note"] = "per-launch time of the dominant kernel"
     kern = {k: dict(avg_ms=round(v["ms"] / v["launches"], 4), launches=v["launches"]) for k, v in tim.items()
             if v["launches"]}
     rhos = [float(o[1][-1]) for o in out]
