@@ -761,10 +761,17 @@ mvtv_status mvtv_problem_set_data(mvtv_problem* P, const double* oty, const doub
         P->wmean = acc / double(P->g.N);
         for (uint32_t i = 0; i < P->g.N; ++i) acc2 += (wdiag[i] - P->wmean) * (wdiag[i] - P->wmean);
         P->wstd = std::sqrt(acc2 / double(P->g.N));
+        // a slab rank's share of the global mean / spread (its owned planes), summed over the ranks by mvtv_slab_run
+        P->wsum_own = P->wsum2_own = 0.0;
+        for (uint32_t i = P->g.ibeg; i < P->g.iend; ++i) {
+            P->wsum_own += wdiag[i];
+            P->wsum2_own += wdiag[i] * wdiag[i];
+        }
     } else {
         P->wmode = W_IDENTITY;
         P->wmean = 1.0;
         P->wstd = 0.0;
+        P->wsum_own = P->wsum2_own = double(P->g.iend - P->g.ibeg);
     }
     HIP_TRY(hipStreamSynchronize(P->stream));
     return MVTV_OK;

@@ -272,10 +272,12 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
 // the local block into coef [chunk s][6][line in chunk]; phase 3: x = scale * (local solve with the
 // neighbours' values lr [chunk s][2][line in chunk]) in place. lo_ext / hi_ext: the lines continue on the
 // rank below / above. launch_tri_iface: the interface systems of one chunk's lines over the G ranks.
+// sigma, w0: the operator c0 = w0 + ..., c1 (ignored when ctl gives sigma); skip: return at once when *skip
 hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, int phase, double* x, double* coef,
                            const double* lr, uint32_t chunk, int lo_ext, int hi_ext, double scale,
-                           const AdmmCtl* ctl);
-hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint32_t chunk, int G, const AdmmCtl* ctl);
+                           const AdmmCtl* ctl, double sigma = 1.0, double w0 = 1.0, const int32_t* skip = nullptr);
+hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint32_t chunk, int G, const AdmmCtl* ctl,
+                            const int32_t* skip = nullptr);
 // z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /
 // launch_gather, *nparts workgroup rows
 bool edge3d_ok(const Geom& g);

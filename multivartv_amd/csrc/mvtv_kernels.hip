@@ -257,7 +257,8 @@ __global__ __launch_bounds__(kThreads) void k_apply_A(Geom g, StencilK sk, doubl
         if (st->done) return;
     }
     double red[1] = {0.0};
-    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < g.N; i += gridDim.x * kThreads) {
+    // nodes [ibeg, iend): a slab rank's owned planes (its ghost planes are read as neighbours only)
+    for (uint32_t i = g.ibeg + blockIdx.x * kThreads + threadIdx.x; i < g.iend; i += gridDim.x * kThreads) {
         uint32_t c[kMaxDims];
         decode<P>(g, i, c);
         const double xi = x[i];

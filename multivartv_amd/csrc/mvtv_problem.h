@@ -94,6 +94,7 @@ struct mvtv_problem {
     double* g4 = nullptr;         // 4 N-arrays: the two-pass 4-D gather's partial sums
     double wmean = 1.0;           // mean(W): the preconditioner's identity weight
     double wstd = 0.0;            // std(W): chooses the diagonally scaled spectral preconditioner
+    double wsum_own = 0.0, wsum2_own = 0.0;   // sum W, sum W^2 over the nodes [ibeg, iend) (slab: owned planes)
     double* pcg_s = nullptr;      // 1/s of the scaled spectral preconditioner
     double* pcg_t = nullptr;      // r / s, the preconditioner's input
     AdmmCtl* ctl = nullptr;       // device control block of the asynchronous ADMM loop

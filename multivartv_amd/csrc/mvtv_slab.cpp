@@ -436,8 +436,8 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
                      double rho0, mvtv_admm_stats* stats) {
     if (!P->slab) return fail(MVTV_BAD_ARG, "not a slab problem (mvtv_problem_create_slab)");
     if (opts->variant != MVTV_VARIANT_RCPP) return fail(MVTV_BAD_ARG, "the slab loop runs variant B");
-    if (P->wmode != W_IDENTITY || !P->spec_lead || P->g.p < 2)
-        return fail(MVTV_BAD_ARG, "slab loop: W = I, p >= 2, m_j <= 4096 products of 2, 3, 5, 7 for j < p - 1");
+    if (P->wmode == W_NONE || !P->spec_lead || P->g.p < 2)
+        return fail(MVTV_BAD_ARG, "slab loop: W = I or diagonal, p >= 2, m_j <= 4096 products of 2, 3, 5, 7 for j < p - 1");
     if (C->size == 1 && !P->spec_mesh)
         return fail(MVTV_BAD_ARG, "slab loop on one rank: the last dimension too must be <= 4096 and 2-3-5-7");
     if (!(lambda >= 0.0) || !(rho0 > 0.0)) return fail(MVTV_BAD_ARG, "lambda >= 0 and rho0 > 0");
@@ -460,16 +460,26 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     for (int r = 0; r <= G; ++r) zbs[size_t(r)] = uint32_t(uint64_t(sg.mg) * uint64_t(r) / uint64_t(G));
     if (zbs[size_t(rk)] != sg.zb || zbs[size_t(rk) + 1] != sg.zb + sg.nz)
         return fail(MVTV_BAD_ARG, "slab plane range differs from the even split of the communicator");
-    {   // every rank must enqueue the same loop: the fused pass or not, and the same edge layout (the z halo
-        // moves whole planes in it). One sum of the flags; a mismatch fails on every rank alike
-        double flags[4] = {P->f3d ? 1.0 : 0.0, P->g.eaos ? 1.0 : 0.0, P->e3d ? 1.0 : 0.0, double(sg.plane)};
+    const bool wd = P->wmode == W_DIAG;
+    double w0 = 1.0, wstd = 0.0;   // mean and spread of W over the whole mesh
+    {   // every rank must enqueue the same loop: the fused pass or not, the same edge layout (the z halo moves
+        // whole planes in it), W or not. One sum of the flags, with the ranks' shares of sum W and sum W^2; a
+        // mismatch fails on every rank alike
+        double flags[7] = {P->f3d ? 1.0 : 0.0, P->g.eaos ? 1.0 : 0.0, P->e3d ? 1.0 : 0.0, double(sg.plane),
+                           wd ? 1.0 : 0.0, P->wsum_own, P->wsum2_own};
         HIP_TRY(hipMemcpyAsync(P->red, flags, sizeof(flags), hipMemcpyHostToDevice, s));
-        MVTV_TRY(C->allreduce_sum(P->red, 4, s));
-        double sum[4];
+        MVTV_TRY(C->allreduce_sum(P->red, 7, s));
+        double sum[7];
         HIP_TRY(hipMemcpyAsync(sum, P->red, sizeof(sum), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < 5; ++k)
             if (sum[k] != double(G) * flags[k]) return fail(MVTV_BAD_ARG, "slab ranks disagree on the loop layout");
+        const double n_all = double(sg.plane) * double(sg.mg);
+        if (wd) {
+            w0 = sum[5] / n_all;
+            wstd = std::sqrt(std::max(0.0, sum[6] / n_all - w0 * w0));
+            if (!(w0 > 0.0)) w0 = 1.0;
+        }
     }
 
     const double tol = opts->tol > 0 ? opts->tol : 1e-4;
@@ -590,87 +600,226 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         return C->end(sc);
     };
 
+    // ghost planes of a node vector v (theta, or PCG's search direction): the first and last owned planes to
+    // the neighbours, on sc, handed the data by event e and recording EV_THD when done
+    auto halo = [&](double* v, hipEvent_t e) -> mvtv_status {
+        MVTV_TRY(handoff(e, s, sc));
+        MVTV_TRY(C->begin());
+        if (rk > 0) MVTV_TRY(C->send(v + first_owned, pl, rk - 1, sc));
+        if (rk < G - 1) MVTV_TRY(C->send(v + last_owned, pl, rk + 1, sc));
+        if (rk > 0) MVTV_TRY(C->recv(v, pl, rk - 1, sc));
+        if (rk < G - 1) MVTV_TRY(C->recv(v + last_owned + pl, pl, rk + 1, sc));
+        MVTV_TRY(C->end(sc));
+        HIP_TRY(hipEventRecord(ev[EV_THD], sc));
+        return MVTV_OK;
+    };
+    auto theta_halo = [&]() -> mvtv_status { return halo(P->theta, ev[EV_TH]); };
+
+    // ---- W != I: the theta-solve (W + sigma D^T D) theta = b by PCG with the spectral preconditioner of
+    //      A0 = mean(W) I + sigma D^T D (mvtv_capi.cpp pcgs_solve, the one-GPU solve), distributed: the
+    //      operator on the owned planes after a halo of the search direction, the preconditioner as the direct
+    //      slab solve (local passes + the substructured line solves), every dot product a local sum plus one
+    //      all-reduce of 1-3 numbers, the PCG scalars on the device (identical on every rank, so every rank
+    //      enqueues the same iterations and collectives). Host-synchronous per ADMM iteration: sigma, rho
+    //      and the polls of the PCG come from the (identical) control block
+    const double pcg_rtol = opts->pcg_rtol > 0 ? opts->pcg_rtol : 1e-10;
+    const int pcg_maxit = opts->pcg_max_iter > 0 ? opts->pcg_max_iter : 20000;
+    int pcg_total = 0, pcg_most = 0, pcg_unconv = 0, pcg_hint = 0;
+    double cmean = 0.0;   // mean over the global mesh of D^T D's diagonal (pcgs_solve's dbar)
+    for (int S = 1; S < (1 << p); ++S) {
+        double prod = P->g.cS[S];
+        for (int j = 0; j < p; ++j) {
+            const double mj = j == p - 1 ? double(sg.mg) : double(P->g.m[j]);
+            if ((S >> j) & 1) prod *= 2.0 * (mj - 1.0) / mj;
+        }
+        cmean += prod;
+    }
+    if (wd) {
+        if (!P->p2) MVTV_TRY(alloc(&P->p2, nodes));
+        if (!P->pcg_b) MVTV_TRY(alloc(&P->pcg_b, nodes));
+        if (!P->pcg_s) MVTV_TRY(alloc(&P->pcg_s, nodes));
+        if (!P->pcg_t) MVTV_TRY(alloc(&P->pcg_t, nodes));
+    }
+    // z = M0^-1 v on the owned planes (v and z offset to the first owned node)
+    auto precond = [&](const double* v, double* z, double sigma, const int32_t* skip) -> mvtv_status {
+        for (int d = 0; d <= p - 2; ++d)
+            HIP_TRY(launch_dct_pass(P->spec, og, s, 0, d, d == 0 ? v : z, nullptr, 0.0, nullptr, 0.0, z, sigma, w0,
+                                    nullptr, 0, 0.0, skip));
+        if (solo) {
+            HIP_TRY(launch_dct_pass(P->spec, og, s, 2, p - 1, z, nullptr, 0.0, nullptr, 0.0, z, sigma, w0, nullptr, 0,
+                                    1.0 / (double(sg.lines) * double(sg.mg)), skip));
+        } else {
+            HIP_TRY(launch_tri_slab(P->spec, og, s, 1, z, co_send, nullptr, uint32_t(ch), rk > 0, rk < G - 1, scale,
+                                    nullptr, sigma, w0, skip));
+            MVTV_TRY(handoff(ev[EV_CO], s, sc));
+            MVTV_TRY(a2a(co_send, co_recv, 6));
+            MVTV_TRY(handoff(ev[EV_COD], sc, s));
+            HIP_TRY(launch_tri_iface(s, co_recv, lr_send, uint32_t(ch), G, nullptr, skip));
+            MVTV_TRY(handoff(ev[EV_LR], s, sc));
+            MVTV_TRY(a2a(lr_send, lr_recv, 2));
+            MVTV_TRY(handoff(ev[EV_LRD], sc, s));
+            HIP_TRY(launch_tri_slab(P->spec, og, s, 3, z, nullptr, lr_recv, uint32_t(ch), rk > 0, rk < G - 1, scale,
+                                    nullptr, sigma, w0, skip));
+        }
+        for (int d = p - 2; d >= 0; --d)
+            HIP_TRY(launch_dct_pass(P->spec, og, s, 1, d, z, nullptr, 0.0, nullptr, 0.0, z, sigma, w0, nullptr, 0, 0.0,
+                                    skip));
+        return MVTV_OK;
+    };
+    // the global sum of nr per-workgroup partial rows, then k_finalize's PCG step `op` on it
+    double* pred = P->red + 8;
+    auto global_step = [&](int nparts, int nr, int op, double rtol2, int maxit) -> mvtv_status {
+        HIP_TRY(launch_finalize(s, P->partials, nparts, nr, 0, 0, pred, P->st));
+        if (!solo) {
+            MVTV_TRY(handoff(ev[EV_RED], s, sc));
+            MVTV_TRY(C->allreduce_sum(pred, size_t(nr), sc));
+            MVTV_TRY(handoff(ev[EV_AR], sc, s));
+        }
+        HIP_TRY(launch_finalize(s, pred, 1, nr, 0, op, nullptr, P->st, rtol2, maxit));
+        return MVTV_OK;
+    };
+    auto pcg_theta = [&](const double* gp) -> mvtv_status {
+        const double sigma = c.sigma, rho = c.rho, cprev = c.c_prev;
+        const Launch L{s, P->grid};
+        Geom vg = og;   // the owned nodes as one vector
+        const size_t off = sg.off;
+        double *x = P->theta, *r = P->r, *z = P->q, *pv = P->p, *q = P->p2, *b = P->pcg_b;
+        const double dbar = w0 + sigma * cmean;
+        const bool scaled = wstd >= 0.1 * dbar;
+        double* sinv = scaled ? P->pcg_s : nullptr;
+        double* t = scaled ? P->pcg_t : nullptr;
+        auto o = [&](double* v) { return v ? v + off : nullptr; };
+        if (scaled) HIP_TRY(launch_pcgs_sinv(P->g, L, sigma, W_DIAG, P->wdiag, dbar, sinv));
+        double* rin = scaled ? t : r;
+        int h = P->tstart(MVTV_K_PCG_INIT);
+        HIP_TRY(launch_apply_A(P->g, L, sigma, W_DIAG, P->wdiag, x, q, nullptr, nullptr));   // owned planes of A x
+        P->tstop(h);
+        HIP_TRY(launch_pcgs_vec(vg, L, 0, P->oty + off, P->ga + off, rho, gp + off, rho * cprev, x + off, r + off,
+                                pv + off, q + off, nullptr, b + off, o(sinv), o(t), P->st, nullptr, 0));
+        MVTV_TRY(precond(rin + off, z + off, sigma, nullptr));
+        HIP_TRY(launch_pcgs_vec(vg, L, 2, nullptr, nullptr, 0.0, nullptr, 0.0, x + off, r + off, pv + off, q + off,
+                                z + off, b + off, o(sinv), nullptr, P->st, P->partials, 1));
+        MVTV_TRY(global_step(L.grid, PR_N, 1, pcg_rtol * pcg_rtol, pcg_maxit));
+        HIP_TRY(hipMemcpyAsync(pv + off, z + off, size_t(og.N) * sizeof(double), hipMemcpyDeviceToDevice, s));
+        const int32_t* skip = &P->st->done;
+        auto iteration = [&]() -> mvtv_status {
+            if (!solo) {   // the search direction's ghost planes
+                MVTV_TRY(halo(pv, ev[EV_EDGE]));
+                HIP_TRY(hipStreamWaitEvent(s, ev[EV_THD], 0));
+            }
+            int hh = P->tstart(MVTV_K_PCG_APPLY);
+            HIP_TRY(launch_apply_A(P->g, L, sigma, W_DIAG, P->wdiag, pv, q, P->partials, P->st));   // q = A p, p.q
+            P->tstop(hh);
+            MVTV_TRY(global_step(L.grid, 1, 2, 0.0, 0));                                           // alpha
+            HIP_TRY(launch_pcgs_vec(vg, L, 1, nullptr, nullptr, 0.0, nullptr, 0.0, x + off, r + off, pv + off, q + off,
+                                    nullptr, b + off, o(sinv), o(t), P->st, nullptr, 0));
+            MVTV_TRY(precond(rin + off, z + off, sigma, skip));                                   // z = M^-1 r
+            HIP_TRY(launch_pcgs_vec(vg, L, 2, nullptr, nullptr, 0.0, nullptr, 0.0, x + off, r + off, pv + off, q + off,
+                                    z + off, b + off, o(sinv), nullptr, P->st, P->partials, 0));
+            MVTV_TRY(global_step(L.grid, PR_N, 3, 0.0, 0));                                        // beta, done
+            HIP_TRY(launch_pcgs_vec(vg, L, 3, nullptr, nullptr, 0.0, nullptr, 0.0, x + off, r + off, pv + off, q + off,
+                                    z + off, b + off, nullptr, nullptr, P->st, nullptr, 0));
+            return MVTV_OK;
+        };
+        // polls as pcgs_solve: the last solve's count first, then every 2 iterations. The state is identical on
+        // every rank, so every rank enqueues the same iterations
+        int enq_pcg = 0, batch = pcg_hint > 0 ? std::max(2, pcg_hint) : kPcgPoll;
+        for (;;) {
+            for (int k = 0; k < batch && enq_pcg < pcg_maxit; ++k, ++enq_pcg) MVTV_TRY(iteration());
+            HIP_TRY(hipMemcpyAsync(P->host_st, P->st, sizeof(PcgState), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (P->host_st->done || enq_pcg >= pcg_maxit) break;
+            batch = 2;
+        }
+        const int pit = P->host_st->iter;
+        pcg_hint = pit;
+        pcg_total += pit;
+        pcg_most = std::max(pcg_most, pit);
+        const double relres = P->host_st->bnorm2 > 0 ? std::sqrt(P->host_st->rnorm2 / P->host_st->bnorm2) : 0.0;
+        if (pit >= pcg_maxit && !(relres <= pcg_rtol)) {
+            pcg_unconv += 1;
+            if (opts->pcg_strict) return fail(MVTV_PCG_NOT_CONVERGED, "PCG hit pcg_max_iter");
+        }
+        if (!solo) {
+            MVTV_TRY(theta_halo());
+            HIP_TRY(hipStreamWaitEvent(s, ev[EV_THD], 0));
+        }
+        return MVTV_OK;
+    };
+
     auto enqueue = [&](int j) -> mvtv_status {
         const int um = j == 0 ? U_EXPLICIT : U_FROM_Z;
         double* gp = gbuf[j & 1];
         double* gn = gbuf[(j + 1) & 1];
         double* zo = ebuf[j & 1];
         double* zn = ebuf[(j + 1) & 1];
-        // -- theta-solve: forward passes along dims 0..p-2 on the owned planes, in place
-        for (int d = 0; d <= p - 2; ++d) {
-            const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
-            if (d == 0)
-                HIP_TRY(launch_dct_pass(P->spec, og, s, 0, 0, P->oty + sg.off, P->ga + sg.off, 0.0, gp + sg.off, 0.0,
-                                        th, 0.0, 1.0, P->ctl));
-            else
-                HIP_TRY(launch_dct_pass(P->spec, og, s, 0, d, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl));
-            P->tstop(h);
-        }
-        // -- the line solves along dim p-1
-        if (solo) {   // the whole lines are here: the single-GPU pass (tridiagonal solve or DCT / divide / inverse)
-            const int h = P->tstart(MVTV_K_DCT);
-            HIP_TRY(launch_dct_pass(P->spec, og, s, 2, p - 1, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl, 0,
-                                    1.0 / (double(sg.lines) * double(sg.mg))));
-            P->tstop(h);
+        if (wd) {
+            MVTV_TRY(pcg_theta(gp));
         } else {
-            int h = P->tstart(MVTV_K_DCT);
-            HIP_TRY(launch_tri_slab(P->spec, og, s, 1, th, co_send, nullptr, uint32_t(ch), rk > 0, rk < G - 1, scale,
-                                    P->ctl));
-            P->tstop(h);
-            MVTV_TRY(handoff(ev[EV_CO], s, sc));
-            MVTV_TRY(a2a(co_send, co_recv, 6));
-            MVTV_TRY(handoff(ev[EV_COD], sc, s));
-            HIP_TRY(launch_tri_iface(s, co_recv, lr_send, uint32_t(ch), G, P->ctl));
-            MVTV_TRY(handoff(ev[EV_LR], s, sc));
-            MVTV_TRY(a2a(lr_send, lr_recv, 2));
-            MVTV_TRY(handoff(ev[EV_LRD], sc, s));
-            h = P->tstart(MVTV_K_DCT);
-            HIP_TRY(launch_tri_slab(P->spec, og, s, 3, th, nullptr, lr_recv, uint32_t(ch), rk > 0, rk < G - 1, scale,
-                                    P->ctl));
-            P->tstop(h);
-        }
-        // -- theta halo (both ghost planes) on sc, started as soon as the planes it sends are final
-        auto theta_halo = [&]() -> mvtv_status {
-            MVTV_TRY(handoff(ev[EV_TH], s, sc));
-            MVTV_TRY(C->begin());
-            if (rk > 0) MVTV_TRY(C->send(P->theta + first_owned, pl, rk - 1, sc));
-            if (rk < G - 1) MVTV_TRY(C->send(P->theta + last_owned, pl, rk + 1, sc));
-            if (rk > 0) MVTV_TRY(C->recv(P->theta, pl, rk - 1, sc));
-            if (rk < G - 1) MVTV_TRY(C->recv(P->theta + last_owned + pl, pl, rk + 1, sc));
-            MVTV_TRY(C->end(sc));
-            HIP_TRY(hipEventRecord(ev[EV_THD], sc));
-            return MVTV_OK;
-        };
-        // -- inverse passes along dims p-2..0, in place. The last one (dim 0) works plane by plane, so it
-        //    transforms the first and last owned planes first and the halo carrying them overlaps the interior
-        for (int d = p - 2; d >= 0; --d) {
-            if (d == 0 && !solo && sg.nz >= 3) {
-                Geom one = og, mid = og;
-                one.m[p - 1] = 1;
-                one.N = sg.plane;
-                one.iend = one.N;
-                mid.m[p - 1] = sg.nz - 2;
-                mid.N = sg.plane * (sg.nz - 2);
-                mid.iend = mid.N;
-                double* edge_planes[2] = {th, th + size_t(sg.nz - 1) * pl};
-                for (double* ep : edge_planes) {
-                    const int h = P->tstart(MVTV_K_DCT);
-                    HIP_TRY(launch_dct_pass(P->spec, one, s, 1, 0, ep, nullptr, 0.0, nullptr, 0.0, ep, 0.0, 1.0, P->ctl));
-                    P->tstop(h);
-                }
-                MVTV_TRY(theta_halo());
+            // -- theta-solve: forward passes along dims 0..p-2 on the owned planes, in place
+            for (int d = 0; d <= p - 2; ++d) {
+                const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
+                if (d == 0)
+                    HIP_TRY(launch_dct_pass(P->spec, og, s, 0, 0, P->oty + sg.off, P->ga + sg.off, 0.0, gp + sg.off, 0.0,
+                                            th, 0.0, 1.0, P->ctl));
+                else
+                    HIP_TRY(launch_dct_pass(P->spec, og, s, 0, d, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl));
+                P->tstop(h);
+            }
+            // -- the line solves along dim p-1
+            if (solo) {   // the whole lines are here: the single-GPU pass (tridiagonal solve or DCT / divide / inverse)
                 const int h = P->tstart(MVTV_K_DCT);
-                HIP_TRY(launch_dct_pass(P->spec, mid, s, 1, 0, th + pl, nullptr, 0.0, nullptr, 0.0, th + pl, 0.0, 1.0,
-                                        P->ctl));
+                HIP_TRY(launch_dct_pass(P->spec, og, s, 2, p - 1, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl, 0,
+                                        1.0 / (double(sg.lines) * double(sg.mg))));
                 P->tstop(h);
             } else {
-                const int h = P->tstart(MVTV_K_DCT);
-                HIP_TRY(launch_dct_pass(P->spec, og, s, 1, d, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl));
+                int h = P->tstart(MVTV_K_DCT);
+                HIP_TRY(launch_tri_slab(P->spec, og, s, 1, th, co_send, nullptr, uint32_t(ch), rk > 0, rk < G - 1, scale,
+                                        P->ctl));
                 P->tstop(h);
-                if (d == 0 && !solo) MVTV_TRY(theta_halo());
+                MVTV_TRY(handoff(ev[EV_CO], s, sc));
+                MVTV_TRY(a2a(co_send, co_recv, 6));
+                MVTV_TRY(handoff(ev[EV_COD], sc, s));
+                HIP_TRY(launch_tri_iface(s, co_recv, lr_send, uint32_t(ch), G, P->ctl));
+                MVTV_TRY(handoff(ev[EV_LR], s, sc));
+                MVTV_TRY(a2a(lr_send, lr_recv, 2));
+                MVTV_TRY(handoff(ev[EV_LRD], sc, s));
+                h = P->tstart(MVTV_K_DCT);
+                HIP_TRY(launch_tri_slab(P->spec, og, s, 3, th, nullptr, lr_recv, uint32_t(ch), rk > 0, rk < G - 1, scale,
+                                        P->ctl));
+                P->tstop(h);
             }
+            // -- inverse passes along dims p-2..0, in place. The last one (dim 0) works plane by plane, so it
+            //    transforms the first and last owned planes first and the halo carrying them overlaps the interior
+            for (int d = p - 2; d >= 0; --d) {
+                if (d == 0 && !solo && sg.nz >= 3) {
+                    Geom one = og, mid = og;
+                    one.m[p - 1] = 1;
+                    one.N = sg.plane;
+                    one.iend = one.N;
+                    mid.m[p - 1] = sg.nz - 2;
+                    mid.N = sg.plane * (sg.nz - 2);
+                    mid.iend = mid.N;
+                    double* edge_planes[2] = {th, th + size_t(sg.nz - 1) * pl};
+                    for (double* ep : edge_planes) {
+                        const int h = P->tstart(MVTV_K_DCT);
+                        HIP_TRY(launch_dct_pass(P->spec, one, s, 1, 0, ep, nullptr, 0.0, nullptr, 0.0, ep, 0.0, 1.0, P->ctl));
+                        P->tstop(h);
+                    }
+                    MVTV_TRY(theta_halo());
+                    const int h = P->tstart(MVTV_K_DCT);
+                    HIP_TRY(launch_dct_pass(P->spec, mid, s, 1, 0, th + pl, nullptr, 0.0, nullptr, 0.0, th + pl, 0.0, 1.0,
+                                            P->ctl));
+                    P->tstop(h);
+                } else {
+                    const int h = P->tstart(MVTV_K_DCT);
+                    HIP_TRY(launch_dct_pass(P->spec, og, s, 1, d, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl));
+                    P->tstop(h);
+                    if (d == 0 && !solo) MVTV_TRY(theta_halo());
+                }
+            }
+            if (!solo) HIP_TRY(hipStreamWaitEvent(s, ev[EV_THD], 0));
         }
-        if (!solo) HIP_TRY(hipStreamWaitEvent(s, ev[EV_THD], 0));
         // -- edge update + gather on the owned planes, partial sums into P->red
         if (fused) {
             if (zh_pending) HIP_TRY(hipStreamWaitEvent(s, ev[EV_ZH], 0));   // z_old's ghost plane is in place
@@ -737,7 +886,8 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     // every rank enqueues the same collectives. Iterations enqueued past convergence are no-ops in their
     // kernels, but their collectives still move their buffers
     const int limit = opts->fixed_iters > 0 ? opts->fixed_iters : max_counter + 1;
-    int target = opts->fixed_iters > 0 ? opts->fixed_iters : 16;
+    // (W != I: one iteration per poll, the PCG needs the control block's sigma on the host)
+    int target = wd ? 1 : (opts->fixed_iters > 0 ? opts->fixed_iters : 16);
     int enq = 0;
     std::vector<size_t> mark;
     for (;;) {
@@ -748,7 +898,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         HIP_TRY(hipMemcpyAsync(P->host_ctl, P->ctl, sizeof(AdmmCtl), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (c.done || enq >= limit) break;
-        target = enq + std::max(4, enq / 4);
+        target = wd ? enq + 1 : enq + std::max(4, enq / 4);
     }
     if (!solo) HIP_TRY(hipStreamSynchronize(sc));   // the last z halo
     const int it_done = c.it;
@@ -772,7 +922,10 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     S.s_norm = c.s_norm;
     S.eps_pri = c.eps_pri;
     S.eps_dual = c.eps_dual;
-    S.theta_solver = MVTV_SOLVER_SPECTRAL;
+    S.theta_solver = wd ? MVTV_SOLVER_PCG_SPECTRAL : MVTV_SOLVER_SPECTRAL;
+    S.pcg_iters = pcg_total;
+    S.pcg_iters_max = pcg_most;
+    S.pcg_unconverged = pcg_unconv;
     S.status = c.status ? MVTV_MAXITER : MVTV_OK;
     S.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (stats) *stats = S;

@@ -1411,6 +1411,7 @@ __global__ __launch_bounds__(1024) void k_tris(const SpecArgs a, int sl, int nse
                                                uint32_t chunk, int lo_ext, int hi_ext, double scale) {
     constexpr int TQ = tris::TQ, NS = tris::NSMAX;
     double sigma = a.sigma;
+    if (a.skip && *a.skip) return;
     if (a.ctl) {
         if (a.ctl->done) return;
         sigma = a.ctl->sigma;
@@ -1601,8 +1602,9 @@ __global__ __launch_bounds__(1024) void k_tris(const SpecArgs a, int sl, int nse
 // u_r = ga_r + de_r u_{r+1}, v_r = al_r + be_r u_{r+1} (kept in the input's first four rows), then
 // substituted back. Out [r][2][chunk]: (L, R) of rank r = (v_{r-1}, u_{r+1}).
 __global__ __launch_bounds__(256) void k_tris_iface(double* __restrict__ co, double* __restrict__ lr, uint32_t chunk,
-                                                    int G, const AdmmCtl* ctl) {
+                                                    int G, const AdmmCtl* ctl, const int32_t* skip) {
     if (ctl && ctl->done) return;
+    if (skip && *skip) return;
     const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= chunk) return;
     const size_t C = chunk;
@@ -1641,12 +1643,13 @@ static void tris_seg(uint32_t n, int* sl, int* nseg) {
 
 hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, int phase, double* x, double* coef,
                            const double* lr, uint32_t chunk, int lo_ext, int hi_ext, double scale,
-                           const AdmmCtl* ctl) {
+                           const AdmmCtl* ctl, double sigma, double w0, const int32_t* skip) {
     const int p = og.p, d = p - 1;
     SpecArgs a{};
     a.ctl = ctl;
-    a.sigma = 1.0;
-    a.w0 = 1.0;
+    a.skip = skip;
+    a.sigma = sigma;
+    a.w0 = w0;
     a.lam = sp.lam;
     for (int j = 0; j < kMaxDims; ++j) {
         a.lam_off[j] = sp.lam_off[j];
@@ -1678,9 +1681,10 @@ hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, in
     return hipGetLastError();
 }
 
-hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint32_t chunk, int G, const AdmmCtl* ctl) {
+hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint32_t chunk, int G, const AdmmCtl* ctl,
+                            const int32_t* skip) {
     if (G < 1 || chunk == 0) return hipErrorInvalidValue;
-    klaunch(k_tris_iface, dim3((chunk + 255) / 256), dim3(256), 0, s, coef_in, lr_out, chunk, G, ctl);
+    klaunch(k_tris_iface, dim3((chunk + 255) / 256), dim3(256), 0, s, coef_in, lr_out, chunk, G, ctl, skip);
     return hipGetLastError();
 }
 

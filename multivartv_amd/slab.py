@@ -131,7 +131,7 @@ class Comm:
 class _Slab(_lib.Problem):
     """A Problem created with mvtv_problem_create_slab (same wrapper, different constructor)."""
 
-    def __init__(self, m_local, oty_local, deltas, order, device, m_global, zb, ze, glo, ghi):
+    def __init__(self, m_local, oty_local, deltas, order, device, m_global, zb, ze, glo, ghi, w_local=None):
         p = len(m_local)
         self.m, self.p = [int(v) for v in m_local], p
         self.N = int(np.prod(m_local))
@@ -145,9 +145,9 @@ class _Slab(_lib.Problem):
         self.deltas = [float(v) for v in deltas]
         self.order, self.weighted, self.device = order, True, device
         self._oty = _lib._f64(oty_local, self.N)
-        self._w = None
+        self._w = None if w_local is None else _lib._f64(w_local, self.N)
         d.oty = _lib._ptr(self._oty)
-        d.wdiag = None
+        d.wdiag = None if self._w is None else _lib._ptr(self._w)
         d.device = device
         sd = SlabDesc()
         sd.m_global, sd.z_begin, sd.z_end, sd.ghost_lo, sd.ghost_hi = m_global, zb, ze, glo, ghi
@@ -159,14 +159,16 @@ class _Slab(_lib.Problem):
 
 
 class SlabADMM:
-    """Variant-B ADMM on one rank's slab of a mesh fit (W = I, p >= 2; m_j for j < p - 1 products of 2, 3, 5, 7
-    up to 4096, the last dimension any length over >= 2 ranks).
+    """Variant-B ADMM on one rank's slab of a mesh fit (p >= 2; m_j for j < p - 1 products of 2, 3, 5, 7 up to
+    4096, the last dimension any length over >= 2 ranks).
 
-    ``oty_owned``: O^T y on the owned planes (= y for lattice data). ``ymean``: the global mean of y
-    (theta_0 = mean(y), rcpp…/solvers.cpp:207). ``comm``: a :class:`Comm` (its rank / size fix the slab).
+    ``oty_owned``: O^T y on the owned planes (= y for lattice data, W y for a diagonal W). ``ymean``: theta_0
+    (the global mean of y, rcpp…/solvers.cpp:207). ``comm``: a :class:`Comm` (its rank / size fix the slab).
+    ``w_owned``: diag(W) = diag(O^T O) on the owned planes (None: W = I). With W the theta-solve is PCG with the
+    spectral preconditioner of mean(W) I + rho D^T D, distributed like the direct solve.
     """
 
-    def __init__(self, m, oty_owned, deltas, ymean, comm: Comm, device=None, order=_lib.ORDER_CPP):
+    def __init__(self, m, oty_owned, deltas, ymean, comm: Comm, device=None, order=_lib.ORDER_CPP, w_owned=None):
         self.m = [int(v) for v in m]
         p = len(self.m)
         if p < 2:
@@ -184,14 +186,20 @@ class SlabADMM:
         self.plane = int(np.prod(self.m[:-1]))
         m_local = self.m[:-1] + [self.nz + self.glo + self.ghi]
         oty_local = np.zeros(int(np.prod(m_local)))
-        oty_local[self.glo * self.plane:(self.glo + self.nz) * self.plane] = np.asarray(oty_owned, dtype=np.float64)
-        self.P = _Slab(m_local, oty_local, deltas, order, device, self.mg, self.zb, self.ze, self.glo, self.ghi)
+        own = slice(self.glo * self.plane, (self.glo + self.nz) * self.plane)
+        oty_local[own] = np.asarray(oty_owned, dtype=np.float64)
+        w_local = None
+        if w_owned is not None:   # ghost planes: never read as W (the operator is formed on owned nodes only)
+            w_local = np.ones(int(np.prod(m_local)))
+            w_local[own] = np.asarray(w_owned, dtype=np.float64)
+        self.P = _Slab(m_local, oty_local, deltas, order, device, self.mg, self.zb, self.ze, self.glo, self.ghi,
+                       w_local)
         self.ymean = float(ymean)
 
-    def run(self, lam, rho0=None, fixed_iters=0, tol=1e-4, max_counter=3000):
+    def run(self, lam, rho0=None, fixed_iters=0, tol=1e-4, max_counter=3000, pcg_rtol=None, pcg_max_iter=None):
         """admm_update B from theta_0 = mean(y), u_0 = 0, rho_0 = lambda/5 (or rho0); collective. Stats dict."""
         o = _lib.default_opts(_lib.VARIANT_RCPP, fixed_iters=int(fixed_iters), tol=float(tol),
-                              max_counter=int(max_counter))
+                              max_counter=int(max_counter), pcg_rtol=pcg_rtol, pcg_max_iter=pcg_max_iter)
         st = _lib.AdmmStats()
         r0 = lam / 5.0 if rho0 is None else float(rho0)
         s = _L().mvtv_slab_run(self.P._h, self.comm._h, _C.byref(o), float(lam), self.ymean, r0, _C.byref(st))
@@ -207,14 +215,18 @@ class SlabADMM:
         self.P.close()
 
 
-def run_local_group(m, y, deltas, lam, world, device=0, **run_kw):
+def run_local_group(m, y, deltas, lam, world, device=0, w=None, theta0=None, **run_kw):
     """Rehearse a `world`-rank decomposition of one mesh in this process (loopback transport, one host thread
-    per rank, every slab on `device`). Returns (stats of rank 0, theta assembled from the owned planes)."""
+    per rank, every slab on `device`). ``w``: diag(W) over the mesh (O^T y = w y), None for W = I; ``theta0``:
+    None for mean(y). Returns (stats of every rank, theta assembled from the owned planes)."""
     comms = Comm.local_group(world)
     b = plane_bounds(int(m[-1]), world)
     pl = int(np.prod(m[:-1]))
     y = np.asarray(y, dtype=np.float64)
-    ranks = [SlabADMM(m, y[b[r] * pl:b[r + 1] * pl], deltas, float(y.mean()), comms[r], device=device)
+    oty = y if w is None else np.asarray(w, dtype=np.float64) * y
+    t0 = float(y.mean()) if theta0 is None else float(theta0)
+    ranks = [SlabADMM(m, oty[b[r] * pl:b[r + 1] * pl], deltas, t0, comms[r], device=device,
+                      w_owned=None if w is None else np.asarray(w, dtype=np.float64)[b[r] * pl:b[r + 1] * pl])
              for r in range(world)]
     out, err = [None] * world, [None] * world
 

@@ -127,6 +127,54 @@ def test_slab_4d_16_four_ranks_vs_c_oracle():
     assert _rel(theta, th) <= 1e-9
 
 
+def _fold_mask(m, seed=3, keep=0.8):
+    """A CV fold's W: 1 on the training nodes, 0 on the held-out ones (config 4's work items)."""
+    return (np.random.default_rng(seed).random(int(np.prod(m))) < keep).astype(np.float64)
+
+
+@pytest.mark.parametrize("m,world", [([32, 32, 32], 1), ([32, 32, 32], 2), ([32, 32, 32], 4), ([64, 48], 2),
+                                     ([8, 8, 8, 16], 4), ([4, 4, 8], 4)],
+                         ids=["3d_32_w1", "3d_32_w2", "3d_32_w4", "2d_64x48_w2", "4d_8x8x8x16_w4",
+                              "3d_4x4x8_w4_small_planes"])
+@pytest.mark.parametrize("fixed", [10, 0])
+def test_slab_weighted_fold_matches_one_gpu(m, world, fixed):
+    """W != I (a CV fold mask): the theta-solve is PCG with the spectral preconditioner of mean(W) I + rho
+    D^T D, its operator applied on the owned planes after a halo of the search direction, the preconditioner
+    the distributed direct solve, every dot product one all-reduce. Against the one-GPU PCG-spectral solve
+    at pcg_rtol 1e-13: iterations and rho exact, theta 1e-8 relative (the PCG stops at different iterates
+    when the sums are ordered differently)."""
+    lam = 0.6
+    y = towers(m)
+    w = _fold_mask(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    t0 = float(y[w > 0].mean())
+    with mv.Problem(m, w * y, wdiag=w, deltas=deltas, order=mv.ORDER_CPP) as P:
+        th, _, rho, st = P.admm(lam, np.full(y.size, t0), u=np.zeros(P.E), rho=lam / 5, fixed_iters=fixed,
+                                return_u=True, theta_solver=mv.SOLVER_PCG_SPECTRAL, pcg_rtol=1e-13)
+    out, theta = slab.run_local_group(m, y, deltas, lam, world, w=w, theta0=t0, fixed_iters=fixed, pcg_rtol=1e-13)
+    for o in out:
+        assert o["iters"] == st["iters"] and o["rho"] == rho
+        assert o["theta_solver"] == mv.SOLVER_PCG_SPECTRAL and o["pcg_iters"] > 0
+    assert _rel(theta, th) <= 1e-8
+
+
+def test_slab_weighted_counts_vs_c_oracle():
+    """Scattered counts W in {0..3} (the diagonally scaled preconditioner: std W >= 0.1 of the operator's
+    mean diagonal at small rho), 2 ranks, 15 fixed iterations against the C oracle's Jacobi-PCG loop."""
+    from oracle import c_oracle
+    m, lam, world, fixed = [16, 16, 24], 0.05, 2, 15
+    y = towers(m)
+    w = np.random.default_rng(11).integers(0, 4, int(np.prod(m))).astype(np.float64)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    t0 = float((w * y).sum() / w.sum())
+    th = np.full(y.size, t0)
+    u = np.zeros(c_oracle.num_edges(m))
+    ref = c_oracle.admm_rcpp(m, w * y, lam, th, u, lam / 5.0, deltas, W=w, fixed_iters=fixed, pcg_rtol=1e-13)
+    out, theta = slab.run_local_group(m, y, deltas, lam, world, w=w, theta0=t0, fixed_iters=fixed, pcg_rtol=1e-13)
+    assert all(o["iters"] == fixed and o["rho"] == ref["rho"] for o in out)
+    assert _rel(theta, th) <= 1e-8
+
+
 @pytest.mark.parametrize("fixed", [7, 0])
 def test_rccl_single_rank(fixed):
     """The RCCL transport at world size 1 (self transfers as device copies, RCCL communicator live):
