@@ -313,6 +313,8 @@ def slab_main(a, D, comm=None):
         g_elapsed, nranks, rccl_ranks = t1 - t0, R, 0
     per = {k: dict(avg_ms=round(v["ms"] / v["launches"], 4), launches=v["launches"]) for k, v in tim.items()
            if v["launches"]}
+    # the line solves cross the ranks (substructured) unless one rank holds the whole lines
+    distributed = nranks > 1 or os.environ.get("MVTV_SLAB_DISTRIBUTED", "0") not in ("", "0")
     if D.rank != 0:
         return None
     return {
@@ -322,8 +324,10 @@ def slab_main(a, D, comm=None):
         "data": "synthetic: towers + 0.5 N(0,1) (splitmix64/Box-Muller, seed 0x4D565456), O = I",
         "config": {"workload": f"{a.dims}D {a.size}^{a.dims} fp64 mesh-TV ADMM, variant B, lambda={lam}, one mesh "
                                f"slab-decomposed along dim {a.dims - 1} over {nranks} ranks", "mesh": m,
-                   "theta_solver": "spectral (distributed: all-to-all transposes of the last dimension)",
-                   "parallelism": f"slab x{nranks} ({transport}: halo planes, all-to-all, 7-sum all-reduce)"},
+                   "theta_solver": "spectral (local transforms; the last dimension's line solves substructured "
+                                   "over the ranks)" if distributed else "spectral (one rank: the whole lines local)",
+                   "parallelism": f"slab x{nranks} ({transport}: halo planes, "
+                                  f"{'6+2 numbers per line all-to-all, ' if distributed else ''}7-sum all-reduce)"},
         "rccl_ranks": rccl_ranks, "rccl_library": slab.Comm.library() if rccl_ranks else None,
         "roofline": _roofline(tim), "kernels_rank0": per,
         "residuals": {"r_norm": st["r_norm"], "s_norm": st["s_norm"]}, "cpu_baseline": None}

@@ -198,11 +198,15 @@ mvtv_status mvtv_solve_spectral(mvtv_problem* prob, double sigma, const double* 
 /* ---- slab decomposition of one mesh over ranks (the metric at 2-8 GPUs) ---------
  * Rank r holds planes [z_begin, z_end) of the last dimension plus one ghost plane below (unless
  * z_begin = 0) and above (unless z_end = m_global); desc->m[p-1] counts owned + ghost planes and
- * desc->oty covers them (ghost values are not used). Rank r owns planes [floor(m r / G), floor(m (r+1) / G)).
- * mvtv_slab_run is the whole variant-B loop of one rank (rcpp…/solvers.cpp:110-133) with its
- * collectives on the problem's stream: all-to-all transposes of the distributed cosine-transform solve,
- * halo planes of theta and of the edge state, one 7-value all-reduce per iteration feeding the device-side
- * adapt_step / stopping decision. Supported: variant B, W = I, u0 = 0, m_j <= 4096 a product of 2, 3, 5, 7
+ * desc->oty (and desc->wdiag, if any) cover them (ghost values are not used). Rank r owns planes
+ * [floor(m r / G), floor(m (r+1) / G)). mvtv_slab_run is the whole variant-B loop of one rank
+ * (rcpp…/solvers.cpp:110-133) with its collectives on a communication stream: the substructured line solves'
+ * two all-to-alls of 6 and 2 numbers per line, halo planes of theta and of the edge state, one 7-value
+ * all-reduce per iteration feeding the device-side adapt_step / stopping decision. With W != I (desc->wdiag)
+ * the theta-solve is PCG with the spectral preconditioner of mean(W) I + sigma D^T D (opts pcg_rtol,
+ * pcg_max_iter, pcg_strict as mvtv_admm_run), distributed: a halo of the search direction per iteration and
+ * one all-reduce per dot product; the loop then polls once per ADMM iteration. Supported: variant B, W = I
+ * or diagonal, u0 = 0, m_j <= 4096 a product of 2, 3, 5, 7
  * for j < p - 1; the last dimension any length when G >= 2 (its line solves are substructured over the ranks;
  * each rank's plane count must be 1..64 segments of <= 32 rows, e.g. any count <= 64 or with a divisor in
  * 2..32 giving <= 64 segments), a 2-3-5-7 length <= 4096 when G = 1. */
