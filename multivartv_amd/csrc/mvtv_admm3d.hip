@@ -396,6 +396,7 @@ struct Fused3dArgs {
     int tiles_x, tiles_y, zchunk, nblocks, zlo, zhi;
     int tpz;          // tiles per z chunk
     int xcd;          // contiguous tile runs per XCD (MVTV_F3D_XCD=0 in a probe build: blockIdx order)
+    int fold;         // g_alpha receives s = rho (D^T alpha + D^T u), rho = ctl->rho (the next solve's b = oty + s)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -431,7 +432,7 @@ __host__ __device__ constexpr int f3a_slot(int k) {   // image slot of block k (
 template <int ORD, int UM, bool DTH, int NB>
 __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __restrict__ szr, double (&red)[7], int X0,
                                             int Yh, int z0, int z1, double t_old, double c_old, double t_new,
-                                            double c_prev) {
+                                            double c_prev, double rho_f) {
     constexpr int P = 3, NC = 8, IW = f3a::IW, IH = f3a::IH, NI = f3a_nimg<NB, ORD>();
     const Geom& g = a.g;
     const int wv = int(threadIdx.x) >> 6, ln = int(threadIdx.x) & 63;
@@ -598,7 +599,7 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
             qa_prev = na;
             qu_prev = nu;
             const uint32_t i = uint32_t(e) * pl + ixy;
-            __builtin_nontemporal_store(ga, a.g_alpha + i);
+            __builtin_nontemporal_store(a.fold ? rho_f * (ga + gu) : ga, a.g_alpha + i);
             __builtin_nontemporal_store(gu, a.g_u + i);
             const double gpc = c_prev * gp;
             const double db = gu - gpc, da = ga + gpc;
@@ -620,13 +621,14 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
 template <int ORD, int UM, bool DTH, int NB>
 __global__ __launch_bounds__(f3a::NT) void k_admm3a(const Fused3dArgs a) {
     constexpr int NT = f3a::NT, NI = f3a_nimg<NB, ORD>();
-    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new, c_prev = a.c_prev;
+    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new, c_prev = a.c_prev, rho_f = 0.0;
     if (a.ctl) {
         if (a.ctl->done) return;
         t_old = a.ctl->t_z;
         c_old = a.ctl->c_prev;
         t_new = a.ctl->t_next;
         c_prev = a.ctl->c_prev;
+        rho_f = a.ctl->rho;
     }
     __shared__ double szr[2 * NI * f3a::IH * f3a::IW];
     double red[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -636,7 +638,8 @@ __global__ __launch_bounds__(f3a::NT) void k_admm3a(const Fused3dArgs a) {
         const int tz = bid / a.tpz, rem = bid - tz * a.tpz;
         const int z0 = a.zlo + tz * a.zchunk, z1 = min(a.zhi, z0 + a.zchunk);
         const int tyi = rem / a.tiles_x, txi = rem - tyi * a.tiles_x;
-        admm3a_tile<ORD, UM, DTH, NB>(a, szr, red, txi * 64, tyi * f3a::TY - 1, z0, z1, t_old, c_old, t_new, c_prev);
+        admm3a_tile<ORD, UM, DTH, NB>(a, szr, red, txi * 64, tyi * f3a::TY - 1, z0, z1, t_old, c_old, t_new, c_prev,
+                                      rho_f);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -741,7 +744,8 @@ bool fused3d_ok(const Geom& g) {
 hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
                          double* z_new, double t_old, double c_old, double t_new, double c_prev,
                          const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
-                         double* partials, int* nparts, const AdmmCtl* ctl) {
+                         double* partials, int* nparts, const AdmmCtl* ctl, bool fold) {
+    if (fold && (g.p != 3 || !ctl)) return hipErrorInvalidValue;   // the folded b: 3-D asynchronous loop only
     if (g.p == 2)
         return launch_admm2d(g, order, umode, s, theta, z_old, z_new, t_old, c_old, t_new, c_prev, theta_old, g_alpha,
                              g_u, g_uprev, partials, nparts, ctl);
@@ -759,6 +763,7 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
     a.t_new = t_new;
     a.c_prev = c_prev;
     a.ctl = ctl;
+    a.fold = fold ? 1 : 0;
     const int grid = (a.nblocks + 7) / 8 * 8;
     *nparts = grid;
     const bool dth = theta_old != nullptr;

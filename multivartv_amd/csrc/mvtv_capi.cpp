@@ -336,9 +336,11 @@ mvtv_status spectral_plan(mvtv_problem* P) {
 
 // Direct solve (I + sigma D^T D) x = oty + ca*ga + cb*gb: forward DCT along dims 0..p-2, the
 // last dim's forward/divide/inverse in one pass, inverse DCT along dims p-2..0. All in place on x.
+// fold: b = oty + fold_ka ga + fold_kb gb from the control block (ga = the fused kernel's folded
+// s = rho (D^T alpha + D^T u), gb = D^T u)
 mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, const double* ga, double ca,
                            const double* gb, double cb, double* x, const AdmmCtl* ctl = nullptr, double w0 = 1.0,
-                           const int32_t* skip = nullptr) {
+                           const int32_t* skip = nullptr, bool fold = false) {
     // pass order: forward along dims order[0..p-2], forward/divide/inverse along order[p-1], inverse
     // back; the MID dimension defaults to p-1 (MVTV_DCT_MID selects another one for experiments)
     const int p = P->g.p;
@@ -356,7 +358,10 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
         const bool first = t == 0;
         const int mode = t == p - 1 ? 2 : 0;
         const int h = P->tstart(first ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
-        if (first && ga)   // b = oty + ca*ga + cb*gb formed on load
+        if (first && ga && fold)   // b = oty + fold_ka s + fold_kb g_u formed on load (g_u read after a rho change)
+            HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, oty, ga, 1.0, gb, 0.0, x, sigma, w0, ctl, 0, 0.0,
+                                    skip, nullptr, true));
+        else if (first && ga)   // b = oty + ca*ga + cb*gb formed on load
             HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, oty, ga, ca, gb ? gb : ga, gb ? cb : 0.0, x,
                                     sigma, w0, ctl, 0, 0.0, skip));
         else
@@ -949,6 +954,13 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         HIP_TRY(hipMemcpyAsync(P->ctl, &c, sizeof(AdmmCtl), hipMemcpyHostToDevice, P->stream));
         double* gbuf[2] = {P->guprev, P->gu};
         double* ebuf[3] = {P->edges, P->edges2, P->edges3};
+        // FOLD (variant B): the fused 3-D kernel stores s = rho (D^T alpha + D^T u) in P->ga instead of D^T alpha, so
+        // the next solve's first pass reads oty and s (2N words) instead of oty, D^T alpha and D^T u (3N); after a
+        // control step that changed rho it forms oty + (rho'/rho) s + rho' (c - 1) D^T u (AdmmCtl::fold_ka / _kb)
+        const uint32_t m0 = P->g.m[0];
+        const bool fold = fused && variant == MVTV_VARIANT_RCPP && P->g.p == 3 && m0 >= 8 && m0 <= 4096 &&
+                          (m0 & (m0 - 1)) == 0 &&
+                          !probe_env("MVTV_FOLD_OFF") && !probe_env("MVTV_DCT_LDS") && !probe_env("MVTV_DCT_MID");
         auto enqueue = [&](int j) -> mvtv_status {
             double* gp = gbuf[j & 1];
             double* gn = gbuf[(j + 1) & 1];
@@ -956,13 +968,14 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
             if (track_theta)
                 HIP_TRY(hipMemcpyAsync(P->thold, P->theta, size_t(P->g.N) * sizeof(double), hipMemcpyDeviceToDevice,
                                        P->stream));
-            MVTV_TRY(spectral_solve(P, sigma, P->oty, P->ga, rho, gp, rho, P->theta, P->ctl));
+            MVTV_TRY(spectral_solve(P, sigma, P->oty, P->ga, rho, gp, rho, P->theta, P->ctl, 1.0, nullptr,
+                                    fold && j > 0));
             if (fused) {   // z ping-pongs between the two edge buffers
                 int hh = P->tstart(MVTV_K_ADMM_FUSED);
                 int npf = 0;
                 HIP_TRY(launch_admm3d(P->g, P->order, um, P->stream, P->theta, ebuf[j % nbuf], ebuf[(j + 1) % nbuf], 0.0, 1.0,
                                       0.0, 1.0, track_theta ? P->thold : nullptr, P->ga, gn, gp, P->partials, &npf,
-                                      P->ctl));
+                                      P->ctl, fold));
                 P->tstop(hh);
                 hh = P->tstart(MVTV_K_REDUCE);
                 HIP_TRY(launch_finalize(P->stream, P->partials, npf, ER_N + GR_N, -(1 << ER_DTH), 0, P->red, P->st, 0.0,

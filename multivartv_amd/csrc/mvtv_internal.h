@@ -128,6 +128,12 @@ struct AdmmCtl {
     double lambda, tol, sqrtN, sqrtE;
     double rho, sigma, c_prev, t_z, t_next;   // t_z: threshold z was formed with; t_next = lambda / rho
     double r_norm, s_norm, eps_pri, eps_dual, dtheta, dual_norm, primal_norm;
+    // folded right-hand side (variant B, fused 3-D kernel): the kernel of an iteration stores s = rho (g_alpha + g_u)
+    // with the rho it ran at, beside g_u. b = oty + rho' g_alpha + rho' c g_u of the next solve is then
+    // oty + fold_ka s + fold_kb g_u, fold_ka = rho' / rho, fold_kb = rho' (c - 1): oty + s unless the control step
+    // changed rho (fix != 0, the first pass also reads g_u)
+    double fold_ka, fold_kb;
+    int32_t fix, pad2;
 };
 
 enum UMode { U_EXPLICIT = 0, U_FROM_Z = 1 };
@@ -266,7 +272,7 @@ bool dct_radix_plan(uint32_t m, int* rad, int* nrad);
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
                            double w0, const AdmmCtl* ctl = nullptr, uint32_t q_off = 0, double inv_n = 0.0,
-                           const int32_t* skip = nullptr, const PcgFuse* pf = nullptr);
+                           const int32_t* skip = nullptr, const PcgFuse* pf = nullptr, bool fold = false);
 // Slab-decomposed last-dimension solve by substructuring (mvtv_spectral.hip, k_tris): og = the owned planes
 // (m[p-1] = their count, stride[p-1] = plane lines). phase 1: per line the first / last rows of G, H, K of
 // the local block into coef [chunk s][6][line in chunk]; phase 3: x = scale * (local solve with the
@@ -287,7 +293,7 @@ bool fused3d_ok(const Geom& g);
 hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
                          double* z_new, double t_old, double c_old, double t_new, double c_prev,
                          const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
-                         double* partials, int* nparts, const AdmmCtl* ctl = nullptr);
+                         double* partials, int* nparts, const AdmmCtl* ctl = nullptr, bool fold = false);
 hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
                          double t_old, double c_old, double t_new, const double* theta_old, double* partials,
                          int* nparts, const AdmmCtl* ctl = nullptr);

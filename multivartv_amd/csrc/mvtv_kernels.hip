@@ -384,6 +384,10 @@ __device__ __forceinline__ void admm_control_step(AdmmCtl* __restrict__ c, const
         c->dtheta = R[ER_DTH];
     }
     c->r_norm = r_norm;
+    // b_next = oty + rho_next D^T alpha + rho_next c_next D^T u from the folded s = rho (D^T alpha + D^T u) and D^T u
+    c->fix = (rho_next != rho || c_next != 1.0) ? 1 : 0;
+    c->fold_ka = c->fix ? rho_next / rho : 1.0;
+    c->fold_kb = c->fix ? rho_next * (c_next - 1.0) : 0.0;
     c->c_prev = c_next;
     c->rho = rho_next;
     if (c->variant == 0) c->sigma = rho_next;

@@ -77,6 +77,7 @@ struct SpecArgs {
     const uint32_t* perm;     // position of sample k in the digit-reversed Makhoul order (this dim)
     int32_t xcd;              // k_dct8: tiles dealt to the XCDs in contiguous runs (grid a multiple of 8)
     PcgFuse pf;               // k_dct8 PC = 1 / 2: the PCG vector work of the preconditioner's d = 0 passes
+    int32_t fold;             // FORMB from the folded s (k_dct8, ctl): b = in + fold_ka ga [+ fold_kb gb if ctl->fix]
 };
 
 enum SpecMode { SPEC_FWD = 0, SPEC_INV = 1, SPEC_MID = 2 };
@@ -502,11 +503,17 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
     if (a.skip && *a.skip) return;
     const double alpha = PC == 1 ? a.pf.st->alpha : 0.0;
     double rz = 0.0, rr = 0.0;   // PC 2 reductions
+    bool rd_gb = true;   // FORMB reads gb (the folded form only after a rho change)
     if (a.ctl) {
         if (a.ctl->done) return;
         sigma = a.ctl->sigma;
         ca = a.ctl->rho;
         cb = a.ctl->rho * a.ctl->c_prev;
+        if (a.fold) {
+            ca = a.ctl->fold_ka;
+            cb = a.ctl->fold_kb;
+            rd_gb = a.ctl->fix != 0;
+        }
     }
     constexpr int M = S::M, TPL = S::TPL, NCL = S::NCL;
     __shared__ double2 buf[NCL * S::LP];
@@ -562,17 +569,23 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
             if (va) {
                 const uint32_t g = gaddr(la, k);
                 v.x = __builtin_nontemporal_load(a.in + g);
-                if (FORMB) v.x += ca * __builtin_nontemporal_load(a.ga + g) + cb * __builtin_nontemporal_load(a.gb + g);
+                if (FORMB && !rd_gb) v.x += ca * __builtin_nontemporal_load(a.ga + g);
+                else if (FORMB) v.x += ca * __builtin_nontemporal_load(a.ga + g) + cb * __builtin_nontemporal_load(a.gb + g);
             }
             if (vb) {
                 const uint32_t g = gaddr(lb, k);
                 v.y = __builtin_nontemporal_load(a.in + g);
-                if (FORMB) v.y += ca * __builtin_nontemporal_load(a.ga + g) + cb * __builtin_nontemporal_load(a.gb + g);
+                if (FORMB && !rd_gb) v.y += ca * __builtin_nontemporal_load(a.ga + g);
+                else if (FORMB) v.y += ca * __builtin_nontemporal_load(a.ga + g) + cb * __builtin_nontemporal_load(a.gb + g);
             }
         } else if (va) {   // d > 0: lines la, lb are adjacent words (vb == va)
             const uint32_t g = gaddr(la, k);
             v = ldnt2(a.in + g);
-            if (FORMB) {
+            if (FORMB && !rd_gb) {
+                const double2 x1 = ldnt2(a.ga + g);
+                v.x += ca * x1.x;
+                v.y += ca * x1.y;
+            } else if (FORMB) {
                 const double2 x1 = ldnt2(a.ga + g);
                 const double2 x2 = ldnt2(a.gb + g);
                 v.x += ca * x1.x + cb * x2.x;
@@ -620,7 +633,11 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
                         return rv;
                     } else {
                         double2 v = ldnt2(a.in + g);
-                        if (FORMB) {
+                        if (FORMB && !rd_gb) {
+                            const double2 g1 = ldnt2(a.ga + g);
+                            v.x += ca * g1.x;
+                            v.y += ca * g1.y;
+                        } else if (FORMB) {
                             const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
                             v.x += ca * g1.x + cb * g2.x;
                             v.y += ca * g1.y + cb * g2.y;
@@ -1890,7 +1907,7 @@ bool dct_pcg_fusable(const Geom& g, size_t partial_words) {
 hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, int d, const double* in,
                            const double* ga, double ca, const double* gb, double cb, double* out, double sigma,
                            double w0, const AdmmCtl* ctl, uint32_t q_off, double inv_n, const int32_t* skip,
-                           const PcgFuse* pf) {
+                           const PcgFuse* pf, bool fold) {
     SpecArgs a{};
     a.ctl = ctl;
     a.skip = skip;
@@ -1923,7 +1940,11 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     a.L = 0;
     while ((1u << a.L) < m) ++a.L;
     const bool formb = ga != nullptr;
+    a.fold = fold ? 1 : 0;   // b from the folded s: k_dct8 (power-of-two m >= 8), asynchronous loop only
     if (m > 4096) return hipErrorInvalidValue;
+    if (a.fold && (!formb || !gb || !ctl || (1u << a.L) != m || (1u << a.ls) != a.stride || a.L < 3 ||
+                   probe_env("MVTV_DCT_LDS") || mode == SPEC_MID))
+        return hipErrorInvalidValue;
     if (pf && pf->mode) {   // PCG-fused d = 0 pass (dct_pcg_fusable meshes): k_dct8 only
         if (d != 0 || formb || (1u << a.L) != m || a.L < 6 || mode != (pf->mode == 1 ? SPEC_FWD : SPEC_INV) ||
             (pf->mode == 2 && !pf->nparts))

@@ -30,3 +30,27 @@ def test_fused_ragged_dim0_matches_oracle(m, iters):
     assert rho == rs["rho"]
     assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
     assert np.max(np.abs(u - ref_u)) <= 1e-9 * max(1.0, np.max(np.abs(ref_u)))
+
+
+@pytest.mark.parametrize("m,lam", [([32, 32, 32], 1.0), ([32, 32, 32], 0.02), ([64, 64, 64], 1.0), ([128, 128, 128], 0.1)],
+                         ids=["m32_lam1", "m32_lam002", "m64_lam1", "m128_lam01"])
+def test_folded_rhs_converged_matches_oracle(m, lam):
+    """The asynchronous spectral loop on a power-of-two m0 stores the folded s = rho (D^T alpha + D^T u) for the
+    next solve's b = oty + s, and after a residual-balancing step that changed rho (7 doublings over these runs)
+    forms b = oty + (rho'/rho) s + rho' (c - 1) D^T u. Converged runs against the C oracle's loop with the exact
+    DCT solve (rcpp…/solvers.cpp:110-133): iterations and rho exactly, theta to 1e-9."""
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    th0 = np.full(y.size, y.mean())
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        th, u, rho, st = P.admm(lam, th0, u=np.zeros(P.E), rho=lam / 5)
+        E = P.E
+    assert st["theta_solver"] == mv.SOLVER_SPECTRAL
+    ref_th = th0.copy()
+    ref_u = np.zeros(E)
+    rs = c_oracle.admm_rcpp_spectral(m, y, lam, ref_th, ref_u, lam / 5, deltas)
+    assert rs["rho"] != lam / 5   # the run adapted rho, so the fix-up path ran
+    assert st["iters"] == rs["iters"]
+    assert rho == rs["rho"]
+    assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
+    assert np.max(np.abs(u - ref_u)) <= 1e-9 * max(1.0, np.max(np.abs(ref_u)))
