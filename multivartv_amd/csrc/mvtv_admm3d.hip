@@ -732,7 +732,7 @@ bool fused2d_ok(const Geom& g);
 hipError_t launch_admm2d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
                          double* z_new, double t_old, double c_old, double t_new, double c_prev,
                          const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
-                         double* partials, int* nparts, const AdmmCtl* ctl);
+                         double* partials, int* nparts, const AdmmCtl* ctl, bool fold);
 
 bool fused3d_ok(const Geom& g) {
     if (g.p == 2) return fused2d_ok(g);
@@ -745,10 +745,10 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
                          double* z_new, double t_old, double c_old, double t_new, double c_prev,
                          const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
                          double* partials, int* nparts, const AdmmCtl* ctl, bool fold) {
-    if (fold && (g.p != 3 || !ctl)) return hipErrorInvalidValue;   // the folded b: 3-D asynchronous loop only
+    if (fold && ((g.p != 2 && g.p != 3) || !ctl)) return hipErrorInvalidValue;   // the folded b: asynchronous loop
     if (g.p == 2)
         return launch_admm2d(g, order, umode, s, theta, z_old, z_new, t_old, c_old, t_new, c_prev, theta_old, g_alpha,
-                             g_u, g_uprev, partials, nparts, ctl);
+                             g_u, g_uprev, partials, nparts, ctl, fold);
     Fused3dArgs a = f3d_args(g);
     a.theta = theta;
     a.z_old = z_old;
@@ -1355,13 +1355,14 @@ template <int ORD, int UM, bool DTH, int NB>
 __global__ __launch_bounds__(f2d::NT) void k_admm2d(const Fused3dArgs a) {
     constexpr int P = 2, NC = 4;
     const Geom& g = a.g;
-    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new, c_prev = a.c_prev;
+    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new, c_prev = a.c_prev, rho_f = 0.0;
     if (a.ctl) {
         if (a.ctl->done) return;
         t_old = a.ctl->t_z;
         c_old = a.ctl->c_prev;
         t_new = a.ctl->t_next;
         c_prev = a.ctl->c_prev;
+        rho_f = a.ctl->rho;
     }
     double red[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
@@ -1486,7 +1487,7 @@ __global__ __launch_bounds__(f2d::NT) void k_admm2d(const Fused3dArgs a) {
             cu = nu;
             if (own) {
                 const uint32_t i = uint32_t(y) * uint32_t(m0) + uint32_t(xc);
-                __builtin_nontemporal_store(ga, a.g_alpha + i);
+                __builtin_nontemporal_store(a.fold ? rho_f * (ga + gu) : ga, a.g_alpha + i);
                 __builtin_nontemporal_store(gu, a.g_u + i);
                 const double gpc = c_prev * gp;
                 const double db = gu - gpc, da = ga + gpc;
@@ -1555,8 +1556,9 @@ bool fused2d_ok(const Geom& g) {
 hipError_t launch_admm2d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
                          double* z_new, double t_old, double c_old, double t_new, double c_prev,
                          const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
-                         double* partials, int* nparts, const AdmmCtl* ctl) {
+                         double* partials, int* nparts, const AdmmCtl* ctl, bool fold) {
     Fused3dArgs a = f2d_args(g);
+    a.fold = fold ? 1 : 0;
     a.theta = theta;
     a.z_old = z_old;
     a.z_new = z_new;

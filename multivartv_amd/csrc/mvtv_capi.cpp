@@ -958,7 +958,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         // the next solve's first pass reads oty and s (2N words) instead of oty, D^T alpha and D^T u (3N); after a
         // control step that changed rho it forms oty + (rho'/rho) s + rho' (c - 1) D^T u (AdmmCtl::fold_ka / _kb)
         const uint32_t m0 = P->g.m[0];
-        const bool fold = fused && variant == MVTV_VARIANT_RCPP && P->g.p == 3 && m0 >= 8 && m0 <= 4096 &&
+        const bool fold = fused && variant == MVTV_VARIANT_RCPP && (P->g.p == 2 || P->g.p == 3) && m0 >= 8 && m0 <= 4096 &&
                           (m0 & (m0 - 1)) == 0 &&
                           !probe_env("MVTV_FOLD_OFF") && !probe_env("MVTV_DCT_LDS") && !probe_env("MVTV_DCT_MID");
         auto enqueue = [&](int j) -> mvtv_status {
