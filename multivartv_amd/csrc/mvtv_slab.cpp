@@ -485,6 +485,11 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     const double tol = opts->tol > 0 ? opts->tol : 1e-4;
     const int max_counter = opts->max_counter > 0 ? opts->max_counter : 3000;
     const bool fused = P->f3d;
+    // folded right-hand side (as mvtv_capi.cpp's loop): the fused kernel stores s = rho (D^T alpha + D^T u) and the
+    // next first pass reads oty + s (oty + (rho'/rho) s + rho' (c - 1) D^T u after a rho change)
+    const uint32_t m0 = P->g.m[0];
+    const bool fold = fused && !wd && P->g.p == 3 && m0 >= 8 && m0 <= 4096 && (m0 & (m0 - 1)) == 0 &&
+                      !probe_env("MVTV_FOLD_OFF") && !probe_env("MVTV_DCT_LDS");
     // interface buffers of the distributed line solves (16 numbers per line): the 6 coefficients of this
     // rank's blocks by chunk, the chunk's coefficients from every rank, the (L, R) values by rank, and the
     // values of this rank's lines by chunk. One rank: the line solves are local, no buffers, no transfers,
@@ -761,7 +766,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
                 const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
                 if (d == 0)
                     HIP_TRY(launch_dct_pass(P->spec, og, s, 0, 0, P->oty + sg.off, P->ga + sg.off, 0.0, gp + sg.off, 0.0,
-                                            th, 0.0, 1.0, P->ctl));
+                                            th, 0.0, 1.0, P->ctl, 0, 0.0, nullptr, nullptr, fold && j > 0));
                 else
                     HIP_TRY(launch_dct_pass(P->spec, og, s, 0, d, th, nullptr, 0.0, nullptr, 0.0, th, 0.0, 1.0, P->ctl));
                 P->tstop(h);
@@ -826,7 +831,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
             int h = P->tstart(MVTV_K_ADMM_FUSED);
             int npf = 0;
             HIP_TRY(launch_admm3d(P->g, P->order, um, s, P->theta, zo, zn, 0.0, 1.0, 0.0, 1.0, nullptr, P->ga, gn, gp,
-                                  P->partials, &npf, P->ctl));
+                                  P->partials, &npf, P->ctl, fold));
             P->tstop(h);
             HIP_TRY(launch_finalize(s, P->partials, npf, ER_N + GR_N, -(1 << ER_DTH), 0, P->red, P->st, 0.0, 0, P->ctl));
         } else {

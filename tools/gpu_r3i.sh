@@ -14,8 +14,8 @@ for rep in 1 2; do
     if [ "$e" = base ]; then ev=""; else ev="$e"; fi
     for c in ${CASES:-3:512 3:256}; do
       d=${c%%:*}; n=${c##*:}
-      env $ev timeout -k 10 200 python bench.py --no-cpu --pcg-steps 0 --steps ${STEPS:-30} --warmup 5 --dims $d --size $n > gpurun_out/r3i/$n.$rep.${e%%=*}.json 2> gpurun_out/r3i/$n.$rep.${e%%=*}.err || { tail -5 gpurun_out/r3i/$n.$rep.${e%%=*}.err; exit 1; }
-      python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2],d['value'],{k:v['avg_ms'] for k,v in d['kernels'].items()})" gpurun_out/r3i/$n.$rep.${e%%=*}.json "$n $e.$rep"
+      env $ev timeout -k 10 200 python bench.py --no-cpu --pcg-steps 0 --steps ${STEPS:-30} --warmup 5 --dims $d --size $n ${BENCH_EXTRA} > gpurun_out/r3i/$n.$rep.${e%%=*}.json 2> gpurun_out/r3i/$n.$rep.${e%%=*}.err || { tail -5 gpurun_out/r3i/$n.$rep.${e%%=*}.err; exit 1; }
+      python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2],d['value'],{k:v['avg_ms'] for k,v in d.get('kernels',{}).items()})" gpurun_out/r3i/$n.$rep.${e%%=*}.json "$n $e.$rep"
     done
   done
 done
