@@ -357,7 +357,7 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
         const int d = order[t];
         const bool first = t == 0;
         const int mode = t == p - 1 ? 2 : 0;
-        const int h = P->tstart(first ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
+        const int h = P->tstart(first ? (fold ? MVTV_K_DCT_FOLD : MVTV_K_DCT_FIRST) : MVTV_K_DCT);
         if (first && ga && fold)   // b = oty + fold_ka s + fold_kb g_u formed on load (g_u read after a rho change)
             HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, mode, d, oty, ga, 1.0, gb, 0.0, x, sigma, w0, ctl, 0, 0.0,
                                     skip, nullptr, true));
@@ -1652,6 +1652,7 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
         case MVTV_K_PCG_DIRECTION: b = 8.0 * ((3.0 + w) * N); break;    // r, p (+W) in, p out
         case MVTV_K_PCG_FUSED: b = 8.0 * ((6.0 + w) * N); break;        // x, r, p (+W) in, x, r, p out
         case MVTV_K_DCT_FIRST: b = 8.0 * 4.0 * N; break;                 // oty, g_alpha, g_u in, x out
+        case MVTV_K_DCT_FOLD: b = 8.0 * 3.0 * N; break;                  // oty, s in, x out (+ g_u after a rho change)
         case MVTV_K_DCT: b = 8.0 * 2.0 * N; break;                       // x in, x out
         case MVTV_K_ADMM_FUSED: b = 8.0 * (4.0 * N + 2.0 * E); break;    // theta, z, g_uprev in; z', g_alpha, g_u out
         default: b = 0.0;
@@ -1665,7 +1666,7 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
 const char* mvtv_kernel_name(int32_t kid) {
     static const char* names[MVTV_K_COUNT] = {"edge_update", "gather_Dt", "pcg_init", "pcg_apply_A",
                                                "pcg_update", "pcg_direction", "reduce", "other", "pcg_fused3d",
-                                               "dct_first", "dct", "admm_fused", "gather4_b"};
+                                               "dct_first", "dct", "admm_fused", "gather4_b", "dct_first_fold"};
     return (kid >= 0 && kid < MVTV_K_COUNT) ? names[kid] : "?";
 }
 

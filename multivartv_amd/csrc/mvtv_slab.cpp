@@ -763,7 +763,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         } else {
             // -- theta-solve: forward passes along dims 0..p-2 on the owned planes, in place
             for (int d = 0; d <= p - 2; ++d) {
-                const int h = P->tstart(d == 0 ? MVTV_K_DCT_FIRST : MVTV_K_DCT);
+                const int h = P->tstart(d == 0 ? ((fold && j > 0) ? MVTV_K_DCT_FOLD : MVTV_K_DCT_FIRST) : MVTV_K_DCT);
                 if (d == 0)
                     HIP_TRY(launch_dct_pass(P->spec, og, s, 0, 0, P->oty + sg.off, P->ga + sg.off, 0.0, gp + sg.off, 0.0,
                                             th, 0.0, 1.0, P->ctl, 0, 0.0, nullptr, nullptr, fold && j > 0));
