@@ -272,7 +272,7 @@ hipError_t launch_gather4d(const Geom& g, int order, int umode, hipStream_t s, c
 bool gather4_ok(const Geom& g);
 hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                           double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
-                          int* nparts, const AdmmCtl* ctl, double* scratch);
+                          int* nparts, const AdmmCtl* ctl, double* scratch, bool fold);
 
 bool edge3d_ok(const Geom& g) {
     if (g.p == 4) return edge4d_ok(g);
@@ -324,11 +324,12 @@ hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, con
 
 hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                            double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
-                           int* nparts, const AdmmCtl* ctl, double* scratch4) {
+                           int* nparts, const AdmmCtl* ctl, double* scratch4, bool fold) {
+    if (fold && !(g.p == 4 && scratch4 && ctl && gather4_ok(g))) return hipErrorInvalidValue;   // two-pass 4-D only
     if (g.p == 4) {
         if (scratch4 && gather4_ok(g))
             return launch_gather4(g, order, umode, s, edges, t, g_alpha, g_u, g_uprev, c_prev, partials, nparts, ctl,
-                                  scratch4);
+                                  scratch4, fold);
         // 4-D: the marching gather (k_gather4d) reads ~65 neighbour words per cell through L1/L2 and
         // measured slower at 128^4 (20.8 vs 18.4 ms) than the grid-stride kernel; opt-in only
         static const bool marching = probe_env("MVTV_G4D") != nullptr;
@@ -1094,6 +1095,7 @@ struct Gather4Args {
     double* partials;
     double t, c_prev;
     const AdmmCtl* ctl;
+    int fold;        // pass B stores s = rho (g_alpha + g_u) in g_alpha (the folded right-hand side)
     int tiles_x, tiles_y, zchunk, nzc, nblocks, wa, wb;   // pass A: planes w in [wa, wb)
     int wlo, whi, wchunk, nwc, n3, nblocks_b;            // pass B: owned planes [wlo, whi)
 };
@@ -1211,10 +1213,11 @@ __global__ __launch_bounds__(64 * TYV) void k_gather4a(const Gather4Args a) {
 
 template <int UM, bool PREV>
 __global__ __launch_bounds__(g4::NTB) void k_gather4b(const Gather4Args a) {
-    double c_prev = a.c_prev;
+    double c_prev = a.c_prev, rho_f = 0.0;
     if (a.ctl) {
         if (a.ctl->done) return;
         c_prev = a.ctl->c_prev;
+        rho_f = a.ctl->rho;
     }
     double red[GR_N] = {0.0, 0.0, 0.0};
     const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
@@ -1241,7 +1244,7 @@ __global__ __launch_bounds__(g4::NTB) void k_gather4b(const Gather4Args a) {
             const double wu = __builtin_nontemporal_load(a.swu + i);
             const double gu = __builtin_nontemporal_load(a.s0u + i) + (wu - pu);
             pu = wu;
-            if constexpr (UM == U_FROM_Z) __builtin_nontemporal_store(ga, a.g_alpha + i);
+            if constexpr (UM == U_FROM_Z) __builtin_nontemporal_store(a.fold ? rho_f * (ga + gu) : ga, a.g_alpha + i);
             __builtin_nontemporal_store(gu, a.g_u + i);
             red[GR_GU2] = fma(gu, gu, red[GR_GU2]);
             if constexpr (PREV) {
@@ -1277,9 +1280,10 @@ static int g4_ty() {
 
 hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                           double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
-                          int* nparts, const AdmmCtl* ctl, double* scratch) {
+                          int* nparts, const AdmmCtl* ctl, double* scratch, bool fold) {
     Gather4Args a{};
     a.g = g;
+    a.fold = fold ? 1 : 0;
     a.edges = edges;
     a.s0a = scratch;
     a.s0u = scratch + size_t(g.N);

@@ -958,7 +958,9 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         // the next solve's first pass reads oty and s (2N words) instead of oty, D^T alpha and D^T u (3N); after a
         // control step that changed rho it forms oty + (rho'/rho) s + rho' (c - 1) D^T u (AdmmCtl::fold_ka / _kb)
         const uint32_t m0 = P->g.m[0];
-        const bool fold = fused && variant == MVTV_VARIANT_RCPP && (P->g.p == 2 || P->g.p == 3) && m0 >= 8 && m0 <= 4096 &&
+        const bool fold_path = fused ? (P->g.p == 2 || P->g.p == 3)
+                                     : (P->g.p == 4 && P->e3d && P->g4 != nullptr && gather4_ok(P->g));   // two-pass 4-D
+        const bool fold = fold_path && variant == MVTV_VARIANT_RCPP && m0 >= 8 && m0 <= 4096 &&
                           (m0 & (m0 - 1)) == 0 &&
                           !probe_env("MVTV_FOLD_OFF") && !probe_env("MVTV_DCT_LDS") && !probe_env("MVTV_DCT_MID");
         auto enqueue = [&](int j) -> mvtv_status {
@@ -1000,7 +1002,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
             int npg = L.grid;
             if (P->e3d)
                 HIP_TRY(launch_gather3d(P->g, P->order, U_FROM_Z, P->stream, P->edges, 0.0, P->ga, gn, gp, 1.0,
-                                        P->partials, &npg, P->ctl, P->g4));
+                                        P->partials, &npg, P->ctl, P->g4, fold));
             else
                 HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, L, P->edges, 0.0, P->ga, gn, gp, 1.0, P->partials,
                                       P->ctl));

@@ -300,7 +300,7 @@ hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, con
 // scratch4: 4 N-arrays for the two-pass 4-D gather (p = 4); nullptr selects the one-pass kernels
 hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                            double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
-                           int* nparts, const AdmmCtl* ctl = nullptr, double* scratch4 = nullptr);
+                           int* nparts, const AdmmCtl* ctl = nullptr, double* scratch4 = nullptr, bool fold = false);
 bool gather4_ok(const Geom& g);
 hipError_t launch_gather_index(hipStream_t s, const double* theta, const int64_t* idx, int64_t n, double* out);
 

@@ -488,7 +488,8 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     // folded right-hand side (as mvtv_capi.cpp's loop): the fused kernel stores s = rho (D^T alpha + D^T u) and the
     // next first pass reads oty + s (oty + (rho'/rho) s + rho' (c - 1) D^T u after a rho change)
     const uint32_t m0 = P->g.m[0];
-    const bool fold = fused && !wd && P->g.p == 3 && m0 >= 8 && m0 <= 4096 && (m0 & (m0 - 1)) == 0 &&
+    const bool fold_path = fused ? P->g.p == 3 : (P->g.p == 4 && P->e3d && P->g4 != nullptr && gather4_ok(P->g));
+    const bool fold = fold_path && !wd && m0 >= 8 && m0 <= 4096 && (m0 & (m0 - 1)) == 0 &&
                       !probe_env("MVTV_FOLD_OFF") && !probe_env("MVTV_DCT_LDS");
     // interface buffers of the distributed line solves (16 numbers per line): the 6 coefficients of this
     // rank's blocks by chunk, the chunk's coefficients from every rank, the (L, R) values by rank, and the
@@ -859,7 +860,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
             int npg = P->grid;
             if (P->e3d)
                 HIP_TRY(launch_gather3d(P->g, P->order, U_FROM_Z, s, P->edges, 0.0, P->ga, gn, gp, 1.0, P->partials,
-                                        &npg, P->ctl, P->g4));
+                                        &npg, P->ctl, P->g4, fold));
             else
                 HIP_TRY(launch_gather(P->g, P->order, U_FROM_Z, P->L(), P->edges, 0.0, P->ga, gn, gp, 1.0,
                                       P->partials, P->ctl));

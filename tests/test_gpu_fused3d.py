@@ -33,10 +33,11 @@ def test_fused_ragged_dim0_matches_oracle(m, iters):
 
 
 @pytest.mark.parametrize("m,lam", [([32, 32, 32], 1.0), ([32, 32, 32], 0.02), ([64, 64, 64], 1.0), ([128, 128, 128], 0.1),
-                                   ([128, 96], 1.0), ([1024, 1024], 0.1)],
-                         ids=["m32_lam1", "m32_lam002", "m64_lam1", "m128_lam01", "2d_128x96", "2d_1024"])
+                                   ([128, 96], 1.0), ([1024, 1024], 0.1), ([16, 16, 16, 16], 1.0), ([32, 32, 32, 32], 0.02)],
+                         ids=["m32_lam1", "m32_lam002", "m64_lam1", "m128_lam01", "2d_128x96", "2d_1024", "4d_16_lam1",
+                              "4d_32_lam002"])
 def test_folded_rhs_converged_matches_oracle(m, lam):
-    """The asynchronous spectral loop (2-D and 3-D fused kernels) on a power-of-two m0 stores the folded s = rho (D^T alpha + D^T u) for the
+    """The asynchronous spectral loop (2-D / 3-D fused kernels, 4-D two-pass gather) on a power-of-two m0 stores the folded s = rho (D^T alpha + D^T u) for the
     next solve's b = oty + s, and after a residual-balancing step that changed rho (7 doublings over these runs)
     forms b = oty + (rho'/rho) s + rho' (c - 1) D^T u. Converged runs against the C oracle's loop with the exact
     DCT solve (rcpp…/solvers.cpp:110-133): iterations and rho exactly, theta to 1e-9."""
