@@ -353,7 +353,19 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
     for (int d = 0; d < p; ++d)
         if (d != mid) order[n++] = d;
     order[n++] = mid;
-    for (int t = 0; t < p; ++t) {
+    // m0 = m1 <= 128: dims 0 and 1 in one pass each way (k_plane8: the plane stays on chip between them)
+    const bool plane = mid >= 2 && plane_pass_ok(P->g);
+    if (plane) {
+        const int h = P->tstart(ga ? (fold ? MVTV_K_DCT_FOLD : MVTV_K_DCT_FIRST) : MVTV_K_DCT);
+        if (ga && fold)
+            HIP_TRY(launch_plane_pass(P->spec, P->g, P->stream, 0, oty, ga, 1.0, gb, 0.0, x, ctl, skip, true));
+        else if (ga)
+            HIP_TRY(launch_plane_pass(P->spec, P->g, P->stream, 0, oty, ga, ca, gb, cb, x, ctl, skip));
+        else
+            HIP_TRY(launch_plane_pass(P->spec, P->g, P->stream, 0, oty, nullptr, 0.0, nullptr, 0.0, x, ctl, skip));
+        P->tstop(h);
+    }
+    for (int t = plane ? 2 : 0; t < p; ++t) {
         const int d = order[t];
         const bool first = t == 0;
         const int mode = t == p - 1 ? 2 : 0;
@@ -369,10 +381,15 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
                                     sigma, w0, ctl, 0, 0.0, skip));
         P->tstop(h);
     }
-    for (int t = p - 2; t >= 0; --t) {
+    for (int t = p - 2; t >= (plane ? 2 : 0); --t) {
         const int h = P->tstart(MVTV_K_DCT);
         HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 1, order[t], x, nullptr, 0.0, nullptr, 0.0, x, sigma, w0,
                                 ctl, 0, 0.0, skip));
+        P->tstop(h);
+    }
+    if (plane) {
+        const int h = P->tstart(MVTV_K_DCT);
+        HIP_TRY(launch_plane_pass(P->spec, P->g, P->stream, 1, x, nullptr, 0.0, nullptr, 0.0, x, ctl, skip));
         P->tstop(h);
     }
     return MVTV_OK;

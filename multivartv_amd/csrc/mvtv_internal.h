@@ -263,6 +263,14 @@ struct PcgFuse {
     size_t cap = 0;
     int* nparts = nullptr;
 };
+// the two in-plane passes (dims 0 and 1) in one launch (k_plane8): m0 = m1 a power of two in [16, 128], p >= 3,
+// >= 1024 planes
+bool plane_pass_ok(const Geom& g);
+// mode 0: forward along dims 0 then 1 (b = in + ca ga + cb gb formed on load when ga != nullptr; fold: from the
+// control block's fold_ka / fold_kb); mode 1: inverse along dims 1 then 0. In place allowed.
+hipError_t launch_plane_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, const double* in,
+                             const double* ga, double ca, const double* gb, double cb, double* out,
+                             const AdmmCtl* ctl = nullptr, const int32_t* skip = nullptr, bool fold = false);
 // true when the d = 0 passes of this mesh run in k_dct8 with their partial rows within partial_words
 bool dct_pcg_fusable(const Geom& g, size_t partial_words);
 // radices (8, 4, 2, 3, 5, 7 in stage order) of a line length m = 2^a 3^b 5^c 7^d; false for any other m

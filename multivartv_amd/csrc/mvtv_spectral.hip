@@ -464,7 +464,8 @@ __device__ __forceinline__ int stage_out_pos(int j, int i) {
 // Stages after the first (the first is peeled: its input comes from HBM or the caller's LDS).
 // STAGE counts radix-8 stages done after R0. Writes the outputs of stage NS_IN's butterflies
 // to LDS, then (if more stages remain) reads the next stage's inputs.
-template <int L, int R, int NS, bool INV, bool LAST_TO_REGS>
+// LDSB: LDS-only barriers (lds_barrier), so global loads issued before the stages stay in flight
+template <int L, int R, int NS, bool INV, bool LAST_TO_REGS, bool LDSB = false>
 __device__ __forceinline__ void stages_from(double2* z, int j, double2* X, int cx, const double2* __restrict__ tw) {
     using S = spec8::Shape<L>;
     stage_compute<L, R, NS, INV>(z, j, tw);
@@ -472,14 +473,16 @@ __device__ __forceinline__ void stages_from(double2* z, int j, double2* X, int c
     if constexpr (NS_NEXT == S::M && LAST_TO_REGS) {
         return;   // caller stores z (output positions stage_out_pos<L, R, NS>)
     } else {
-        __syncthreads();   // everyone has read this stage's inputs
+        if constexpr (LDSB) lds_barrier();   // everyone has read this stage's inputs
+        else __syncthreads();
 #pragma unroll
         for (int i = 0; i < 8; ++i) X[spec8::slot(stage_out_pos<L, R, NS>(j, i), cx)] = z[i];
-        __syncthreads();
+        if constexpr (LDSB) lds_barrier();
+        else __syncthreads();
         if constexpr (NS_NEXT < S::M) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, 8>(j, i), cx)];
-            stages_from<L, 8, NS_NEXT, INV, LAST_TO_REGS>(z, j, X, cx, tw);
+            stages_from<L, 8, NS_NEXT, INV, LAST_TO_REGS, LDSB>(z, j, X, cx, tw);
         }
     }
 }
@@ -774,6 +777,218 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
                 const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
                 st2(k, z[i]);
             }
+        }
+    }
+}
+
+// =============================================================================================
+// Two in-plane passes in one launch (m0 = m1 = 2^L, L <= 7): a workgroup owns one (dim 0, dim 1) plane,
+// 128 KB at L = 7, and keeps it on chip between the two 1-D transforms, so the spectral solve of a 4-D
+// 128^4 mesh makes 5 passes over HBM instead of 7 (3 instead of 5 at 128^3). NCL = M / 2 complex lines x
+// TPL = M / 8 threads: the whole plane is one k_dct8 tile of M lines. Between the passes the coefficients go
+// through a plane image in LDS (aliasing the FFT exchange buffer, barriers on both sides). Every barrier orders
+// LDS only (lds_barrier): __syncthreads would also wait for the next plane's loads.
+//   forward: dim-0 DCT of the rows (b formed on load as k_dct8's first pass), dim-1 DCT of the columns;
+//   inverse: dim-1 inverse of the columns, dim-0 inverse of the rows.
+template <int L, int MODE, bool FORMB>
+__global__ __launch_bounds__((1 << L) / 2 * (1 << L) / 8) void k_plane8(const SpecArgs a, uint32_t nplanes) {
+    using S = spec8::Shape<L>;
+    constexpr int M = S::M, TPL = S::TPL, NCL = M / 2, R0 = S::R0;
+    static_assert(L >= 4 && L <= 7, "the plane must fit the exchange buffer of one workgroup");
+    static_assert(size_t(NCL) * S::LP * 16 >= size_t(M) * M * 8, "plane image aliases the exchange buffer");
+    static_assert(MODE == SPEC_FWD || !FORMB, "b is formed by the forward pass");
+    double ca = a.ca, cb = a.cb;
+    bool rd_gb = true;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        ca = a.ctl->rho;
+        cb = a.ctl->rho * a.ctl->c_prev;
+        if (a.fold) {
+            ca = a.ctl->fold_ka;
+            cb = a.ctl->fold_kb;
+            rd_gb = a.ctl->fix != 0;
+        }
+    }
+    __shared__ double2 buf[NCL * S::LP];
+    double* const PI = reinterpret_cast<double*>(buf);   // plane image [row x1][column x0], pitch M
+    // rows mapping (dim-0 lines: lanes over j) and columns mapping (dim-1 lines: lanes over the line pair); the
+    // loop below re-derives them from an opaque copy of the thread index each plane, so the many per-thread LDS
+    // offsets are not hoisted out of it (kept live across the loop they spill)
+    int t = threadIdx.x;
+    int jr = t % TPL, cr = t / TPL, jc = t / NCL, cc = t % NCL;
+    double2 z[8];
+    // the workgroup walks planes blockIdx.x, + gridDim.x, ...; the next plane's loads are issued as soon as this
+    // plane's have been moved to LDS, so they are in flight during both transforms
+    double2 lv[8], lg1[8];   // forward: in, ga at (row 2cr + r, 2n) (gb, read only after a rho change or without the
+                             // fold, is loaded when used); inverse: the coefficient pairs
+    auto issue = [&](uint32_t e) {
+        const uint32_t pb = e << (2 * L);
+        if constexpr (MODE == SPEC_FWD) {
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const uint32_t g = pb + uint32_t(2 * cr + r) * M + uint32_t(2 * (jr + s4 * TPL));
+                    lv[2 * s4 + r] = ldnt2(a.in + g);
+                    if (FORMB) lg1[2 * s4 + r] = ldnt2(a.ga + g);
+                }
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = jc + s * TPL;
+                lv[2 * s] = ldnt2(a.in + pb + uint32_t(k) * M + uint32_t(2 * cc));
+                lv[2 * s + 1] = ldnt2(a.in + pb + uint32_t(k ? M - k : M / 2) * M + uint32_t(2 * cc));
+            }
+        }
+    };
+    uint32_t e = blockIdx.x;
+    if (e < nplanes) issue(e);
+    for (; e < nplanes; e += gridDim.x) {
+        const uint32_t pb = e << (2 * L);
+        const uint32_t en = e + gridDim.x;
+        // the twiddle tables through opaque pointers: their loads stay in the loop (hoisted out of it, the
+        // per-plane values would all stay live and spill)
+        const double2* tw = a.tw;
+        const double2* twq = a.twq;
+        asm volatile("" : "+s"(tw), "+s"(twq));
+        asm volatile("" : "+v"(t));
+        jr = t % TPL;
+        cr = t / TPL;
+        jc = t / NCL;
+        cc = t % NCL;
+        double2* const Xr = buf + cr * S::LP;
+        double2* const Xc = buf + cc * S::LP;
+        const int cxr = cr & 7, cxc = cc & 7;
+        // coefficients (k, M - k) -> the IFFT input of the Makhoul sequence, in X
+        auto inv_spectrum = [&](double2* X, int cx, int k, double2 Xk, double2 Xmk) {
+            const int ka = k, kb = k ? M - k : M / 2;
+            const double2 q1 = cconj(twq[ka]), q2 = cconj(twq[kb]);
+            if (k == 0) {
+                const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xmk.x));
+                const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xmk.y));
+                X[spec8::slot(0, cx)] = Xk;
+                X[spec8::slot(M / 2, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+            } else {
+                const double2 va1 = cmul(q1, make_double2(Xk.x, -Xmk.x));
+                const double2 vb1 = cmul(q1, make_double2(Xk.y, -Xmk.y));
+                const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xk.x));
+                const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xk.y));
+                X[spec8::slot(ka, cx)] = make_double2(va1.x - vb1.y, va1.y + vb1.x);
+                X[spec8::slot(kb, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+            }
+        };
+        // the natural-order spectrum in X -> DCT-II coefficients (k, M - k) for k = j + s TPL
+        auto fwd_coeff = [&](const double2* X, int cx, int k, double2& Xk, double2& Xmk) {
+            const int ka = k, kb = k ? M - k : M / 2;
+            const double2 Z1 = X[spec8::slot(ka, cx)], Z2 = X[spec8::slot(kb, cx)];
+            const double2 q1 = twq[ka], q2 = twq[kb];
+            if (k == 0) {
+                Xk = make_double2(q1.x * Z1.x, q1.x * Z1.y);
+                Xmk = make_double2(q2.x * Z2.x, q2.x * Z2.y);
+            } else {
+                const double2 Ap = make_double2(0.5 * (Z1.x + Z2.x), 0.5 * (Z1.y - Z2.y));
+                const double2 Bp = make_double2(0.5 * (Z1.y + Z2.y), -0.5 * (Z1.x - Z2.x));
+                Xk = make_double2(q1.x * Ap.x - q1.y * Ap.y, q1.x * Bp.x - q1.y * Bp.y);
+                Xmk = make_double2(q2.x * Ap.x + q2.y * Ap.y, q2.x * Bp.x + q2.y * Bp.y);
+            }
+        };
+        if constexpr (MODE == SPEC_FWD) {
+            // ---- dim 0: rows 2cr, 2cr + 1 as one complex line ----------------------------------------------
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int n = jr + s4 * TPL;
+                double2 xv[2];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    double2 v = lv[2 * s4 + r];
+                    if (FORMB && !rd_gb) {
+                        v.x += ca * lg1[2 * s4 + r].x;
+                        v.y += ca * lg1[2 * s4 + r].y;
+                    } else if (FORMB) {
+                        const double2 g2 = ldnt2(a.gb + pb + uint32_t(2 * cr + r) * M + uint32_t(2 * n));
+                        v.x += ca * lg1[2 * s4 + r].x + cb * g2.x;
+                        v.y += ca * lg1[2 * s4 + r].y + cb * g2.y;
+                    }
+                    xv[r] = v;
+                }
+                Xr[spec8::slot(n, cxr)] = make_double2(xv[0].x, xv[1].x);
+                Xr[spec8::slot(M - 1 - n, cxr)] = make_double2(xv[0].y, xv[1].y);
+            }
+            if (en < nplanes) issue(en);
+            lds_barrier();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) z[i] = Xr[spec8::slot(stage_in_pos<L, R0>(jr, i), cxr)];
+            stages_from<L, R0, 1, false, false, true>(z, jr, Xr, cxr, tw);   // natural-order spectrum in X
+#pragma unroll
+            for (int s = 0; s < 4; ++s) fwd_coeff(Xr, cxr, jr + s * TPL, z[2 * s], z[2 * s + 1]);
+            lds_barrier();   // every spectrum read before the plane image (same LDS) is written
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = jr + s * TPL, ka = k, kb = k ? M - k : M / 2;
+                PI[(2 * cr) * M + ka] = z[2 * s].x;
+                PI[(2 * cr + 1) * M + ka] = z[2 * s].y;
+                PI[(2 * cr) * M + kb] = z[2 * s + 1].x;
+                PI[(2 * cr + 1) * M + kb] = z[2 * s + 1].y;
+            }
+            lds_barrier();
+            // ---- dim 1: columns 2cc, 2cc + 1 as one complex line -------------------------------------------
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int n = stage_in_pos<L, R0>(jc, i);
+                const int k = n < M / 2 ? 2 * n : 2 * (M - 1 - n) + 1;
+                z[i] = *reinterpret_cast<const double2*>(&PI[k * M + 2 * cc]);
+            }
+            stages_from<L, R0, 1, false, false, true>(z, jc, Xc, cxc, tw);   // its first barrier ends the image reads
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = jc + s * TPL, ka = k, kb = k ? M - k : M / 2;
+                double2 Xk, Xmk;
+                fwd_coeff(Xc, cxc, k, Xk, Xmk);
+                stnt2(a.out + pb + uint32_t(ka) * M + uint32_t(2 * cc), Xk);
+                stnt2(a.out + pb + uint32_t(kb) * M + uint32_t(2 * cc), Xmk);
+            }
+            lds_barrier();   // every spectrum read before the next plane's rows are written
+        } else {
+            // ---- dim 1 inverse: columns 2cc, 2cc + 1 --------------------------------------------------------
+#pragma unroll
+            for (int s = 0; s < 4; ++s) inv_spectrum(Xc, cxc, jc + s * TPL, lv[2 * s], lv[2 * s + 1]);
+            if (en < nplanes) issue(en);
+            lds_barrier();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) z[i] = Xc[spec8::slot(stage_in_pos<L, R0>(jc, i), cxc)];
+            stages_from<L, R0, 1, true, true, true>(z, jc, Xc, cxc, tw);   // outputs in registers
+            lds_barrier();   // every exchange read before the plane image is written
+            using LS = LastStage<L>;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int n = stage_out_pos<L, LS::R, LS::NS>(jc, i);
+                const int k = n < M / 2 ? 2 * n : 2 * (M - 1 - n) + 1;
+                *reinterpret_cast<double2*>(&PI[k * M + 2 * cc]) = z[i];
+            }
+            lds_barrier();
+            // ---- dim 0 inverse: rows 2cr, 2cr + 1 -----------------------------------------------------------
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = jr + s * TPL, kb = k ? M - k : M / 2;
+                z[2 * s] = make_double2(PI[(2 * cr) * M + k], PI[(2 * cr + 1) * M + k]);
+                z[2 * s + 1] = make_double2(PI[(2 * cr) * M + kb], PI[(2 * cr + 1) * M + kb]);
+            }
+            lds_barrier();   // every image read before the exchange buffer (same LDS) is written
+#pragma unroll
+            for (int s = 0; s < 4; ++s) inv_spectrum(Xr, cxr, jr + s * TPL, z[2 * s], z[2 * s + 1]);
+            lds_barrier();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) z[i] = Xr[spec8::slot(stage_in_pos<L, R0>(jr, i), cxr)];
+            stages_from<L, R0, 1, true, false, true>(z, jr, Xr, cxr, tw);   // output through X
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int n = jr + s4 * TPL;
+                const double2 v0 = Xr[spec8::slot(n, cxr)], v1 = Xr[spec8::slot(M - 1 - n, cxr)];
+                stnt2(a.out + pb + uint32_t(2 * cr) * M + uint32_t(2 * n), make_double2(v0.x, v1.x));
+                stnt2(a.out + pb + uint32_t(2 * cr + 1) * M + uint32_t(2 * n), make_double2(v0.y, v1.y));
+            }
+            lds_barrier();   // every exchange read before the next plane's spectrum is written
         }
     }
 }
@@ -1890,6 +2105,68 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
         return;
     a.xcd = 0;
     launch_dct8_tile<L, S::TQ>(a, s, mode, d0, formb, std::min(want, S::TQ));   // the default tile
+}
+
+// the fused in-plane passes (k_plane8): m0 = m1 = 2^L, 16 <= m <= 128, dims 0 and 1 transformed first
+bool plane_pass_ok(const Geom& g) {
+    if (g.p < 3 || g.m[0] != g.m[1] || probe_env("MVTV_PLANE_OFF") || probe_env("MVTV_DCT_LDS") ||
+        probe_env("MVTV_DCT_MID"))
+        return false;
+    // and enough planes to fill the chip: 128^3's 128 planes (one workgroup each) ran 1 % slower than the two
+    // passes, 128^4's 16384 3.5 % faster per ADMM iteration (profiles/r03/v15_plane)
+    const uint32_t m = g.m[0];
+    return m >= 16 && m <= 128 && (m & (m - 1)) == 0 && g.N / (uint64_t(m) * m) >= 1024;
+}
+
+// mode SPEC_FWD (dims 0 then 1; b formed on load when ga != nullptr, from the folded s when fold) or SPEC_INV
+// (dims 1 then 0), in place over every (dim 0, dim 1) plane of g
+hipError_t launch_plane_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, const double* in,
+                             const double* ga, double ca, const double* gb, double cb, double* out,
+                             const AdmmCtl* ctl, const int32_t* skip, bool fold) {
+    if (!plane_pass_ok(g) || (mode != SPEC_FWD && mode != SPEC_INV) || (mode == SPEC_INV && ga) ||
+        (fold && (!ga || !gb || !ctl)))
+        return hipErrorInvalidValue;
+    SpecArgs a{};
+    a.ctl = ctl;
+    a.skip = skip;
+    a.in = in;
+    a.ga = ga;
+    a.gb = gb ? gb : ga;
+    a.ca = ca;
+    a.cb = gb ? cb : 0.0;
+    a.out = out;
+    a.tw = reinterpret_cast<const double2*>(sp.tw + sp.tw_off[0]);    // m0 = m1: one table serves both dims
+    a.twq = reinterpret_cast<const double2*>(sp.twq + sp.twq_off[0]);
+    a.fold = fold ? 1 : 0;
+    const uint32_t m = g.m[0];
+    const uint32_t nplanes = g.N / (m * m);
+    // persistent over the planes: one workgroup per CU (the plane's 152 KB of LDS) at m = 128, so the next
+    // plane's loads overlap the transforms; smaller planes keep one workgroup per plane
+    static thread_local int dev = -1, cus = 256;
+    int dv = 0;
+    if (hipGetDevice(&dv) == hipSuccess && dv != dev) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dv) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+        dev = dv;
+    }
+    const dim3 grid(m == 128 ? std::min<uint32_t>(nplanes, uint32_t(cus)) : nplanes);
+    const bool formb = ga != nullptr;
+#define MVTV_PLANE(LL)                                                                                          \
+    do {                                                                                                        \
+        const dim3 block((1u << LL) / 2 * (1u << LL) / 8);                                                      \
+        if (mode == SPEC_INV) klaunch(k_plane8<LL, SPEC_INV, false>, grid, block, 0, s, a, nplanes);            \
+        else if (formb) klaunch(k_plane8<LL, SPEC_FWD, true>, grid, block, 0, s, a, nplanes);                   \
+        else klaunch(k_plane8<LL, SPEC_FWD, false>, grid, block, 0, s, a, nplanes);                             \
+    } while (0)
+    switch (m) {
+        case 16: MVTV_PLANE(4); break;
+        case 32: MVTV_PLANE(5); break;
+        case 64: MVTV_PLANE(6); break;
+        case 128: MVTV_PLANE(7); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef MVTV_PLANE
+    return hipGetLastError();
 }
 
 bool dct_pcg_fusable(const Geom& g, size_t partial_words) {
