@@ -18,7 +18,7 @@ import re
 import sys
 from collections import defaultdict
 
-NAMES = {"k_admm3d": "admm_fused", "k_admm3a": "admm_fused", "k_gather4a": "gather_Dt", "k_gather4b": "gather4_b", "k_edge3d": "edge_update", "k_gather3d": "gather_Dt", "k_dct8": "dct",
+NAMES = {"k_plane8": "dct_plane", "k_admm3d": "admm_fused", "k_admm3a": "admm_fused", "k_gather4a": "gather_Dt", "k_gather4b": "gather4_b", "k_edge3d": "edge_update", "k_gather3d": "gather_Dt", "k_dct8": "dct",
          "k_dct": "dct", "k_dctg": "dct", "k_tri": "dct_tri", "k_trig": "dct_tri",
          "k_cg3d": "pcg_fused3d", "k_edge_update": "edge_update", "k_gather": "gather_Dt",
          "k_apply_A": "pcg_apply_A", "k_pcg_update": "pcg_update", "k_pcg_pupdate": "pcg_direction",
@@ -32,6 +32,8 @@ def short(kname: str) -> str:
                 return "pcg_init"
             if k in ("k_dct8", "k_dct") and re.search(r"k_dct8?<[^>]*true, true", kname):
                 return "dct_first"   # the pass that forms b on load (FORMB)
+            if k == "k_plane8" and re.search(r"k_plane8<\d+, 0, true>", kname):
+                return "dct_plane_first"   # both in-plane forward passes, b formed on load
             return v
     return kname.split("(")[0]
 
