@@ -594,16 +594,41 @@ def main():
         if comm is not None:
             comm.close()
     else:
-        # N > 1: the metric is one mesh over all GPUs (slab, strong); the independent fits (weak) beside it
-        comm = _rccl_comm(D, D.local % mv.device_count())
+        # N > 1: the metric is one mesh over all GPUs (slab, strong); the independent fits (weak) beside it.
+        # A failure of the RCCL communicator or of the slab run (the same on every rank: the ranks agree on it
+        # over gloo) still leaves the independent fits' line, labelled with the error.
+        comm, err = None, None
+        try:
+            comm = _rccl_comm(D, D.local % mv.device_count())
+        except Exception as e:  # noqa: BLE001 (reported in the line)
+            err = f"RCCL communicator: {e!r}"
+        failed, = D.allreduce([1.0 if comm is None else 0.0], "max")
+        if failed and comm is not None:
+            comm.close()
+            comm = None
         ind = independent_main(a, D, comm)
-        line = slab_main(a, D, comm)
-        comm.close()
+        line = None
+        if comm is not None:
+            try:
+                line = slab_main(a, D, comm)
+                ok = 1.0
+            except Exception as e:  # noqa: BLE001
+                err, ok = f"slab run: {e!r}", 0.0
+            failed, = D.allreduce([1.0 - ok], "max")
+            comm.close()
+            if failed:
+                line = None
+                err = err or "slab run failed on another rank"
         if line is not None:
             line["independent_fits"] = {k: ind[k] for k in ("value", "unit", "ms_per_step", "scaling", "roofline",
                                                             "residuals")}
             line["independent_fits"]["workload"] = (f"one {a.size}^{a.dims} fit per GPU (noise seed + rank), "
                                                    f"{D.world} GPUs")
+        elif ind is not None:   # rank 0: the slab line could not be produced
+            line = ind
+            line["slab_error"] = err or "unknown"
+            line["config"]["note"] = ("the one-mesh slab run failed (slab_error); this line is the independent "
+                                      "fits, one mesh per GPU (weak scaling)")
     if line is not None:
         print(json.dumps(line), file=OUT, flush=True)
     D.close()
