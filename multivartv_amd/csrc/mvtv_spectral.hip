@@ -1254,6 +1254,304 @@ __global__ __launch_bounds__(dctg::NT) __attribute__((amdgpu_waves_per_eu(4))) v
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_dctm: register-resident mixed-radix passes for the lengths of the BASELINE-adjacent meshes (500 = 4 5^3,
+// 1000 = 2 4 5^3): k_dct8's Stockham scheme with a compile-time radix plan. A thread holds V complex values
+// of one complex line (two real lines, Makhoul pairing) and runs its V / R radix-R butterflies of each stage in
+// registers; LDS carries the exchanges between stages (k_dctg: one in-place LDS stage per radix with FastDiv
+// index math and a permutation-table load per element). FWD and INV passes (the last dimension takes k_trig or
+// k_dctg's MID pass); TQ = 16 real lines per workgroup, lanes over the lines for a strided pass (16-B accesses
+// of a line pair, 128-B rows when the tile does not straddle a stride boundary), over j for d = 0.
+namespace dctm {
+constexpr int NCL = 8, TQ = 2 * NCL;
+// radix plan and values per thread (every radix divides V): 500 = 2 2 5^3 with V = 10 (400 threads, two
+// workgroups per CU), 1000 = 2 4 5^3 with V = 20 (400 threads)
+template <int M> struct Plan;
+template <> struct Plan<500> {
+    static constexpr int n = 5, V = 10;
+    static constexpr int r[5] = {2, 2, 5, 5, 5};
+};
+template <> struct Plan<1000> {
+    static constexpr int n = 5, V = 20;
+    static constexpr int r[5] = {2, 4, 5, 5, 5};
+};
+template <int M> struct Shape {
+    static constexpr int V = Plan<M>::V;      // complex values per thread
+    static constexpr int T = M / V;           // threads per complex line
+    static constexpr int NT = NCL * T;
+    static constexpr int LP = M + 4;          // line pitch (complex slots)
+};
+}  // namespace dctm
+
+// stage S (span NS) of the thread's butterflies b_s = j + s T; z[s R + r] holds position b_s + r M / R
+template <int M, int S, int NS, bool INV>
+__device__ __forceinline__ void dctm_stages(double2* z, int j, double2* X, const double2* __restrict__ tw) {
+    using P = dctm::Plan<M>;
+    constexpr int V = P::V, R = P::r[S], T = M / V, NB = V / R;
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+        if constexpr (NS > 1) {
+            const int kk = (j + s * T) % NS;
+            constexpr int step = M / (NS * R);
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                double2 w = tw[kk * r * step];
+                if (INV) w = cconj(w);
+                z[s * R + r] = cmul(z[s * R + r], w);
+            }
+        }
+        dft_any<R, INV>(z + s * R);
+    }
+    if constexpr (S + 1 < P::n) {
+        constexpr int R2 = P::r[S + 1];
+        __syncthreads();   // every thread has read this stage's inputs
+#pragma unroll
+        for (int s = 0; s < NB; ++s) {
+            const int b = j + s * T;
+#pragma unroll
+            for (int r = 0; r < R; ++r) X[(b / NS) * NS * R + b % NS + r * NS] = z[s * R + r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < V / R2; ++s)
+#pragma unroll
+            for (int r = 0; r < R2; ++r) z[s * R2 + r] = X[j + s * T + r * (M / R2)];
+        dctm_stages<M, S + 1, NS * R, INV>(z, j, X, tw);
+    }
+}
+// output position of z[i] after the last stage
+template <int M>
+__device__ __forceinline__ int dctm_out_pos(int j, int i) {
+    using P = dctm::Plan<M>;
+    constexpr int R = P::r[P::n - 1], NS = M / R, T = M / P::V;
+    const int s = i / R, r = i % R, b = j + s * T;
+    return (b / NS) * NS * R + b % NS + r * NS;
+}
+// input position of z[i] of the first stage
+template <int M>
+__device__ __forceinline__ int dctm_in_pos(int j, int i) {
+    using P = dctm::Plan<M>;
+    constexpr int R = P::r[0], T = M / P::V;
+    return j + (i / R) * T + (i % R) * (M / R);
+}
+
+template <int M, int MODE, bool D0, bool FORMB>
+__global__ __launch_bounds__(dctm::Shape<M>::NT) void k_dctm(const SpecArgs a) {
+    using S = dctm::Shape<M>;
+    constexpr int T = S::T, NCL = dctm::NCL, V = S::V;
+    static_assert(MODE == SPEC_FWD || MODE == SPEC_INV, "FWD / INV passes");
+    double ca = a.ca, cb = a.cb;
+    bool rd_gb = true;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        ca = a.ctl->rho;
+        cb = a.ctl->rho * a.ctl->c_prev;
+        if (a.fold) {
+            ca = a.ctl->fold_ka;
+            cb = a.ctl->fold_kb;
+            rd_gb = a.ctl->fix != 0;
+        }
+    }
+    __shared__ double2 buf[NCL * S::LP];
+    const int t = threadIdx.x;
+    const int j = D0 ? (t % T) : (t / NCL);
+    const int c = D0 ? (t / T) : (t % NCL);
+    const uint32_t q0 = blockIdx.x * uint32_t(dctm::TQ);
+    const int la = 2 * c;
+    const bool va = q0 + uint32_t(la) < a.nlines;   // lines come in pairs: nlines is even (launcher)
+    double2* X = buf + c * S::LP;
+    const double2* __restrict__ tw = a.tw;
+    // global offset of (real line la of this thread's pair, position k); line la + 1 is the next word
+    const uint32_t q = q0 + uint32_t(la);
+    uint32_t lbase;
+    if (D0) {
+        lbase = q * uint32_t(M);
+    } else {
+        const uint32_t hi = a.fds.div(q);
+        lbase = (q - hi * a.stride) + hi * a.stride * uint32_t(M);
+    }
+    auto gidx = [&](uint32_t k) -> uint32_t { return D0 ? lbase + k : lbase + k * a.stride; };
+    auto ld_pair2 = [&](uint32_t g) -> double2 {   // b (or the input) at global offsets g, g + 1
+        double2 v = ldnt2(a.in + g);
+        if (FORMB && !rd_gb) {
+            const double2 g1 = ldnt2(a.ga + g);
+            v.x += ca * g1.x;
+            v.y += ca * g1.y;
+        } else if (FORMB) {
+            const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
+            v.x += ca * g1.x + cb * g2.x;
+            v.y += ca * g1.y + cb * g2.y;
+        }
+        return v;
+    };
+    auto ld_pair = [&](uint32_t k) -> double2 {   // (line la, line la + 1) at position k, strided pass
+        const uint32_t g = gidx(k);
+        double2 v = ldnt2(a.in + g);
+        if (FORMB && !rd_gb) {
+            const double2 g1 = ldnt2(a.ga + g);
+            v.x += ca * g1.x;
+            v.y += ca * g1.y;
+        } else if (FORMB) {
+            const double2 g1 = ldnt2(a.ga + g), g2 = ldnt2(a.gb + g);
+            v.x += ca * g1.x + cb * g2.x;
+            v.y += ca * g1.y + cb * g2.y;
+        }
+        return v;
+    };
+    double2 z[V];
+    if constexpr (MODE == SPEC_FWD) {
+        // ---- Makhoul input v[n] = x[2n], v[M-1-n] = x[2n+1] into the first stage --------------------------
+        if (D0) {
+            // contiguous lines: 16-B loads of (x[2n], x[2n+1]) of each real line land at positions n, M-1-n
+#pragma unroll
+            for (int s = 0; s < M / 2 / T; ++s) {
+                const int n = j + s * T;
+                double2 xa = make_double2(0.0, 0.0), xb = make_double2(0.0, 0.0);
+                if (va) {   // (x[2n], x[2n+1]) of lines la and la + 1: 16-B loads (M even: aligned)
+                    xa = ld_pair2(lbase + uint32_t(2 * n));
+                    xb = ld_pair2(lbase + uint32_t(M) + uint32_t(2 * n));
+                }
+                X[n] = make_double2(xa.x, xb.x);
+                X[M - 1 - n] = make_double2(xa.y, xb.y);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < V; ++i) z[i] = X[dctm_in_pos<M>(j, i)];
+        } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const int n = dctm_in_pos<M>(j, i);
+                const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
+                z[i] = va ? ld_pair(k) : make_double2(0.0, 0.0);
+            }
+        }
+        dctm_stages<M, 0, 1, false>(z, j, X, tw);
+        __syncthreads();   // every thread has read the last exchange
+#pragma unroll
+        for (int i = 0; i < V; ++i) X[dctm_out_pos<M>(j, i)] = z[i];   // natural-order spectrum
+        __syncthreads();
+        // ---- spectrum -> DCT-II coefficients (k, M - k); k = 0 and M / 2 pair with themselves --------------
+#pragma unroll
+        for (int s = 0; s < (M / 2 + T) / T; ++s) {
+            const int k = j + s * T;
+            if (k > M / 2) continue;
+            const int ka = k, kb = k ? M - k : M / 2;
+            const double2 Z1 = X[ka], Z2 = X[kb];
+            const double2 q1 = a.twq[ka], q2 = a.twq[kb];
+            double2 Xk, Xmk;
+            if (k == 0) {
+                Xk = make_double2(q1.x * Z1.x, q1.x * Z1.y);
+                Xmk = make_double2(q2.x * Z2.x, q2.x * Z2.y);
+            } else {
+                const double2 Ap = make_double2(0.5 * (Z1.x + Z2.x), 0.5 * (Z1.y - Z2.y));
+                const double2 Bp = make_double2(0.5 * (Z1.y + Z2.y), -0.5 * (Z1.x - Z2.x));
+                Xk = make_double2(q1.x * Ap.x - q1.y * Ap.y, q1.x * Bp.x - q1.y * Bp.y);
+                Xmk = make_double2(q2.x * Ap.x + q2.y * Ap.y, q2.x * Bp.x + q2.y * Bp.y);
+            }
+            if (!va || k == M / 2) continue;   // k = M/2 is written by k = 0 (its pair)
+            if (D0) {
+                __builtin_nontemporal_store(Xk.x, a.out + gidx(uint32_t(ka)));
+                __builtin_nontemporal_store(Xk.y, a.out + gidx(uint32_t(ka)) + uint32_t(M));
+                __builtin_nontemporal_store(Xmk.x, a.out + gidx(uint32_t(kb)));
+                __builtin_nontemporal_store(Xmk.y, a.out + gidx(uint32_t(kb)) + uint32_t(M));
+            } else {
+                stnt2(a.out + gidx(uint32_t(ka)), Xk);
+                stnt2(a.out + gidx(uint32_t(kb)), Xmk);
+            }
+        }
+    } else {
+        // ---- DCT-III: coefficient pairs (k, M - k) -> the Makhoul spectrum in X -----------------------------
+#pragma unroll
+        for (int s = 0; s < (M / 2 + T) / T; ++s) {
+            const int k = j + s * T;
+            if (k >= M / 2) continue;   // k = 0 also writes slot M / 2
+            const int ka = k, kb = k ? M - k : M / 2;
+            double2 Xk = make_double2(0.0, 0.0), Xmk = make_double2(0.0, 0.0);
+            if (va) {
+                if (D0) {
+                    Xk = make_double2(__builtin_nontemporal_load(a.in + gidx(uint32_t(ka))),
+                                      __builtin_nontemporal_load(a.in + gidx(uint32_t(ka)) + uint32_t(M)));
+                    Xmk = make_double2(__builtin_nontemporal_load(a.in + gidx(uint32_t(kb))),
+                                       __builtin_nontemporal_load(a.in + gidx(uint32_t(kb)) + uint32_t(M)));
+                } else {
+                    Xk = ldnt2(a.in + gidx(uint32_t(ka)));
+                    Xmk = ldnt2(a.in + gidx(uint32_t(kb)));
+                }
+            }
+            const double2 q1 = cconj(a.twq[ka]), q2 = cconj(a.twq[kb]);
+            if (k == 0) {
+                const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xmk.x));
+                const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xmk.y));
+                X[0] = Xk;
+                X[M / 2] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+            } else {
+                const double2 va1 = cmul(q1, make_double2(Xk.x, -Xmk.x));
+                const double2 vb1 = cmul(q1, make_double2(Xk.y, -Xmk.y));
+                const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xk.x));
+                const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xk.y));
+                X[ka] = make_double2(va1.x - vb1.y, va1.y + vb1.x);
+                X[kb] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < V; ++i) z[i] = X[dctm_in_pos<M>(j, i)];
+        dctm_stages<M, 0, 1, true>(z, j, X, tw);
+        // ---- un-permute v[n] -> x[2n] (n < M/2), x[2(M-1-n)+1] -------------------------------------------
+        if (D0) {
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < V; ++i) X[dctm_out_pos<M>(j, i)] = z[i];
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < M / 2 / T; ++s) {
+                const int n = j + s * T;
+                const double2 v0 = X[n], v1 = X[M - 1 - n];
+                if (va) {
+                    stnt2(a.out + lbase + uint32_t(2 * n), make_double2(v0.x, v1.x));
+                    stnt2(a.out + lbase + uint32_t(M) + uint32_t(2 * n), make_double2(v0.y, v1.y));
+                }
+            }
+        } else if (va) {
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const int n = dctm_out_pos<M>(j, i);
+                const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
+                stnt2(a.out + gidx(k), z[i]);
+            }
+        }
+    }
+}
+
+// k_dctm serves FWD / INV passes of m = 500 / 1000 lines; false: the caller takes k_dctg
+static bool launch_dctm(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
+    const uint32_t m = a.m[a.d];
+    // the first pass (b formed on load) stays on k_dctg: k_dctm's measured 1.20 against 1.16 ms at 500^3
+    if ((m != 500 && m != 1000) || mode == SPEC_MID || formb || (a.nlines & 1u) || probe_env("MVTV_DCTM_OFF"))
+        return false;
+    if (!d0 && (a.stride & 1u)) return false;   // line pairs must be adjacent words
+    const dim3 grid((a.nlines + uint32_t(dctm::TQ) - 1) / uint32_t(dctm::TQ));
+#define MVTV_DCTM(MM)                                                                                           \
+    do {                                                                                                        \
+        const dim3 block(dctm::Shape<MM>::NT);                                                                  \
+        if (mode == SPEC_INV) {                                                                                 \
+            if (d0) klaunch(k_dctm<MM, SPEC_INV, true, false>, grid, block, 0, s, a);                           \
+            else klaunch(k_dctm<MM, SPEC_INV, false, false>, grid, block, 0, s, a);                             \
+        } else if (d0) {                                                                                        \
+            if (formb) klaunch(k_dctm<MM, SPEC_FWD, true, true>, grid, block, 0, s, a);                         \
+            else klaunch(k_dctm<MM, SPEC_FWD, true, false>, grid, block, 0, s, a);                              \
+        } else {                                                                                                \
+            if (formb) klaunch(k_dctm<MM, SPEC_FWD, false, true>, grid, block, 0, s, a);                        \
+            else klaunch(k_dctm<MM, SPEC_FWD, false, false>, grid, block, 0, s, a);                             \
+        }                                                                                                       \
+    } while (0)
+    if (m == 500) MVTV_DCTM(500);
+    else MVTV_DCTM(1000);
+#undef MVTV_DCTM
+    return true;
+}
+
 static void launch_dctg(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
     const dim3 grid((a.nlines + uint32_t(a.tq) - 1) / uint32_t(a.tq)), block(dctg::NT);
     const size_t smem = size_t(a.tq / 2) * (a.m[a.d] + spec::PAD) * sizeof(double2);
@@ -2247,6 +2545,7 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
                 return hipGetLastError();
             }
         }
+        if (launch_dctm(a, s, mode, d == 0, formb)) return hipGetLastError();
         // <= 16 lines (128-B rows for d > 0) in <= 64 KB of LDS
         int tq = 16;
         while (tq > 2 && (tq / 2) * int(m + spec::PAD) > spec::LDS_WORDS / 2 + 8 * spec::PAD) tq /= 2;

@@ -46,7 +46,10 @@ CASES = [([2], None, "cpp", False), ([8], None, "cpp", False), ([1024], None, "p
          ([5, 5, 5, 5], [0.1, 0.2, 0.3, 0.4], "cpp", False), ([6, 6, 6, 6], None, "py", False),
          ([7, 7, 7], [0.2, 0.3, 0.4], "cpp", True), ([3, 4096], [0.5, 0.5], "cpp", False),
          # mixed-radix mesh whose last dimension takes the general-length tridiagonal pass (k_trig)
-         ([4096, 100], [0.5, 0.5], "cpp", False)]
+         ([4096, 100], [0.5, 0.5], "cpp", False),
+         # register-resident mixed-radix passes along dim 0 (k_dctm, m = 500 / 1000; the strided form is checked
+         # at 500^3 below: unequal dims are refused at p >= 3, the reference's mixed-partial rule)
+         ([500, 6], [0.3, 0.7], "cpp", False), ([1000, 4], None, "py", False)]
 
 
 def _problem(m, deltas, order, unit, seed=0):
@@ -75,10 +78,10 @@ def test_spectral_vs_superlu(m, deltas, order, unit, sigma):
 
 
 @pytest.mark.parametrize("m", [[256, 256, 256], [1024, 1024], [64, 64, 64, 64], [100, 100, 100], [240, 240, 240],
-                               [60, 60, 60, 60]])
+                               [60, 60, 60, 60], [500, 500, 500], [1000, 1000]])
 def test_spectral_residual_baseline_sizes(m):
-    """Config-sized meshes (3D 256^3, 2D 1024^2; 4D at 64^4) and mixed-radix ones (k_dctg passes, k_trig
-    last dimension): residual through the stencil operator."""
+    """Config-sized meshes (3D 256^3, 2D 1024^2; 4D at 64^4) and mixed-radix ones (k_dctg / k_dctm passes,
+    k_trig last dimension): residual through the stencil operator."""
     p = len(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     N = int(np.prod(m))
