@@ -1527,8 +1527,10 @@ __global__ __launch_bounds__(dctm::Shape<M>::NT) void k_dctm(const SpecArgs a) {
 // k_dctm serves FWD / INV passes of m = 500 / 1000 lines; false: the caller takes k_dctg
 static bool launch_dctm(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
     const uint32_t m = a.m[a.d];
-    // the first pass (b formed on load) stays on k_dctg: k_dctm's measured 1.20 against 1.16 ms at 500^3
-    if ((m != 500 && m != 1000) || mode == SPEC_MID || formb || (a.nlines & 1u) || probe_env("MVTV_DCTM_OFF"))
+    // the first pass (b formed on load): k_dctm at 500 (V = 10: 0.89 against k_dctg's 1.09 ms at 500^3), k_dctg at
+    // 1000 (V = 20: 31 against 29 us at 1000^2; profiles/r03/v19_dctm)
+    if ((m != 500 && m != 1000) || mode == SPEC_MID || (formb && m != 500) || (a.nlines & 1u) ||
+        probe_env("MVTV_DCTM_OFF"))
         return false;
     if (!d0 && (a.stride & 1u)) return false;   // line pairs must be adjacent words
     const dim3 grid((a.nlines + uint32_t(dctm::TQ) - 1) / uint32_t(dctm::TQ));
