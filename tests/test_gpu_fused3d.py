@@ -33,14 +33,16 @@ def test_fused_ragged_dim0_matches_oracle(m, iters):
 
 
 @pytest.mark.parametrize("m,lam", [([32, 32, 32], 1.0), ([32, 32, 32], 0.02), ([64, 64, 64], 1.0), ([128, 128, 128], 0.1),
-                                   ([128, 96], 1.0), ([1024, 1024], 0.1), ([16, 16, 16, 16], 1.0), ([32, 32, 32, 32], 0.02)],
+                                   ([128, 96], 1.0), ([1024, 1024], 0.1), ([16, 16, 16, 16], 1.0), ([32, 32, 32, 32], 0.02),
+                                   ([500, 24], 1.0), ([500, 40], 0.1)],
                          ids=["m32_lam1", "m32_lam002", "m64_lam1", "m128_lam01", "2d_128x96", "2d_1024", "4d_16_lam1",
-                              "4d_32_lam002"])
+                              "4d_32_lam002", "2d_500x24_unfolded", "2d_500x40_unfolded"])
 def test_folded_rhs_converged_matches_oracle(m, lam):
     """The asynchronous spectral loop (2-D / 3-D fused kernels, 4-D two-pass gather) on a power-of-two m0 stores the folded s = rho (D^T alpha + D^T u) for the
     next solve's b = oty + s, and after a residual-balancing step that changed rho (7 doublings over these runs)
     forms b = oty + (rho'/rho) s + rho' (c - 1) D^T u. Converged runs against the C oracle's loop with the exact
-    DCT solve (rcpp…/solvers.cpp:110-133): iterations and rho exactly, theta to 1e-9."""
+    DCT solve (rcpp…/solvers.cpp:110-133): iterations and rho exactly, theta to 1e-9. The m0 = 500 cases take the
+    unfolded first pass (b = oty + rho' D^T alpha + rho' c D^T u) in k_dctm."""
     y = towers(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     th0 = np.full(y.size, y.mean())
