@@ -49,7 +49,9 @@ CASES = [([2], None, "cpp", False), ([8], None, "cpp", False), ([1024], None, "p
          ([4096, 100], [0.5, 0.5], "cpp", False),
          # register-resident mixed-radix passes along dim 0 (k_dctm, m = 500 / 1000; the strided form is checked
          # at 500^3 below: unequal dims are refused at p >= 3, the reference's mixed-partial rule)
-         ([500, 6], [0.3, 0.7], "cpp", False), ([1000, 4], None, "py", False)]
+         ([500, 6], [0.3, 0.7], "cpp", False), ([1000, 4], None, "py", False),
+         # an odd number of lines: k_dctm pairs lines, so these fall back to k_dctg
+         ([500, 7], [0.3, 0.7], "cpp", False), ([1000, 3], None, "py", False)]
 
 
 def _problem(m, deltas, order, unit, seed=0):
