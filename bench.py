@@ -166,6 +166,24 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
         return t.cpu().tolist()
 
+    def allreduce_within(self, vals, seconds, op="max"):
+        """allreduce that gives up after `seconds` (None then): the agreement after a failure, whose peers may be
+        stuck in an RCCL collective the failed rank will never join."""
+        if not self.dist:
+            return list(vals)
+        import datetime
+
+        import torch
+        t = torch.tensor(list(vals), dtype=torch.float64)
+        try:
+            w = self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM,
+                                     async_op=True)
+            if not w.wait(timeout=datetime.timedelta(seconds=seconds)):
+                return None
+        except Exception:  # noqa: BLE001 (a timed-out or broken group: no agreement)
+            return None
+        return t.tolist()
+
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
@@ -614,7 +632,23 @@ def main():
                 ok = 1.0
             except Exception as e:  # noqa: BLE001
                 err, ok = f"slab run: {e!r}", 0.0
-            failed, = D.allreduce([1.0 - ok], "max")
+            if ok:
+                failed, = D.allreduce([0.0], "max")
+            else:
+                # a failure that is not every rank's (one rank errs mid-loop) leaves the peers inside an RCCL
+                # collective or a stream sync, where a gloo agreement would wait ~30 min: bounded wait, then rank 0
+                # prints what it has and this process exits non-zero, so the launcher ends the stuck peers
+                agreed = D.allreduce_within([1.0], 120.0, "max")
+                if agreed is None:
+                    log(f"rank {D.rank}: {err}; peers did not reach the agreement, exiting")
+                    if ind is not None:
+                        ind["slab_error"] = err
+                        ind["config"]["note"] = ("the one-mesh slab run failed on this rank (slab_error); this line "
+                                                 "is the independent fits, one mesh per GPU (weak scaling)")
+                        print(json.dumps(ind), file=OUT, flush=True)
+                    sys.stderr.flush()
+                    os._exit(3)
+                failed = agreed[0]
             comm.close()
             if failed:
                 line = None

@@ -88,8 +88,8 @@ typedef enum mvtv_theta_solver {
     MVTV_SOLVER_AUTO = 0,      /* SPECTRAL where it is exact; else PCG_SPECTRAL on the same meshes; else PCG */
     MVTV_SOLVER_PCG = 1,       /* Jacobi-PCG on the 3^p-point stencil, warm-started, pcg_rtol */
     MVTV_SOLVER_SPECTRAL = 2,  /* direct: cosine transforms + a tridiagonal solve along the last dim. Exact for
-                                  W = I (mesh == data) with every m_j <= 4096 a product of 2, 3, 5, 7;
-                                  MVTV_BAD_ARG otherwise */
+                                  W = I (mesh == data) with every m_j <= 4096 (FFT plans for lengths with prime
+                                  factors 2, 3, 5, 7, Bluestein's chirp-z for any other); MVTV_BAD_ARG otherwise */
     MVTV_SOLVER_PCG_SPECTRAL = 3 /* PCG preconditioned by S (mean(W) I + sigma D^T D) S, its middle factor inverted
                                   exactly by cosine transforms, S = I or a Jacobi-like diagonal scaling when W varies
                                   strongly against sigma D^T D's diagonal: for W != I (scattered data, CV folds) on
@@ -130,7 +130,7 @@ int32_t mvtv_problem_blocks(const mvtv_problem* prob);
 mvtv_status mvtv_problem_block_info(const mvtv_problem* prob, int32_t k, int32_t* code, int32_t* sprime, double* weight);
 /* new O^T y and W for the same mesh (CV folds re-run create_cache_objects, rcpp…/solvers.cpp:347-348) */
 mvtv_status mvtv_problem_set_data(mvtv_problem* prob, const double* oty, const double* wdiag);
-/* 1 if MVTV_SOLVER_SPECTRAL applies to this problem (W = I, every m_j <= 4096 a product of 2, 3, 5, 7), else 0 */
+/* 1 if MVTV_SOLVER_SPECTRAL applies to this problem (W = I, every m_j <= 4096), else 0 */
 int32_t mvtv_problem_spectral_ok(const mvtv_problem* prob);
 
 /* ---- the hot path ------------------------------------------------------------------ */
@@ -206,10 +206,10 @@ mvtv_status mvtv_solve_spectral(mvtv_problem* prob, double sigma, const double* 
  * the theta-solve is PCG with the spectral preconditioner of mean(W) I + sigma D^T D (opts pcg_rtol,
  * pcg_max_iter, pcg_strict as mvtv_admm_run), distributed: a halo of the search direction per iteration and
  * one all-reduce per dot product; the loop then polls once per ADMM iteration. Supported: variant B, W = I
- * or diagonal, u0 = 0, m_j <= 4096 a product of 2, 3, 5, 7
- * for j < p - 1; the last dimension any length when G >= 2 (its line solves are substructured over the ranks;
- * each rank's plane count must be 1..64 segments of <= 32 rows, e.g. any count <= 64 or with a divisor in
- * 2..32 giving <= 64 segments), a 2-3-5-7 length <= 4096 when G = 1. */
+ * or diagonal, u0 = 0, m_j <= 4096 for j < p - 1; the last dimension any length when G >= 2 (its line solves
+ * are substructured over the ranks; each rank's plane count must be 1..64 segments of <= 32 rows, e.g. any
+ * count <= 64 or with a divisor in 2..32 giving <= 64 segments: checked on every rank before the first
+ * collective, MVTV_BAD_ARG on all of them otherwise), <= 4096 when G = 1. */
 typedef struct mvtv_slab_desc {
     int64_t m_global;          /* planes of dim p-1 in the whole mesh */
     int64_t z_begin, z_end;    /* owned planes */

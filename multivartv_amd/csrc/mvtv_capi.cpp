@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <complex>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -126,7 +127,7 @@ void free_all(mvtv_problem* P) {
     if (P->st) (void)hipFree(P->st);
     if (P->ctl) (void)hipFree(P->ctl);
     if (P->host_ctl) (void)hipHostFree(P->host_ctl);
-    for (double* t : {P->spec.tw, P->spec.twq, P->spec.lam})
+    for (double* t : {P->spec.tw, P->spec.twq, P->spec.lam, P->spec.blu})
         if (t) (void)hipFree(t);
     if (P->spec.perm) (void)hipFree(P->spec.perm);
     P->spec = SpecPlan{};
@@ -280,6 +281,73 @@ mvtv_status pcg_solve(mvtv_problem* P, double sigma, const double* oty, const do
 
 bool spectral_ok(const mvtv_problem* P) { return P->spec_mesh && P->wmode == W_IDENTITY; }
 
+// M = 2^ceil(log2(2m - 1)): the circular convolution length of Bluestein's identity for length m
+uint32_t bluestein_length(uint32_t m) {
+    uint32_t M = 1;
+    while (M < 2 * m - 1) M <<= 1;
+    return M;
+}
+
+// In-place radix-2 DFT (sign -1, unnormalised) in long double: the convolution kernels' transforms, once per
+// problem (twiddles from exact angles 2 pi (k mod M) / M)
+void fft_ld(std::vector<std::complex<long double>>& x) {
+    const size_t M = x.size();
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (size_t i = 1, j = 0; i < M; ++i) {
+        size_t bit = M >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) std::swap(x[i], x[j]);
+    }
+    for (size_t len = 2; len <= M; len <<= 1) {
+        for (size_t i = 0; i < M; i += len)
+            for (size_t k = 0; k < len / 2; ++k) {
+                const long double ang = -2.0L * pi * (long double)(k * (M / len)) / (long double)M;
+                const std::complex<long double> w(cosl(ang), sinl(ang));
+                const std::complex<long double> u = x[i + k], v = x[i + k + len / 2] * w;
+                x[i + k] = u + v;
+                x[i + k + len / 2] = u - v;
+            }
+    }
+}
+
+// Bluestein tables of one dimension (SpecPlan::blu layout): chirp c[n] = e^{-i pi n^2/m} (n^2 mod 2m exactly), the
+// transforms / M of the kernels b_f[j] = conj c[|j|] (forward DFT, s = -1) and b_i[j] = c[|j|] (inverse, s = +1)
+// wrapped to length M, and the length-M twiddles e^{-2 pi i k/M}, k < M/2
+void bluestein_tables(uint32_t m, uint32_t M, std::vector<double>& out) {
+    const long double pi = 3.141592653589793238462643383279502884L;
+    std::vector<std::complex<long double>> c(m), bf(M, 0.0L), bi(M, 0.0L);
+    for (uint32_t n = 0; n < m; ++n) {
+        const uint64_t r = (uint64_t(n) * n) % (2 * uint64_t(m));
+        const long double ang = -pi * (long double)r / (long double)m;
+        c[n] = std::complex<long double>(cosl(ang), sinl(ang));
+    }
+    for (uint32_t j = 0; j < m; ++j) {
+        bf[j] = std::conj(c[j]);
+        bi[j] = c[j];
+        if (j > 0) {
+            bf[M - j] = std::conj(c[j]);
+            bi[M - j] = c[j];
+        }
+    }
+    fft_ld(bf);
+    fft_ld(bi);
+    for (uint32_t n = 0; n < m; ++n) {
+        out.push_back(double(c[n].real()));
+        out.push_back(double(c[n].imag()));
+    }
+    for (auto* v : {&bf, &bi})
+        for (uint32_t k = 0; k < M; ++k) {
+            out.push_back(double((*v)[k].real() / (long double)M));
+            out.push_back(double((*v)[k].imag() / (long double)M));
+        }
+    for (uint32_t k = 0; k < M / 2; ++k) {
+        const long double ang = -2.0L * pi * (long double)k / (long double)M;
+        out.push_back(double(cosl(ang)));
+        out.push_back(double(sinl(ang)));
+    }
+}
+
 // Device tables of the spectral solve. Twiddles and eigenvalues are evaluated in long double.
 mvtv_status spectral_plan(mvtv_problem* P) {
     std::vector<double> tw, twq, lam;
@@ -321,11 +389,24 @@ mvtv_status spectral_plan(mvtv_problem* P) {
             perm.push_back(pos);
         }
     }
+    // Bluestein tables of the lengths without a 2-3-5-7 plan (k_dctb; mvtv_spectral.hip)
+    std::vector<double> blu;
+    for (int j = 0; j < P->g.p; ++j) {
+        const uint32_t m = (P->slab && j == P->g.p - 1) ? uint32_t(P->m_global) : P->g.m[j];
+        int rad[8], nrad = 0;
+        sp.blu_M[j] = 0;
+        if (m > 4096 || dct_radix_plan(m, rad, &nrad)) continue;
+        const uint32_t M = bluestein_length(m);
+        sp.blu_M[j] = M;
+        sp.blu_off[j] = uint32_t(blu.size());
+        bluestein_tables(m, M, blu);
+    }
     auto up = [&](double** dst, const std::vector<double>& v) -> mvtv_status {
         MVTV_TRY(alloc(dst, v.size()));
         HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice));
         return MVTV_OK;
     };
+    if (!blu.empty()) MVTV_TRY(up(&sp.blu, blu));
     MVTV_TRY(up(&sp.tw, tw));
     MVTV_TRY(up(&sp.twq, twq));
     MVTV_TRY(up(&sp.lam, lam));
@@ -698,11 +779,11 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
         return s;
     }
     P->host_st = reinterpret_cast<PcgState*>(P->host_red + 16);
+    // cosine transforms of any length <= 4096: FFT plans for 2-3-5-7 lengths, Bluestein (k_dctb) for the rest
     P->spec_mesh = P->spec_pow2 = P->spec_lead = true;
     for (int j = 0; j < p; ++j) {
         const uint32_t mj = uint32_t(mg[j]);
-        int rad[8], nrad = 0;
-        if (mj > 4096 || !dct_radix_plan(mj, rad, &nrad)) {
+        if (mj > 4096) {
             P->spec_mesh = false;
             if (j < p - 1) P->spec_lead = false;
         }
@@ -852,9 +933,9 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     if (o.theta_solver < MVTV_SOLVER_AUTO || o.theta_solver > MVTV_SOLVER_PCG_SPECTRAL)
         return fail(MVTV_BAD_ARG, "theta_solver");
     if (o.theta_solver == MVTV_SOLVER_SPECTRAL && !spectral_ok(P))
-        return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and every m_j <= 4096 a product of 2, 3, 5, 7");
+        return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and every m_j <= 4096");
     if (o.theta_solver == MVTV_SOLVER_PCG_SPECTRAL && (!P->spec_mesh || P->wmode == W_NONE))
-        return fail(MVTV_BAD_ARG, "spectral preconditioner needs every m_j <= 4096 a product of 2, 3, 5, 7");
+        return fail(MVTV_BAD_ARG, "spectral preconditioner needs every m_j <= 4096");
     const bool spectral = o.theta_solver == MVTV_SOLVER_SPECTRAL ||
                           (o.theta_solver == MVTV_SOLVER_AUTO && spectral_ok(P));
     // AUTO with W != I on a spectral mesh: PCG with the spectral preconditioner (K an order of magnitude
@@ -1050,6 +1131,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         if (P->timing && it_done < int(mark.size()))   // iterations enqueued past the stop did no work
             for (size_t e = mark[size_t(it_done)]; e < P->pending.size(); ++e) P->pending[e].kid = -1;
         P->harvest();
+        if (P->timing && fold) P->fold_fix += c.nfix;
         if (o.fixed_iters <= 0 && c.status == 0) P->admm_hint = it_done + 1;
         if (it_done & 1) std::swap(P->guprev, P->gu);   // P->guprev holds D^T u of the current state
         if (fused && nbuf == 3) {   // the state is in ebuf[it_done % 3]
@@ -1609,7 +1691,7 @@ mvtv_status mvtv_lambda_max_cpp(mvtv_problem* P, double* out, int32_t* iters) {
 
 mvtv_status mvtv_solve_spectral(mvtv_problem* P, double sigma, const double* b, double* x_out) {
     if (!P || !b || !x_out) return fail(MVTV_BAD_ARG, "null argument");
-    if (!spectral_ok(P)) return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and every m_j <= 4096 a product of 2, 3, 5, 7");
+    if (!spectral_ok(P)) return fail(MVTV_BAD_ARG, "spectral theta-solve needs W = I and every m_j <= 4096");
     DeviceGuard dg(P->device);
     double* dx = nullptr;
     MVTV_TRY(alloc(&dx, P->g.N));
@@ -1641,6 +1723,7 @@ mvtv_status mvtv_timing_enable(mvtv_problem* P, int32_t on) {
         P->ms[k] = 0.0;
         P->launches[k] = 0;
     }
+    P->fold_fix = 0;
     return MVTV_OK;
 }
 
@@ -1671,7 +1754,9 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
         case MVTV_K_PCG_DIRECTION: b = 8.0 * ((3.0 + w) * N); break;    // r, p (+W) in, p out
         case MVTV_K_PCG_FUSED: b = 8.0 * ((6.0 + w) * N); break;        // x, r, p (+W) in, x, r, p out
         case MVTV_K_DCT_FIRST: b = 8.0 * 4.0 * N; break;                 // oty, g_alpha, g_u in, x out
-        case MVTV_K_DCT_FOLD: b = 8.0 * 3.0 * N; break;                  // oty, s in, x out (+ g_u after a rho change)
+        case MVTV_K_DCT_FOLD:   // oty, s in, x out; + g_u in the launches after a rho change (mean over the launches)
+            b = 8.0 * N * (3.0 + (P->launches[kid] > 0 ? double(P->fold_fix) / double(P->launches[kid]) : 0.0));
+            break;
         case MVTV_K_DCT: b = 8.0 * 2.0 * N; break;                       // x in, x out
         case MVTV_K_ADMM_FUSED: b = 8.0 * (4.0 * N + 2.0 * E); break;    // theta, z, g_uprev in; z', g_alpha, g_u out
         default: b = 0.0;

@@ -133,7 +133,8 @@ struct AdmmCtl {
     // oty + fold_ka s + fold_kb g_u, fold_ka = rho' / rho, fold_kb = rho' (c - 1): oty + s unless the control step
     // changed rho (fix != 0, the first pass also reads g_u)
     double fold_ka, fold_kb;
-    int32_t fix, pad2;
+    int32_t fix;
+    int32_t nfix;   // iterations after which fix was set and the loop went on (folded first passes reading g_u)
 };
 
 enum UMode { U_EXPLICIT = 0, U_FROM_Z = 1 };
@@ -248,6 +249,11 @@ struct SpecPlan {
     double* lam = nullptr;    // per dim: m_j eigenvalues 4 sin^2(pi k/(2 m_j)) of the Neumann Laplacian
     uint32_t* perm = nullptr; // per dim (at lam_off): position of sample k in the mixed-radix FFT's input order
     uint32_t tw_off[kMaxDims] = {0, 0, 0, 0}, twq_off[kMaxDims] = {0, 0, 0, 0}, lam_off[kMaxDims] = {0, 0, 0, 0};
+    // lengths without a 2-3-5-7 plan (Bluestein, k_dctb): per such dim, at blu_off (doubles), m complex chirp values
+    // e^{-i pi n^2/m}, then M values each of the forward and inverse kernels' transforms / M, then M/2 twiddles
+    // e^{-2 pi i k/M}; blu_M[j] = M = 2^ceil(log2(2 m_j - 1)), 0 for a planned dim
+    double* blu = nullptr;
+    uint32_t blu_off[kMaxDims] = {0, 0, 0, 0}, blu_M[kMaxDims] = {0, 0, 0, 0};
 };
 // PCG vector work folded into the d = 0 passes of a preconditioner solve (spectrally preconditioned PCG,
 // power-of-two m_0 >= 64): mode 1, first pass (`in` = r): r -= alpha q and x += alpha p on load (r, x
@@ -290,6 +296,8 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
 hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, int phase, double* x, double* coef,
                            const double* lr, uint32_t chunk, int lo_ext, int hi_ext, double scale,
                            const AdmmCtl* ctl, double sigma = 1.0, double w0 = 1.0, const int32_t* skip = nullptr);
+// a block of n planes splits into k_tris segments (<= 64 of <= 32 rows): false for e.g. a prime n > 64
+bool tri_slab_ok(uint32_t n);
 hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint32_t chunk, int G, const AdmmCtl* ctl,
                             const int32_t* skip = nullptr);
 // z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /

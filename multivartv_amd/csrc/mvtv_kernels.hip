@@ -415,6 +415,7 @@ __device__ __forceinline__ void admm_control_step(AdmmCtl* __restrict__ c, const
             c->done = 1;
         }
     }
+    if (!c->done) c->nfix += c->fix;   // the next folded first pass reads g_u too (bytes accounting)
 }
 
 // --------------------------------------------------------------------- reductions / scalars

@@ -125,6 +125,7 @@ struct mvtv_problem {
     std::vector<hipEvent_t> ev_pool;
     double ms[MVTV_K_COUNT] = {0};
     int64_t launches[MVTV_K_COUNT] = {0};
+    int64_t fold_fix = 0;   // timed folded first passes that also read g_u (a rho change before them)
 
     Launch L() const { return Launch{stream, grid}; }
 

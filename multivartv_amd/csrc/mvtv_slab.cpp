@@ -18,9 +18,10 @@
 //                then takes adapt_step / stopping on every rank from bit-identical inputs.
 //   z halo       (p = 3) last owned plane of z_new -> rank+1's ghost plane of the same buffer.
 // The collectives run on a stream of their own, handed their inputs by events, so the z halo overlaps the
-// next iteration's theta-solve. Transports (mvtv_comm): RCCL over xGMI (one process per GPU; librccl is
-// resolved at run time, reusing a copy already mapped) or an in-process loopback group (every rank on its
-// own host thread, device-to-device copies between the ranks' buffers): the same loop, testable on one GPU.
+// next iteration's theta-solve. Transports (mvtv_comm): RCCL over xGMI (one process per GPU; ROCm's
+// librccl.so.1 is dlopen'd at the first communicator, never torch's copy: see rccl_api) or an in-process
+// loopback group (every rank on its own host thread, device-to-device copies between the ranks' buffers):
+// the same loop, testable on one GPU.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -437,9 +438,9 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     if (!P->slab) return fail(MVTV_BAD_ARG, "not a slab problem (mvtv_problem_create_slab)");
     if (opts->variant != MVTV_VARIANT_RCPP) return fail(MVTV_BAD_ARG, "the slab loop runs variant B");
     if (P->wmode == W_NONE || !P->spec_lead || P->g.p < 2)
-        return fail(MVTV_BAD_ARG, "slab loop: W = I or diagonal, p >= 2, m_j <= 4096 products of 2, 3, 5, 7 for j < p - 1");
+        return fail(MVTV_BAD_ARG, "slab loop: W = I or diagonal, p >= 2, m_j <= 4096 for j < p - 1");
     if (C->size == 1 && !P->spec_mesh)
-        return fail(MVTV_BAD_ARG, "slab loop on one rank: the last dimension too must be <= 4096 and 2-3-5-7");
+        return fail(MVTV_BAD_ARG, "slab loop on one rank: the last dimension too must be <= 4096");
     if (!(lambda >= 0.0) || !(rho0 > 0.0)) return fail(MVTV_BAD_ARG, "lambda >= 0 and rho0 > 0");
     const auto t0 = std::chrono::steady_clock::now();
     DeviceGuard dg(P->device);
@@ -465,15 +466,21 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     {   // every rank must enqueue the same loop: the fused pass or not, the same edge layout (the z halo moves
         // whole planes in it), W or not. One sum of the flags, with the ranks' shares of sum W and sum W^2; a
         // mismatch fails on every rank alike
-        double flags[7] = {P->f3d ? 1.0 : 0.0, P->g.eaos ? 1.0 : 0.0, P->e3d ? 1.0 : 0.0, double(sg.plane),
-                           wd ? 1.0 : 0.0, P->wsum_own, P->wsum2_own};
+        // slot 7: this rank's block of every line can be cut into the line solves' segments (k_tris: <= 64
+        // segments of <= 32 rows); checked here, before any rank enters a collective the infeasible one would skip
+        const bool lines_ok = G == 1 || tri_slab_ok(sg.nz);
+        double flags[8] = {P->f3d ? 1.0 : 0.0, P->g.eaos ? 1.0 : 0.0, P->e3d ? 1.0 : 0.0, double(sg.plane),
+                           wd ? 1.0 : 0.0, P->wsum_own, P->wsum2_own, lines_ok ? 1.0 : 0.0};
         HIP_TRY(hipMemcpyAsync(P->red, flags, sizeof(flags), hipMemcpyHostToDevice, s));
-        MVTV_TRY(C->allreduce_sum(P->red, 7, s));
-        double sum[7];
+        MVTV_TRY(C->allreduce_sum(P->red, 8, s));
+        double sum[8];
         HIP_TRY(hipMemcpyAsync(sum, P->red, sizeof(sum), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         for (int k = 0; k < 5; ++k)
             if (sum[k] != double(G) * flags[k]) return fail(MVTV_BAD_ARG, "slab ranks disagree on the loop layout");
+        if (sum[7] != double(G))
+            return fail(MVTV_BAD_ARG, "slab line solves: a rank's block of the last dimension has no split into <= 64 "
+                                      "segments of <= 32 planes (e.g. a prime plane count above 64)");
         const double n_all = double(sg.plane) * double(sg.mg);
         if (wd) {
             w0 = sum[5] / n_all;
@@ -893,7 +900,9 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     // kernels, but their collectives still move their buffers
     const int limit = opts->fixed_iters > 0 ? opts->fixed_iters : max_counter + 1;
     // (W != I: one iteration per poll, the PCG needs the control block's sigma on the host)
-    int target = wd ? 1 : (opts->fixed_iters > 0 ? opts->fixed_iters : 16);
+    // (tolerance mode: the last converged run's count first, as the one-GPU loop, so a warm-started path enqueues
+    // few iterations past its stop; every rank holds the same hint)
+    int target = wd ? 1 : (opts->fixed_iters > 0 ? opts->fixed_iters : (P->admm_hint > 0 ? P->admm_hint : 16));
     int enq = 0;
     std::vector<size_t> mark;
     for (;;) {
@@ -911,6 +920,8 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     if (P->timing && it_done < int(mark.size()))
         for (size_t e = mark[size_t(it_done)]; e < P->pending.size(); ++e) P->pending[e].kid = -1;
     P->harvest();
+    if (P->timing && fold) P->fold_fix += c.nfix;
+    if (opts->fixed_iters <= 0 && c.status == 0) P->admm_hint = it_done + 1;
     if (it_done & 1) {
         std::swap(P->guprev, P->gu);
         if (fused) std::swap(P->edges, P->edges2);

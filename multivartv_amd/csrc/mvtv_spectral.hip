@@ -78,6 +78,11 @@ struct SpecArgs {
     int32_t xcd;              // k_dct8: tiles dealt to the XCDs in contiguous runs (grid a multiple of 8)
     PcgFuse pf;               // k_dct8 PC = 1 / 2: the PCG vector work of the preconditioner's d = 0 passes
     int32_t fold;             // FORMB from the folded s (k_dct8, ctl): b = in + fold_ka ga [+ fold_kb gb if ctl->fix]
+    // Bluestein lengths (k_dctb; L = log2 M then, tw = the length-M FFT twiddles): the chirp c[n] = e^{-i pi n^2/m}
+    // and the transforms / M of the forward / inverse convolution kernels
+    const double2* bchirp;
+    const double2* bvf;
+    const double2* bvi;
 };
 
 enum SpecMode { SPEC_FWD = 0, SPEC_INV = 1, SPEC_MID = 2 };
@@ -1600,6 +1605,267 @@ bool dct_radix_plan(uint32_t m, int* rad, int* nrad) {
 }
 
 // =============================================================================================
+// Any other length m <= 4096 (a prime factor >= 11: 31, 37, 79, 1009 ... the released R API's default mesh
+// m = floor(sqrt(n)) per dimension, rcpp-code/MultivarTV/R/MultivarTV.R:44-48, lands on such lengths). The
+// length-m complex DFT of the Makhoul pairing by Bluestein's chirp-z identity nk = (n^2 + k^2 - (k - n)^2) / 2:
+//
+//   Y[k] = c[k] sum_n (y[n] c[n]) b[k - n],   c[n] = e^{s i pi n^2 / m},  b[j] = conj c[j]   (s = -1 / +1)
+//
+// a linear convolution, evaluated as a circular one of length M = 2^ceil(log2(2m - 1)) with k_dct's radix-2^2
+// LDS FFT (fft_lines): the chirped input goes in at bit-reversed slots, the forward FFT leaves natural order,
+// the product with the transform of b (a per-dimension table, 1/M folded in) goes through the inverse FFT,
+// which leaves the convolution at bit-reversed slots again. So every length-m quantity lives at slot
+// brev_M(n): the Makhoul pairing (k, m - k), the MID divide and b formed on load are k_dctg's, read and
+// written there. Per line pair: two length-M FFTs per transform (four in a MID pass); fp64 round-off grows
+// as log M, like the planned FFTs'.
+namespace dctb {
+constexpr int NT = 256;   // spec::NT: fft_lines strides over the workgroup's threads
+}
+
+template <int MODE, bool D0, bool FORMB>
+__global__ __launch_bounds__(dctb::NT) void k_dctb(const SpecArgs a) {
+    double sigma = a.sigma, ca = a.ca, cb = a.cb;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+        ca = a.ctl->rho;
+        cb = a.ctl->rho * a.ctl->c_prev;
+    }
+    extern __shared__ double2 buf[];   // tq / 2 complex lines of M + PAD slots (launch-time size)
+    __shared__ double lc0[16], lc1[16];
+    const int m = int(a.m[a.d]);
+    const int L = a.L, M = 1 << L;     // a.L = log2 M here
+    const int tq = a.tq, ncl = tq >> 1, lncl = __ffs(ncl) - 1;
+    const int LP = M + spec::PAD;
+    const uint32_t q0 = blockIdx.x * uint32_t(tq);
+    const double2* __restrict__ chirp = a.bchirp;   // c[n] = e^{-i pi n^2 / m} (s = -1), n < m
+
+    if (MODE == SPEC_MID && threadIdx.x < uint32_t(tq)) {   // c0 + c1 lam_d(k) per line, as k_dctg
+        const uint32_t q = a.q_off + q0 + threadIdx.x;
+        double lamv[kMaxDims] = {0, 0, 0, 0};
+        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
+        const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
+        for (int j = 0; j < a.p; ++j) {
+            if (j == a.d) continue;
+            const uint32_t qq = (j < jlast) ? a.fd[j].div(rest) : 0u;
+            lamv[j] = a.lam[a.lam_off[j] + (rest - qq * a.m[j])];
+            rest = qq;
+        }
+        double c0 = a.w0, c1 = 0.0;
+        for (int S = 1; S < (1 << a.p); ++S) {
+            if (a.cS[S] == 0.0) continue;
+            double prod = sigma * a.cS[S];
+            for (int j = 0; j < a.p; ++j)
+                if (j != a.d && ((S >> j) & 1)) prod *= lamv[j];
+            if ((S >> a.d) & 1) c1 += prod;
+            else c0 += prod;
+        }
+        lc0[threadIdx.x] = c0;
+        lc1[threadIdx.x] = c1;
+    }
+
+    auto gaddr = [&](uint32_t ql, uint32_t k) -> uint32_t {
+        const uint32_t q = q0 + ql;
+        if (D0) return q * uint32_t(m) + k;
+        const uint32_t hi = a.fds.div(q);
+        return (q - hi * a.stride) + hi * a.stride * uint32_t(m) + k * a.stride;
+    };
+    auto slot = [&](int n) { return int(__brev(uint32_t(n)) >> (32 - L)); };
+    // (complex line, sample k) of work item e: lanes over k for d = 0 (contiguous lines), over the line pairs for
+    // a strided pass (the pair's two words are adjacent, the tile's pairs one row)
+    auto item = [&](int e, int& cl, int& k) {
+        if (D0) {
+            cl = int(a.fm.div(uint32_t(e)));
+            k = e - cl * m;
+        } else {
+            cl = e & (ncl - 1);
+            k = e >> lncl;
+        }
+    };
+    auto load_pair = [&](int cl, int k) -> double2 {
+        double v[2] = {0.0, 0.0};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t ql = uint32_t(2 * cl + h);
+            if (q0 + ql < a.nlines) {
+                const uint32_t gi = gaddr(ql, uint32_t(k));
+                v[h] = __builtin_nontemporal_load(a.in + gi);
+                if (FORMB)
+                    v[h] += ca * __builtin_nontemporal_load(a.ga + gi) + cb * __builtin_nontemporal_load(a.gb + gi);
+            }
+        }
+        return make_double2(v[0], v[1]);
+    };
+    // zero the convolution's padding slots n in [m, M)
+    auto zero_pad = [&]() {
+        const int np = ncl * (M - m);
+        for (int e = threadIdx.x; e < np; e += dctb::NT) {
+            const int cl = e / (M - m), n = m + (e - cl * (M - m));
+            buf[cl * LP + slot(n)] = make_double2(0.0, 0.0);
+        }
+    };
+    // circular convolution of every line with b (bhat = its transform / M): bit-reversed in and out
+    auto convolve = [&](const double2* __restrict__ bhat) {
+        fft_lines<false, false>(buf, a.tw, ncl, L, LP);
+        for (int e = threadIdx.x; e < ncl * M; e += dctb::NT) {
+            const int cl = e >> L, k = e & (M - 1);
+            buf[cl * LP + k] = cmul(buf[cl * LP + k], bhat[k]);
+        }
+        __syncthreads();
+        fft_lines<true, true>(buf, a.tw, ncl, L, LP);
+    };
+
+    // ---- load: forward / MID: y[n] c[n] at slot(n), n = the Makhoul position of sample k; inverse: X[k] at slot(k)
+    const int total = ncl * m;
+    for (int e = threadIdx.x; e < total; e += dctb::NT) {
+        int cl, k;
+        item(e, cl, k);
+        const double2 v = load_pair(cl, k);
+        if (MODE == SPEC_INV) {
+            buf[cl * LP + slot(k)] = v;
+        } else {
+            const int n = (k & 1) ? m - 1 - (k >> 1) : (k >> 1);
+            buf[cl * LP + slot(n)] = cmul(v, chirp[n]);
+        }
+    }
+    if (MODE != SPEC_INV) zero_pad();
+    __syncthreads();
+    if (MODE != SPEC_INV) convolve(a.bvf);
+
+    // ---- spectrum <-> DCT coefficients over the pairs (k, m - k) (k_dctg), at their slots ------------------
+    {
+        const int half = m >> 1, npl = (m & 1) ? half + 1 : half;
+        const int npairs = ncl * npl;
+        for (int t = threadIdx.x; t < npairs; t += dctb::NT) {
+            const int line = t / npl, k = t - line * npl;
+            double2* x = buf + line * LP;
+            const bool self = k == 0;
+            const bool mid = self && !(m & 1);
+            const int ka = k, kb = self ? half : m - k;
+            const int sa = slot(ka), sb = slot(kb);
+            double2 Xk, Xmk = make_double2(0.0, 0.0);
+            if (MODE != SPEC_INV) {   // Z[k] = c[k] conv[k]
+                const double2 Z1 = cmul(x[sa], chirp[ka]), q1 = a.twq[ka];
+                if (self) {
+                    Xk = make_double2(q1.x * Z1.x, q1.x * Z1.y);
+                    if (mid) {
+                        const double2 Z2 = cmul(x[sb], chirp[kb]), q2 = a.twq[kb];
+                        Xmk = make_double2(q2.x * Z2.x, q2.x * Z2.y);
+                    }
+                } else {
+                    const double2 Z2 = cmul(x[sb], chirp[kb]), q2 = a.twq[kb];
+                    const double2 Ap = make_double2(0.5 * (Z1.x + Z2.x), 0.5 * (Z1.y - Z2.y));
+                    const double2 Bp = make_double2(0.5 * (Z1.y + Z2.y), -0.5 * (Z1.x - Z2.x));
+                    Xk = make_double2(q1.x * Ap.x - q1.y * Ap.y, q1.x * Bp.x - q1.y * Bp.y);
+                    Xmk = make_double2(q2.x * Ap.x + q2.y * Ap.y, q2.x * Bp.x + q2.y * Bp.y);
+                }
+            } else {
+                Xk = x[sa];
+                if (!self || mid) Xmk = x[sb];
+            }
+            if (MODE == SPEC_MID) {
+                const double* lamd = a.lam + a.lam_off[a.d];
+                const int l0 = 2 * line, l1 = 2 * line + 1;
+                const double la = lamd[ka];
+                Xk.x *= a.inv_n / (lc0[l0] + lc1[l0] * la);
+                Xk.y *= a.inv_n / (lc0[l1] + lc1[l1] * la);
+                if (!self || mid) {
+                    const double lb = lamd[kb];
+                    Xmk.x *= a.inv_n / (lc0[l0] + lc1[l0] * lb);
+                    Xmk.y *= a.inv_n / (lc0[l1] + lc1[l1] * lb);
+                }
+            }
+            if (MODE == SPEC_FWD) {
+                x[sa] = Xk;
+                if (!self || mid) x[sb] = Xmk;
+                continue;
+            }
+            // V[k] = conj(q[k]) (X[k] - i X[m-k]), then the inverse transform's input chirp conj c[k]
+            const double2 q2 = cconj(a.twq[kb]);
+            if (self) {
+                x[sa] = cmul(Xk, cconj(chirp[0]));
+                if (mid) {
+                    const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xmk.x));
+                    const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xmk.y));
+                    x[sb] = cmul(make_double2(va2.x - vb2.y, va2.y + vb2.x), cconj(chirp[kb]));
+                }
+            } else {
+                const double2 q1 = cconj(a.twq[ka]);
+                const double2 va1 = cmul(q1, make_double2(Xk.x, -Xmk.x));
+                const double2 vb1 = cmul(q1, make_double2(Xk.y, -Xmk.y));
+                const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xk.x));
+                const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xk.y));
+                x[sa] = cmul(make_double2(va1.x - vb1.y, va1.y + vb1.x), cconj(chirp[ka]));
+                x[sb] = cmul(make_double2(va2.x - vb2.y, va2.y + vb2.x), cconj(chirp[kb]));
+            }
+        }
+        if (MODE != SPEC_FWD) zero_pad();   // (disjoint from the pairs' slots)
+        __syncthreads();
+    }
+
+    if (MODE != SPEC_FWD) convolve(a.bvi);
+
+    // ---- store: forward: X[k] from slot(k); inverse / MID: sample k = conj c[n] conv[n], n its Makhoul position
+    for (int e = threadIdx.x; e < total; e += dctb::NT) {
+        int cl, k;
+        item(e, cl, k);
+        double2 v;
+        if (MODE == SPEC_FWD) {
+            v = buf[cl * LP + slot(k)];
+        } else {
+            const int n = (k & 1) ? m - 1 - (k >> 1) : (k >> 1);
+            v = cmul(buf[cl * LP + slot(n)], cconj(chirp[n]));
+        }
+        const uint32_t ql = uint32_t(2 * cl);
+        if (q0 + ql < a.nlines) __builtin_nontemporal_store(v.x, a.out + gaddr(ql, uint32_t(k)));
+        if (q0 + ql + 1 < a.nlines) __builtin_nontemporal_store(v.y, a.out + gaddr(ql + 1, uint32_t(k)));
+    }
+}
+
+static hipError_t launch_dctb(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
+    const int M = 1 << a.L;
+    // <= 16 lines in <= 64 KB of LDS (two complex lines' worth at least); M = 8192 takes one line pair in 128 KB
+    int tq = 16;
+    while (tq > 2 && size_t(tq / 2) * size_t(M + spec::PAD) * sizeof(double2) > 65536) tq /= 2;
+    a.tq = tq;
+    const size_t smem = size_t(tq / 2) * size_t(M + spec::PAD) * sizeof(double2);
+    if (smem > 160 * 1024) return hipErrorInvalidValue;
+    const dim3 grid((a.nlines + uint32_t(tq) - 1) / uint32_t(tq)), block(dctb::NT);
+#define MVTV_DCTB(MODE, D0, FB)                                                                               \
+    do {                                                                                                       \
+        if (smem > 65536)                                                                                      \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dctb<MODE, D0, FB>),                    \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(smem));                  \
+        klaunch(k_dctb<MODE, D0, FB>, grid, block, uint32_t(smem), s, a);                                      \
+    } while (0)
+    if (mode == SPEC_FWD) {
+        if (d0) {
+            if (formb) MVTV_DCTB(SPEC_FWD, true, true);
+            else MVTV_DCTB(SPEC_FWD, true, false);
+        } else if (formb) {
+            MVTV_DCTB(SPEC_FWD, false, true);
+        } else {
+            MVTV_DCTB(SPEC_FWD, false, false);
+        }
+    } else if (mode == SPEC_INV) {
+        if (d0) MVTV_DCTB(SPEC_INV, true, false);
+        else MVTV_DCTB(SPEC_INV, false, false);
+    } else {
+        if (d0) {
+            if (formb) MVTV_DCTB(SPEC_MID, true, true);
+            else MVTV_DCTB(SPEC_MID, true, false);
+        } else if (formb) {
+            MVTV_DCTB(SPEC_MID, false, true);
+        } else {
+            MVTV_DCTB(SPEC_MID, false, false);
+        }
+    }
+#undef MVTV_DCTB
+    return hipGetLastError();
+}
+
+// =============================================================================================
 // Last dimension by a tridiagonal solve instead of DCT / divide / inverse DCT.
 //
 // After the forward transforms along dims 0..p-2, line q of the last dimension d carries the 1-D
@@ -2173,6 +2439,12 @@ static void tris_seg(uint32_t n, int* sl, int* nseg) {
     *nseg = int(n / s);
 }
 
+bool tri_slab_ok(uint32_t n) {
+    int sl = 0, nseg = 0;
+    tris_seg(n, &sl, &nseg);
+    return n >= 1 && sl <= 32 && nseg <= tris::NSMAX;
+}
+
 hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, int phase, double* x, double* coef,
                            const double* lr, uint32_t chunk, int lo_ext, int hi_ext, double scale,
                            const AdmmCtl* ctl, double sigma, double w0, const int32_t* skip) {
@@ -2196,7 +2468,7 @@ hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, in
     const uint32_t n = og.m[d];
     int sl = 0, nseg = 0;
     tris_seg(n, &sl, &nseg);
-    if (n < 1 || sl > 32 || nseg > tris::NSMAX || chunk == 0 || a.nlines % chunk != 0)
+    if (!tri_slab_ok(n) || chunk == 0 || a.nlines % chunk != 0)
         return hipErrorInvalidValue;
     const dim3 grid((a.nlines + uint32_t(tris::TQ) - 1) / uint32_t(tris::TQ)), block(uint32_t(tris::TQ * nseg));
     // segments of <= 16 rows (blocks up to 1024 planes) keep the row registers at 16
@@ -2529,15 +2801,18 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
         a.pf = *pf;
     }
     if ((1u << a.L) != m || (1u << a.ls) != a.stride) {   // mixed radix, or a power of two over a general stride
-        if (!dct_radix_plan(m, a.rad, &a.nrad)) return hipErrorInvalidValue;
+        const bool planned = dct_radix_plan(m, a.rad, &a.nrad);
+        if (!planned && sp.blu_M[d] == 0) return hipErrorInvalidValue;
         a.fds = FastDiv(a.stride);
         a.fm = FastDiv(m);
-        for (int st = 0, L = 1; st < a.nrad; ++st) {
-            a.fper[st] = FastDiv(m / uint32_t(a.rad[st]));
-            a.fL[st] = FastDiv(uint32_t(L));
-            L *= a.rad[st];
+        if (planned) {
+            for (int st = 0, L = 1; st < a.nrad; ++st) {
+                a.fper[st] = FastDiv(m / uint32_t(a.rad[st]));
+                a.fL[st] = FastDiv(uint32_t(L));
+                L *= a.rad[st];
+            }
+            a.perm = sp.perm + sp.lam_off[d];
         }
-        a.perm = sp.perm + sp.lam_off[d];
         if (mode == SPEC_MID && d > 0 && !formb && a.nlines / uint32_t(trig::TQ) >= 256u && !probe_env("MVTV_DCT_TRI0")) {
             const int sl = trig_seg(m);
             if (sl > 0) {
@@ -2546,6 +2821,16 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
                 klaunch(k_trig, grid, dim3(trig::TQ * nseg), 0, s, a, sl, nseg);
                 return hipGetLastError();
             }
+        }
+        if (!planned) {   // Bluestein (k_dctb): L = log2 M, the length-M twiddles
+            const double2* t = reinterpret_cast<const double2*>(sp.blu + sp.blu_off[d]);
+            a.L = 0;
+            while ((1u << a.L) < sp.blu_M[d]) ++a.L;
+            a.bchirp = t;
+            a.bvf = t + m;
+            a.bvi = t + m + sp.blu_M[d];
+            a.tw = t + m + 2 * sp.blu_M[d];
+            return launch_dctb(a, s, mode, d == 0, formb);
         }
         if (launch_dctm(a, s, mode, d == 0, formb)) return hipGetLastError();
         // <= 16 lines (128-B rows for d > 0) in <= 64 KB of LDS

@@ -159,8 +159,8 @@ class _Slab(_lib.Problem):
 
 
 class SlabADMM:
-    """Variant-B ADMM on one rank's slab of a mesh fit (p >= 2; m_j for j < p - 1 products of 2, 3, 5, 7 up to
-    4096, the last dimension any length over >= 2 ranks).
+    """Variant-B ADMM on one rank's slab of a mesh fit (p >= 2; m_j <= 4096 for j < p - 1, the last dimension
+    any length over >= 2 ranks).
 
     ``oty_owned``: O^T y on the owned planes (= y for lattice data, W y for a diagonal W). ``ymean``: theta_0
     (the global mean of y, rcpp…/solvers.cpp:207). ``comm``: a :class:`Comm` (its rank / size fix the slab).

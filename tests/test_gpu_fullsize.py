@@ -85,6 +85,20 @@ def test_config5_tile_shapes_4d_vs_c_oracle():
     _vs_c_oracle([128, 128, 128, 16], 2)
 
 
+@pytest.mark.timeout(300)
+def test_config3_256_cubed_vs_c_oracle():
+    """Config 3 at its own kernel geometry: k_admm3a at 256^3 runs 76 tiles x 10 dim-2 chunks of 26 planes with a
+    ragged 22-plane last chunk (mvtv_admm3d.hip f3d_args), which the 64^3 / 128^3 / 512^3 cases never take."""
+    _vs_c_oracle([256, 256, 256], 2)
+
+
+@pytest.mark.timeout(900)
+def test_config5_128_4d_vs_c_oracle():
+    """Config 5 at its own kernel geometry: k_edge4d marching all 128 w-planes and k_gather4a's 2 z-chunks of 64
+    (16 chunks of 8 at 128 x 128 x 128 x 16). One iteration: the C oracle holds ~160 GB of host edge state."""
+    _vs_c_oracle([128, 128, 128, 128], 1)
+
+
 def test_metric_config_512_cubed():
     ss, sp = _two_solvers([512, 512, 512], 3)
     assert sp["pcg_unconverged"] == 0

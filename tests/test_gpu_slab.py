@@ -82,9 +82,44 @@ def test_loopback_failing_rank_does_not_hang_its_peers():
         c.close()
 
 
-@pytest.mark.parametrize("m,world", [([60, 60, 45], 3), ([24, 24, 37], 2), ([48, 48, 130], 4), ([40, 100], 4)],
+def test_uneven_infeasible_line_split_fails_on_every_rank():
+    """m_global = 133 over 2 ranks: 66 and 67 planes. Only the 67-plane block (prime, > 64) has no split into the
+    line solves' segments; the ranks' layout agreement carries that flag, so BOTH fail with MVTV_BAD_ARG before the
+    first collective (over RCCL the 66-plane rank would otherwise wait in the coefficient all-to-all forever)."""
+    import threading
+    m, lam = [8, 8, 133], 1.0
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    comms = slab.Comm.local_group(2)
+    b = slab.plane_bounds(m[-1], 2)
+    assert [b[1] - b[0], b[2] - b[1]] == [66, 67]
+    ranks = [slab.SlabADMM(m, y[b[r] * 64:b[r + 1] * 64], deltas, float(y.mean()), comms[r]) for r in range(2)]
+    errs = [None, None]
+
+    def work(r):
+        try:
+            ranks[r].run(lam, fixed_iters=2)
+        except Exception as e:   # noqa: BLE001
+            errs[r] = e
+
+    ts = [threading.Thread(target=work, args=(r,)) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in ts)
+    for e in errs:
+        assert isinstance(e, mv.MvtvError) and "line solves" in str(e), e
+    for r in ranks:
+        r.close()
+    for c in comms:
+        c.close()
+
+
+@pytest.mark.parametrize("m,world", [([60, 60, 45], 3), ([24, 24, 37], 2), ([48, 48, 130], 4), ([40, 100], 4),
+                                     ([31, 31, 40], 2), ([24, 24, 37], 1)],
                          ids=["3d_60x60x45_w3_mixed_radix", "3d_24x24x37_w2_prime_last", "3d_48x48x130_w4",
-                              "2d_40x100_w4"])
+                              "2d_40x100_w4", "3d_31x31x40_w2_bluestein_lead", "3d_24x24x37_w1_bluestein_last"])
 def test_slab_any_last_dimension_vs_c_oracle(m, world):
     """The last dimension's line solves are substructured over the ranks, so it may have any length (37 is
     prime; 45, 130 not powers of two) and the leading dims any 2-3-5-7 length (k_dctg passes): 12 fixed
@@ -103,9 +138,10 @@ def test_slab_any_last_dimension_vs_c_oracle(m, world):
 
 
 def test_slab_one_rank_needs_a_spectral_last_dimension():
-    y = towers([24, 24, 37])
+    """One rank solves the last dimension locally: any length up to 4096 (Bluestein past 2-3-5-7), not above."""
+    y = towers([4, 4, 4099])
     comm = slab.Comm.local_group(1)[0]
-    S = slab.SlabADMM([24, 24, 37], y, [(1.0 + 2e-4) / v for v in (24, 24, 37)], y.mean(), comm)
+    S = slab.SlabADMM([4, 4, 4099], y, [(1.0 + 2e-4) / v for v in (4, 4, 4099)], y.mean(), comm)
     with pytest.raises(mv.MvtvError):
         S.run(1.0, fixed_iters=2)
     S.close()

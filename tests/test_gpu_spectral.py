@@ -51,7 +51,15 @@ CASES = [([2], None, "cpp", False), ([8], None, "cpp", False), ([1024], None, "p
          # at 500^3 below: unequal dims are refused at p >= 3, the reference's mixed-partial rule)
          ([500, 6], [0.3, 0.7], "cpp", False), ([1000, 4], None, "py", False),
          # an odd number of lines: k_dctm pairs lines, so these fall back to k_dctg
-         ([500, 7], [0.3, 0.7], "cpp", False), ([1000, 3], None, "py", False)]
+         ([500, 7], [0.3, 0.7], "cpp", False), ([1000, 3], None, "py", False),
+         # lengths with a prime factor >= 11 (Bluestein, k_dctb): FWD / INV along dim 0, MID along a 1-D mesh, a
+         # strided MID along the last dimension (few lines, and 4096 lines of a prime length k_trig cannot split),
+         # M = 8192 (one line pair in 128 KB of LDS), the R API's default m = floor(sqrt(n)) (31 at n = 1000)
+         ([31], None, "cpp", False), ([1009], None, "py", False), ([4093], None, "cpp", False),
+         ([37, 37], [0.3, 0.7], "cpp", False), ([22, 13], None, "py", False), ([4096, 67], [0.5, 0.5], "cpp", False),
+         ([67, 4096], None, "cpp", False), ([2039, 6], [0.3, 0.7], "cpp", False),
+         ([11, 11, 11], [0.2, 0.3, 0.4], "cpp", False), ([8, 8, 11], [0.5, 0.25, 0.125], "cpp", False),
+         ([31, 31, 31], None, "py", False), ([11, 11, 11, 11], [0.1, 0.2, 0.3, 0.4], "cpp", False)]
 
 
 def _problem(m, deltas, order, unit, seed=0):
@@ -80,10 +88,11 @@ def test_spectral_vs_superlu(m, deltas, order, unit, sigma):
 
 
 @pytest.mark.parametrize("m", [[256, 256, 256], [1024, 1024], [64, 64, 64, 64], [100, 100, 100], [240, 240, 240],
-                               [60, 60, 60, 60], [500, 500, 500], [1000, 1000]])
+                               [60, 60, 60, 60], [500, 500, 500], [1000, 1000], [1009, 1009], [251, 251, 251],
+                               [2039, 2048]])
 def test_spectral_residual_baseline_sizes(m):
-    """Config-sized meshes (3D 256^3, 2D 1024^2; 4D at 64^4) and mixed-radix ones (k_dctg / k_dctm passes,
-    k_trig last dimension): residual through the stencil operator."""
+    """Config-sized meshes (3D 256^3, 2D 1024^2; 4D at 64^4), mixed-radix ones (k_dctg / k_dctm passes,
+    k_trig last dimension) and prime lengths (k_dctb): residual through the stencil operator."""
     p = len(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     N = int(np.prod(m))
@@ -110,14 +119,18 @@ def test_spectral_matches_pcg_large():
 
 def test_spectral_rejected_when_not_exact():
     rng = np.random.default_rng(0)
-    with mv.Problem([22, 8], rng.standard_normal(176), deltas=[1, 1]) as P:      # 22 = 2 * 11
+    with mv.Problem([4099, 2], rng.standard_normal(8198), deltas=[1, 1]) as P:      # m_0 > 4096
         assert not P.spectral_ok()
         with pytest.raises(mv.MvtvError):
-            P.solve_spectral(1.0, np.zeros(176))
+            P.solve_spectral(1.0, np.zeros(8198))
         with pytest.raises(mv.MvtvError):
-            P.admm(1.0, np.zeros(176), u=np.zeros(P.E), rho=0.2, theta_solver=mv.SOLVER_SPECTRAL)
-        _, _, _, st = P.admm(1.0, np.zeros(176), u=np.zeros(P.E), rho=0.2, fixed_iters=2)
+            P.admm(1.0, np.zeros(8198), u=np.zeros(P.E), rho=0.2, theta_solver=mv.SOLVER_SPECTRAL)
+        _, _, _, st = P.admm(1.0, np.zeros(8198), u=np.zeros(P.E), rho=0.2, fixed_iters=2)
         assert st["theta_solver"] == mv.SOLVER_PCG
+    with mv.Problem([22, 8], rng.standard_normal(176), deltas=[1, 1]) as P:      # 22 = 2 * 11: Bluestein
+        assert P.spectral_ok()
+        _, _, _, st = P.admm(1.0, np.zeros(176), u=np.zeros(P.E), rho=0.2, fixed_iters=2)
+        assert st["theta_solver"] == mv.SOLVER_SPECTRAL
     with mv.Problem([8, 8], rng.standard_normal(64), wdiag=rng.uniform(0, 2, 64).round(), deltas=[1, 1]) as P:
         assert not P.spectral_ok()                                               # W != I
         _, _, _, st = P.admm(1.0, np.zeros(64), u=np.zeros(P.E), rho=0.2, fixed_iters=2)
@@ -210,7 +223,8 @@ def _fold_problem(m, k, seed):
     return W, W * y
 
 
-@pytest.mark.parametrize("case", ["scat_32x32", "scat_16x16x16", "fold_64x64", "fold_16x16x16"])
+@pytest.mark.parametrize("case", ["scat_32x32", "scat_16x16x16", "fold_64x64", "fold_16x16x16", "scat_31x31",
+                                  "fold_37x37", "scat_11x11x11"])
 def test_spectrally_preconditioned_pcg(case):
     """W != I (scattered data, CV folds): PCG preconditioned by S (mean(W) I + sigma D^T D) S (the middle
     factor applied exactly by cosine transforms) reproduces the SuperLU trajectory like Jacobi-PCG."""
@@ -258,3 +272,59 @@ def test_async_loop_max_counter(variant, monkeypatch):
     assert sa["status"] == ss["status"] == 1          # MVTV_MAXITER
     assert sa["iters"] == ss["iters"] and ra == rs
     assert _rel(ta, ts) <= 1e-12
+
+
+@pytest.mark.parametrize("m", [[31, 31, 31], [37, 37], [11, 11, 11, 11], [67, 67, 31]],
+                         ids=["31^3", "37^2", "11^4", "67x67x31"])
+def test_bluestein_admm_vs_c_oracle(m):
+    """Prime lengths through the bench's loop (asynchronous control, b formed on load by k_dctb's first pass, the
+    fused edge kernels) against the C oracle's variant-B loop with scipy.fft's exact solve (any length):
+    rcpp-code/MultivarTV/src/solvers.cpp:110-133, 12 fixed iterations, rho exact, theta / u 1e-10."""
+    from multivartv_amd.synth import towers
+    from oracle import c_oracle
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    lam, rho0, fixed = 0.8, 0.16, 12
+    th0 = np.full(y.size, y.mean())
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        assert P.spectral_ok()
+        P.state_set(th0, None, rho0)
+        st = P.run(lam, fixed_iters=fixed)
+        tg, ug, rg = P.state_get(want_u=True)
+    assert st["theta_solver"] == mv.SOLVER_SPECTRAL and st["iters"] == fixed
+    th, u = th0.copy(), np.zeros(c_oracle.num_edges(m))
+    ref = c_oracle.admm_rcpp_spectral(m, y, lam, th, u, rho0, deltas, fixed_iters=fixed)
+    assert rg == ref["rho"]
+    assert _rel(tg, th) <= 1e-10
+    assert np.max(np.abs(ug - u)) <= 1e-10 * max(1.0, np.max(np.abs(u)))
+    assert st["r_norm"] == pytest.approx(ref["r_norm"], rel=1e-9)
+
+
+def test_r_default_mesh_scattered_fold_takes_spectral_pcg():
+    """The released R API's default mesh for n = 1000 points, m = floor(sqrt(n)) = 31 per dimension
+    (rcpp-code/MultivarTV/R/MultivarTV.R:44-48), one CV fold of scattered data (W = training counts): AUTO takes PCG
+    with the cosine-transform preconditioner (Bluestein at 31), K-bar < 50 per theta-solve (Jacobi-PCG needs
+    several times that), and the trajectory matches the SuperLU oracle (rcpp…/solvers.cpp:113)."""
+    m, n = [31, 31], 1000
+    rng = np.random.default_rng(17)
+    x = rng.uniform(0, 1, size=(n, 2))
+    yv = np.where(np.all(x > 0.6, axis=1), 1.0, 0.0) + 0.3 * rng.standard_normal(n)
+    train = rng.permutation(n) % 5 != 0
+    axes = [np.linspace(0.0, 1.0, v) for v in m]
+    idx = np.abs(x[:, :1] - axes[0][None, :]).argmin(axis=1) + 31 * np.abs(x[:, 1:] - axes[1][None, :]).argmin(axis=1)
+    W = np.bincount(idx[train], minlength=961).astype(float)
+    oty = np.bincount(idx[train], weights=yv[train], minlength=961)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    D = O.build_D(m, O.block_table(2, deltas, "cpp"))
+    lam, rho0, fixed = 0.5, 0.1, 20
+    th0 = np.full(W.size, oty.sum() / W.sum())
+    ref = O.admm_rcpp(D, oty, W, lam, th0, np.zeros(D.shape[0]), rho0, fixed_iters=fixed)
+    with mv.Problem(m, oty, wdiag=W, deltas=deltas, order=mv.ORDER_CPP) as P:
+        th, u, rho, st = P.admm(lam, th0, u=np.zeros(P.E), rho=rho0, fixed_iters=fixed, pcg_rtol=1e-13)
+        _, _, _, sj = P.admm(lam, th0, u=np.zeros(P.E), rho=rho0, fixed_iters=fixed, pcg_rtol=1e-13,
+                             theta_solver=mv.SOLVER_PCG)
+    assert st["theta_solver"] == mv.SOLVER_PCG_SPECTRAL and rho == ref.rho
+    assert _rel(th, ref.theta) <= 1e-9
+    kbar, kjac = st["pcg_iters"] / fixed, sj["pcg_iters"] / fixed
+    print(f"31 x 31 scattered fold: K-bar spectral {kbar:.1f}, Jacobi {kjac:.1f}")
+    assert kbar < 50 and kbar < kjac
