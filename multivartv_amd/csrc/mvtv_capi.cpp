@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <complex>
+#include <cstdint>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -137,6 +138,9 @@ void free_all(mvtv_problem* P) {
         (void)hipEventDestroy(pd.b);
     }
     for (auto e : P->ev_pool) (void)hipEventDestroy(e);
+    for (auto& lg : P->graphs)
+        if (lg.exec) (void)hipGraphExecDestroy(lg.exec);
+    P->graphs.clear();
     if (P->stream) (void)hipStreamDestroy(P->stream);
     if (P->comm_stream) (void)hipStreamDestroy(P->comm_stream);
 }
@@ -280,6 +284,18 @@ mvtv_status pcg_solve(mvtv_problem* P, double sigma, const double* oty, const do
 }
 
 bool spectral_ok(const mvtv_problem* P) { return P->spec_mesh && P->wmode == W_IDENTITY; }
+
+// Graph replay of the asynchronous loop: probe builds only (MVTV_ADMM_GRAPH=1). Measured slower than the stream
+// launches it replaces, one process each, event-free (tools/launch_gap_probe.py, profiles/r04/v1_launch_gap):
+// 1024^2 13510 against 14083 ADMM it/s, 2048^2 6088 against 6187. The ~37 us of "gaps" per 1024^2 iteration that
+// the round-3 trace showed were the per-launch timing events (10105 it/s with them).
+bool admm_graph_enabled() {
+    static const bool on = [] {
+        const char* e = probe_env("MVTV_ADMM_GRAPH");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
 
 // M = 2^ceil(log2(2m - 1)): the circular convolution length of Bluestein's identity for length m
 uint32_t bluestein_length(uint32_t m) {
@@ -430,6 +446,32 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
         return e ? std::atoi(e) : -1;
     }();
     const int mid = (mid_env >= 1 && mid_env < p) ? mid_env : p - 1;
+    // 3-D: dim 2 forward (b formed on load), the two marching passes (dim-0 transforms + the dim-1 line solves),
+    // dim 2 inverse: 9N words instead of 11N
+    if (!P->slab && march_ok(P->g)) {
+        int h = P->tstart(ga ? (fold ? MVTV_K_DCT_FOLD : MVTV_K_DCT_FIRST) : MVTV_K_DCT);
+        if (ga && fold)
+            HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 0, 2, oty, ga, 1.0, gb, 0.0, x, sigma, w0, ctl, 0, 0.0, skip,
+                                    nullptr, true));
+        else if (ga)
+            HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 0, 2, oty, ga, ca, gb ? gb : ga, gb ? cb : 0.0, x, sigma, w0,
+                                    ctl, 0, 0.0, skip));
+        else
+            HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 0, 2, oty, nullptr, 0.0, nullptr, 0.0, x, sigma, w0, ctl, 0,
+                                    0.0, skip));
+        P->tstop(h);
+        h = P->tstart(MVTV_K_DCT);
+        HIP_TRY(launch_march(P->spec, P->g, P->stream, false, x, sigma, w0, ctl, skip));
+        P->tstop(h);
+        h = P->tstart(MVTV_K_DCT);
+        HIP_TRY(launch_march(P->spec, P->g, P->stream, true, x, sigma, w0, ctl, skip));
+        P->tstop(h);
+        h = P->tstart(MVTV_K_DCT);
+        HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 1, 2, x, nullptr, 0.0, nullptr, 0.0, x, sigma, w0, ctl, 0, 0.0,
+                                skip));
+        P->tstop(h);
+        return MVTV_OK;
+    }
     int order[MVTV_MAX_DIMS], n = 0;
     for (int d = 0; d < p; ++d)
         if (d != mid) order[n++] = d;
@@ -1055,7 +1097,8 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         // FOLD (variant B): the fused 3-D kernel stores s = rho (D^T alpha + D^T u) in P->ga instead of D^T alpha, so
         // the next solve's first pass reads oty and s (2N words) instead of oty, D^T alpha and D^T u (3N); after a
         // control step that changed rho it forms oty + (rho'/rho) s + rho' (c - 1) D^T u (AdmmCtl::fold_ka / _kb)
-        const uint32_t m0 = P->g.m[0];
+        // (the first pass transforms dim 0, or dim 2 on k_march meshes)
+        const uint32_t m0 = (!P->slab && march_ok(P->g)) ? P->g.m[2] : P->g.m[0];
         const bool fold_path = fused ? (P->g.p == 2 || P->g.p == 3)
                                      : (P->g.p == 4 && P->e3d && P->g4 != nullptr && gather4_ok(P->g));   // two-pass 4-D
         const bool fold = fold_path && variant == MVTV_VARIANT_RCPP && m0 >= 8 && m0 <= 4096 &&
@@ -1115,10 +1158,48 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         const int limit = o.fixed_iters > 0 ? o.fixed_iters
                                             : (variant == MVTV_VARIANT_PY ? max_counter : max_counter + 1);
         int target = o.fixed_iters > 0 ? o.fixed_iters : (P->admm_hint > 0 ? P->admm_hint : 16);
+        // Iterations j >= 1 repeat with period 2 (the z and D^T u ping-pongs), so iterations (odd j, j + 1) can be
+        // replayed as one captured HIP graph instead of ~10 stream launches: without per-launch events, for meshes
+        // whose launches are short enough for the launch path to matter (< 2^24 nodes)
+        hipGraphExec_t gexec = nullptr;
+        if (!P->timing && nbuf == 2 && P->g.N < (uint32_t(1) << 24) && admm_graph_enabled()) {
+            const std::vector<const void*> key = {P->theta, P->oty, P->ga, P->thold, gbuf[0], gbuf[1], ebuf[0], ebuf[1],
+                                                  reinterpret_cast<const void*>(uintptr_t(fold)),
+                                                  reinterpret_cast<const void*>(uintptr_t(track_theta)),
+                                                  reinterpret_cast<const void*>(uintptr_t(fused))};
+            auto it = std::find_if(P->graphs.begin(), P->graphs.end(), [&](const auto& lg) { return lg.key == key; });
+            if (it == P->graphs.end()) {
+                // capture iterations 1 and 2; any failure leaves stream launches for this key (best effort)
+                mvtv_problem::LoopGraph lg;
+                lg.key = key;
+                hipGraph_t gr = nullptr;
+                if (hipStreamBeginCapture(P->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+                    const bool ok = enqueue(1) == MVTV_OK && enqueue(2) == MVTV_OK;
+                    const bool ended = hipStreamEndCapture(P->stream, &gr) == hipSuccess;
+                    if (ok && ended && gr && hipGraphInstantiate(&lg.exec, gr, nullptr, nullptr, 0) != hipSuccess)
+                        lg.exec = nullptr;
+                    if (gr) (void)hipGraphDestroy(gr);
+                }
+                (void)hipGetLastError();
+                if (P->graphs.size() >= 4) {   // the two z / D^T u parities of a few buffer sets
+                    if (P->graphs.front().exec) (void)hipGraphExecDestroy(P->graphs.front().exec);
+                    P->graphs.erase(P->graphs.begin());
+                }
+                P->graphs.push_back(lg);
+                it = P->graphs.end() - 1;
+            }
+            gexec = it->exec;
+        }
+        const bool use_graph = gexec != nullptr;
         std::vector<size_t> mark;   // first timing entry of each enqueued iteration
         int enq = 0;
         for (;;) {
             while (enq < target && enq < limit) {
+                if (use_graph && (enq & 1) && enq + 2 <= std::min(target, limit)) {
+                    HIP_TRY(hipGraphLaunch(gexec, P->stream));
+                    enq += 2;
+                    continue;
+                }
                 mark.push_back(P->pending.size());
                 MVTV_TRY(enqueue(enq++));
             }

@@ -277,6 +277,13 @@ bool plane_pass_ok(const Geom& g);
 hipError_t launch_plane_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int mode, const double* in,
                              const double* ga, double ca, const double* gb, double cb, double* out,
                              const AdmmCtl* ctl = nullptr, const int32_t* skip = nullptr, bool fold = false);
+// 3-D meshes solved as dim-2 forward pass, k_march forward, k_march backward, dim-2 inverse pass (m0 a power of two in
+// [256, 2048], m1 a multiple of the march step, 128 <= m2 <= 4096)
+bool march_ok(const Geom& g);
+// the marching passes over every dim-2 frequency plane of x, in place: forward (dim-0 DCT of the rows + Thomas
+// forward elimination along dim 1) or backward (back substitution + inverse dim-0 DCT, scaled by m1 / N)
+hipError_t launch_march(const SpecPlan& sp, const Geom& g, hipStream_t s, bool bwd, double* x, double sigma, double w0,
+                        const AdmmCtl* ctl = nullptr, const int32_t* skip = nullptr);
 // true when the d = 0 passes of this mesh run in k_dct8 with their partial rows within partial_words
 bool dct_pcg_fusable(const Geom& g, size_t partial_words);
 // radices (8, 4, 2, 3, 5, 7 in stage order) of a line length m = 2^a 3^b 5^c 7^d; false for any other m

@@ -100,6 +100,13 @@ struct mvtv_problem {
     AdmmCtl* ctl = nullptr;       // device control block of the asynchronous ADMM loop
     AdmmCtl* host_ctl = nullptr;  // pinned mirror
     int admm_hint = 0;            // ADMM iterations of the last converged run (enqueue-ahead depth)
+    // the asynchronous loop's two-iteration launch sequence captured as a HIP graph (mvtv_capi.cpp), valid while the
+    // buffers and flags it was captured with (graph_key) are unchanged
+    struct LoopGraph {
+        std::vector<const void*> key;
+        hipGraphExec_t exec = nullptr;   // nullptr: the capture failed, stream launches for this key
+    };
+    std::vector<LoopGraph> graphs;
 
     // slab decomposition (mvtv_problem_create_slab): this problem holds planes [zb, ze) of dim p-1
     // of a mesh with m_global planes, plus ghost planes below / above

@@ -999,6 +999,261 @@ __global__ __launch_bounds__((1 << L) / 2 * (1 << L) / 8) void k_plane8(const Sp
 }
 
 // =============================================================================================
+// 3-D meshes: the dim-0 transforms and the tridiagonal solve along dim 1 in two marching passes.
+//
+// Transforms along different dimensions commute, so a 3-D solve can run the dim-2 forward transform first (b formed
+// on load) and leave dims 0 and 1 for last: after the dim-0 and dim-2 transforms, line (k0, k2) along dim 1 carries
+// c0 I + c1 T (k_tri's operator). A workgroup owns one dim-2 frequency plane (m0 x m1, contiguous) and marches
+// its rows (dim-1 positions), NR at a time:
+//   forward  (k_march<L, false>): DCT-II of the NR rows along dim 0 (k_dct8's register radix-8 stages), then one
+//            Thomas forward-elimination step per row for every k0 line, x'_i = (g_i - A x'_{i-1}) / den_i, the
+//            previous row's x' carried in registers; x' written in place;
+//   backward (k_march<L, true>): rows in reverse, x_i = x'_i - (A / den_i) x_{i+1}, then the inverse DCT along
+//            dim 0 of the NR rows; theta written in place (scaled by inv_n m1).
+// The dim-1 forward / inverse transform passes and the separate tridiagonal pass become these two: a 3-D solve
+// moves 9N words instead of 11N (the first pass 3N, then 2N each).
+//
+// The backward sweep needs den_i in reverse order, which the forward recurrence den_i = B - A^2 / den_{i-1}
+// cannot give without storing it. Its closed form does: den_i = p_{i+1} / p_i with p_{i+1} = B p_i - A^2 p_{i-1},
+// p_0 = 1, p_1 = B0 = c0 + c1 (the Neumann first row), so with the roots l1 > l2 of l^2 - B l + A^2 and
+// q = l2 / l1, r = beta / alpha:
+//     den_i = l1 (1 + r q^{i+1}) / (1 + r q^i),  l1 = (B + s) / 2,  s = sqrt(c0 (c0 + 4 c1)),
+//     r = 4 c0 c1 / (c0 + s)^2,  q = 4 c1^2 / (B + s)^2,  1 - q = (c0 + s)(B + s + 2 c1) / (B + s)^2
+//     (B = c0 + 2 c1, A = -c1)
+// every term free of cancellation (a numpy study against long-double Thomas: as accurate as fp64 Thomas for
+// c1 / c0 from 1e-2 to 1e7). The last row subtracts c1 (Neumann end). Both sweeps evaluate the same closed form,
+// so they apply one factorisation; q^i comes from one exp per line per step, then q-multiplications over the
+// step's rows.
+namespace march {
+template <int L>
+struct Shape {
+    static constexpr int M = 1 << L;
+    static constexpr int TPL = M / 8;          // FFT threads per complex line (k_dct8's D0 mapping)
+    static constexpr int NCL = 2048 / M;       // complex lines = row pairs per step
+    static constexpr int NR = 2 * NCL;         // rows per step
+    static constexpr int NT = NCL * TPL;       // 256 threads
+    static constexpr int LPT = M / NT;         // k0 lines per thread in the elimination
+};
+}  // namespace march
+
+template <int L, bool BWD>
+__global__ __launch_bounds__(256) void k_march(const SpecArgs a, uint32_t m1) {
+    using S = spec8::Shape<L>;
+    using T = march::Shape<L>;
+    constexpr int M = T::M, TPL = T::TPL, NCL = T::NCL, NR = T::NR, NT = T::NT, LPT = T::LPT, R0 = S::R0;
+    static_assert(NT == 256 && LPT >= 1, "k_march: 256 threads, m0 in [256, 2048]");
+    double sigma = a.sigma;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+    }
+    __shared__ double2 buf[NCL * S::LP];   // FFT exchange (k_dct8's slot layout)
+    __shared__ double C[NR * M];          // the step's coefficients [row][k0]
+    const uint32_t e = blockIdx.x;        // dim-2 frequency
+    const uint32_t pb = e * (uint32_t(M) * m1);
+    const int t = threadIdx.x;
+    const int j = t % TPL, c = t / TPL;
+    double2* const X = buf + c * S::LP;
+    const int cx = c & 7;
+    const double2* __restrict__ tw = a.tw;
+    const double2* __restrict__ twq = a.twq;
+
+    // line constants of k0 = t + l NT: c0 + c1 T along dim 1 (dims 0 and 2 transformed), then the closed form
+    double A[LPT], il1[LPT], rr[LPT], qq[LPT], lq[LPT], c1v[LPT];
+    {
+        const double lam2 = a.lam[a.lam_off[2] + e];
+#pragma unroll
+        for (int l = 0; l < LPT; ++l) {
+            const double lam0 = a.lam[a.lam_off[0] + uint32_t(t + l * NT)];
+            double c0 = a.w0, c1 = 0.0;
+            for (int Sm = 1; Sm < 8; ++Sm) {
+                if (a.cS[Sm] == 0.0) continue;
+                double prod = sigma * a.cS[Sm];
+                if (Sm & 1) prod *= lam0;
+                if (Sm & 4) prod *= lam2;
+                if (Sm & 2) c1 += prod;
+                else c0 += prod;
+            }
+            const double B = c0 + 2.0 * c1, sq = sqrt(c0 * (c0 + 4.0 * c1));
+            const double l1 = 0.5 * (B + sq);
+            const double cs = c0 + sq, bs = B + sq;
+            A[l] = -c1;
+            c1v[l] = c1;
+            il1[l] = 1.0 / l1;
+            rr[l] = 4.0 * c0 * c1 / (cs * cs);
+            // log q: from q = 4 c1^2 / (B + s)^2 while q is small (-inf when c1 = 0), from 1 - q near 1 (where the
+            // rounding of 1 - q ~ 1 could also push log1p's argument below -1)
+            const double qd = 4.0 * c1 * c1 / (bs * bs);
+            lq[l] = qd < 0.5 ? log(qd) : log1p(-(cs * (bs + 2.0 * c1)) / (bs * bs));
+            qq[l] = qd < 0.5 ? qd : exp(lq[l]);
+        }
+    }
+    // q^i at the first row of a step (exact start: no drift over the march)
+    auto qpow = [&](int l, uint32_t i) -> double { return i == 0 ? 1.0 : exp(double(i) * lq[l]); };
+
+    // the natural-order spectrum in X -> DCT-II coefficients (k, M - k) for k = j + s TPL (k_plane8's fwd_coeff)
+    auto fwd_coeff = [&](int k, double2& Xk, double2& Xmk) {
+        const int ka = k, kb = k ? M - k : M / 2;
+        const double2 Z1 = X[spec8::slot(ka, cx)], Z2 = X[spec8::slot(kb, cx)];
+        const double2 q1 = twq[ka], q2 = twq[kb];
+        if (k == 0) {
+            Xk = make_double2(q1.x * Z1.x, q1.x * Z1.y);
+            Xmk = make_double2(q2.x * Z2.x, q2.x * Z2.y);
+        } else {
+            const double2 Ap = make_double2(0.5 * (Z1.x + Z2.x), 0.5 * (Z1.y - Z2.y));
+            const double2 Bp = make_double2(0.5 * (Z1.y + Z2.y), -0.5 * (Z1.x - Z2.x));
+            Xk = make_double2(q1.x * Ap.x - q1.y * Ap.y, q1.x * Bp.x - q1.y * Bp.y);
+            Xmk = make_double2(q2.x * Ap.x + q2.y * Ap.y, q2.x * Bp.x + q2.y * Bp.y);
+        }
+    };
+    // coefficients (k, M - k) -> the IFFT input of the Makhoul sequence, in X (k_plane8's inv_spectrum)
+    auto inv_spectrum = [&](int k, double2 Xk, double2 Xmk) {
+        const int ka = k, kb = k ? M - k : M / 2;
+        const double2 q1 = cconj(twq[ka]), q2 = cconj(twq[kb]);
+        if (k == 0) {
+            const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xmk.x));
+            const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xmk.y));
+            X[spec8::slot(0, cx)] = Xk;
+            X[spec8::slot(M / 2, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+        } else {
+            const double2 va1 = cmul(q1, make_double2(Xk.x, -Xmk.x));
+            const double2 vb1 = cmul(q1, make_double2(Xk.y, -Xmk.y));
+            const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xk.x));
+            const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xk.y));
+            X[spec8::slot(ka, cx)] = make_double2(va1.x - vb1.y, va1.y + vb1.x);
+            X[spec8::slot(kb, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+        }
+    };
+
+    double2 z[8];
+    if constexpr (!BWD) {
+        double xs[LPT];   // x'_{i-1} per line
+#pragma unroll
+        for (int l = 0; l < LPT; ++l) xs[l] = 0.0;
+        double2 lv[8];    // the step's rows (2c, 2c + 1) at (2n, 2n + 1), n = j + s4 TPL
+        auto issue = [&](uint32_t i0) {
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    lv[2 * s4 + r] = ldnt2(a.in + pb + (i0 + uint32_t(2 * c + r)) * uint32_t(M) +
+                                           uint32_t(2 * (j + s4 * TPL)));
+        };
+        issue(0);
+        for (uint32_t i0 = 0; i0 < m1; i0 += NR) {
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int n = j + s4 * TPL;
+                X[spec8::slot(n, cx)] = make_double2(lv[2 * s4].x, lv[2 * s4 + 1].x);
+                X[spec8::slot(M - 1 - n, cx)] = make_double2(lv[2 * s4].y, lv[2 * s4 + 1].y);
+            }
+            if (i0 + NR < m1) issue(i0 + NR);   // in flight during this step (LDS-only barriers below)
+            lds_barrier();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, R0>(j, i), cx)];
+            stages_from<L, R0, 1, false, false, true>(z, j, X, cx, tw);   // natural-order spectrum in X
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = j + s * TPL, kb = k ? M - k : M / 2;
+                double2 Xk, Xmk;
+                fwd_coeff(k, Xk, Xmk);
+                C[(2 * c) * M + k] = Xk.x;
+                C[(2 * c + 1) * M + k] = Xk.y;
+                C[(2 * c) * M + kb] = Xmk.x;
+                C[(2 * c + 1) * M + kb] = Xmk.y;
+            }
+            lds_barrier();
+            // forward elimination along dim 1, rows i0 .. i0 + NR - 1
+#pragma unroll
+            for (int l = 0; l < LPT; ++l) {
+                const uint32_t k0 = uint32_t(t + l * NT);
+                double qi = qpow(l, i0);
+                double u = 1.0 + rr[l] * qi;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const uint32_t i = i0 + uint32_t(r);
+                    qi *= qq[l];
+                    const double u1 = 1.0 + rr[l] * qi;
+                    // 1 / den_i = u_i / (l1 u_{i+1}); the last row: den - c1
+                    const double w = (i + 1 == m1) ? 1.0 / (u1 / (u * il1[l]) - c1v[l]) : u * il1[l] / u1;
+                    xs[l] = (C[r * M + int(k0)] - A[l] * xs[l]) * w;
+                    __builtin_nontemporal_store(xs[l], a.out + pb + i * uint32_t(M) + k0);
+                    u = u1;
+                }
+            }
+            // (the next step's first LDS writes touch X, whose reads ended before the barrier above; its C
+            // writes come after its first barrier)
+        }
+    } else {
+        const double sc = a.inv_n * double(m1);   // the dim-0 and dim-2 transforms are unnormalised
+        double xn[LPT];   // x_{i+1} per line
+#pragma unroll
+        for (int l = 0; l < LPT; ++l) xn[l] = 0.0;
+        double lx[LPT][NR];   // the step's x' rows at this thread's lines
+        auto issue = [&](uint32_t i0) {
+#pragma unroll
+            for (int l = 0; l < LPT; ++l)
+#pragma unroll
+                for (int r = 0; r < NR; ++r)
+                    lx[l][r] = __builtin_nontemporal_load(a.in + pb + (i0 + uint32_t(r)) * uint32_t(M) + uint32_t(t + l * NT));
+        };
+        issue(m1 - NR);
+        for (int i0 = int(m1) - NR; i0 >= 0; i0 -= NR) {
+            double cur[LPT][NR];
+#pragma unroll
+            for (int l = 0; l < LPT; ++l)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) cur[l][r] = lx[l][r];
+            if (i0 >= NR) issue(uint32_t(i0 - NR));
+            // back substitution, rows i0 + NR - 1 down to i0
+#pragma unroll
+            for (int l = 0; l < LPT; ++l) {
+                const uint32_t k0 = uint32_t(t + l * NT);
+                double u[NR + 1];
+                double qi = qpow(l, uint32_t(i0));
+                u[0] = 1.0 + rr[l] * qi;
+#pragma unroll
+                for (int r = 1; r <= NR; ++r) {
+                    qi *= qq[l];
+                    u[r] = 1.0 + rr[l] * qi;
+                }
+#pragma unroll
+                for (int r = NR - 1; r >= 0; --r) {
+                    const uint32_t i = uint32_t(i0 + r);
+                    double x = cur[l][r];
+                    if (i + 1 < m1) x -= A[l] * u[r] * il1[l] / u[r + 1] * xn[l];   // e_i = A / den_i
+                    xn[l] = x;
+                    C[r * M + int(k0)] = x * sc;
+                }
+            }
+            lds_barrier();
+            // inverse DCT along dim 0 of rows (2c, 2c + 1)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = j + s * TPL, kb = k ? M - k : M / 2;
+                inv_spectrum(k, make_double2(C[(2 * c) * M + k], C[(2 * c + 1) * M + k]),
+                             make_double2(C[(2 * c) * M + kb], C[(2 * c + 1) * M + kb]));
+            }
+            lds_barrier();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, R0>(j, i), cx)];
+            stages_from<L, R0, 1, true, false, true>(z, j, X, cx, tw);   // output through X
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int n = j + s4 * TPL;
+                const double2 v0 = X[spec8::slot(n, cx)], v1 = X[spec8::slot(M - 1 - n, cx)];
+                stnt2(a.out + pb + uint32_t(i0 + 2 * c) * uint32_t(M) + uint32_t(2 * n), make_double2(v0.x, v1.x));
+                stnt2(a.out + pb + uint32_t(i0 + 2 * c + 1) * uint32_t(M) + uint32_t(2 * n), make_double2(v0.y, v1.y));
+            }
+            // (the next step writes C before its first barrier: every C read of this step came before this step's
+            // second barrier; its X writes come after its first barrier, which every thread reaches only after its
+            // stores above)
+        }
+    }
+}
+
+// =============================================================================================
 // Mixed-radix lengths: m = 2^a 3^b 5^c 7^d <= 4096 that is not a power of two (meshes such as
 // 24 x 40, 100^3 or 1000^2). Same Makhoul pairing and pass structure as k_dct8, with the complex
 // FFT of length m run in LDS as in-place Cooley-Tukey stages of radix 8, 4, 2, 3, 5, 7: decimation
@@ -1574,6 +1829,8 @@ static void launch_dctg(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
         if (d0) {
             if (formb) MVTV_DCTG(SPEC_FWD, true, true);
             else MVTV_DCTG(SPEC_FWD, true, false);
+        } else if (formb) {
+            MVTV_DCTG(SPEC_FWD, false, true);
         } else {
             MVTV_DCTG(SPEC_FWD, false, false);
         }
@@ -2596,6 +2853,8 @@ static void launch_dct8_tile(SpecArgs& a, hipStream_t s, int mode, bool d0, bool
         if (d0) {
             if (formb) MVTV_DCT8(SPEC_FWD, true, true);
             else MVTV_DCT8(SPEC_FWD, true, false);
+        } else if (formb) {   // the first pass of a k_march solve (dim 2 first)
+            MVTV_DCT8(SPEC_FWD, false, true);
         } else {
             MVTV_DCT8(SPEC_FWD, false, false);
         }
@@ -2738,6 +2997,52 @@ hipError_t launch_plane_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, i
         default: return hipErrorInvalidValue;
     }
 #undef MVTV_PLANE
+    return hipGetLastError();
+}
+
+// 3-D meshes whose dim-0 lines are 256 - 2048 points (a power of two) and enough dim-2 planes to fill the chip:
+// dim 2 first, then the marching dim-0 transform + dim-1 tridiagonal passes (k_march)
+bool march_ok(const Geom& g) {
+    if (g.p != 3 || probe_env("MVTV_MARCH_OFF") || probe_env("MVTV_DCT_LDS") || probe_env("MVTV_DCT_MID")) return false;
+    const uint32_t m0 = g.m[0];
+    if (m0 < 256 || m0 > 2048 || (m0 & (m0 - 1)) != 0) return false;
+    const uint32_t nr = 2u * (2048u / m0);
+    return g.m[1] % nr == 0 && g.m[2] >= 128 && g.m[2] <= 4096;
+}
+
+hipError_t launch_march(const SpecPlan& sp, const Geom& g, hipStream_t s, bool bwd, double* x, double sigma, double w0,
+                        const AdmmCtl* ctl, const int32_t* skip) {
+    if (!march_ok(g)) return hipErrorInvalidValue;
+    SpecArgs a{};
+    a.ctl = ctl;
+    a.skip = skip;
+    a.in = x;
+    a.out = x;
+    a.tw = reinterpret_cast<const double2*>(sp.tw + sp.tw_off[0]);
+    a.twq = reinterpret_cast<const double2*>(sp.twq + sp.twq_off[0]);
+    a.lam = sp.lam;
+    for (int j = 0; j < kMaxDims; ++j) {
+        a.lam_off[j] = sp.lam_off[j];
+        a.m[j] = g.m[j];
+    }
+    for (int S = 0; S < 16; ++S) a.cS[S] = g.cS[S];
+    a.sigma = sigma;
+    a.w0 = w0;
+    a.inv_n = 1.0 / double(g.N);
+    const dim3 grid(g.m[2]), block(256);
+#define MVTV_MARCH(LL)                                                                                         \
+    do {                                                                                                       \
+        if (bwd) klaunch(k_march<LL, true>, grid, block, 0, s, a, g.m[1]);                                     \
+        else klaunch(k_march<LL, false>, grid, block, 0, s, a, g.m[1]);                                        \
+    } while (0)
+    switch (g.m[0]) {
+        case 256: MVTV_MARCH(8); break;
+        case 512: MVTV_MARCH(9); break;
+        case 1024: MVTV_MARCH(10); break;
+        case 2048: MVTV_MARCH(11); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef MVTV_MARCH
     return hipGetLastError();
 }
 
