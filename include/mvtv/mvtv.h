@@ -255,7 +255,8 @@ typedef enum mvtv_kernel_id {
     MVTV_K_ADMM_FUSED = 11,   /* 3-D: edge update + D^T gather in one pass over the edge state */
     MVTV_K_GATHER4B = 12,     /* 4-D two-pass gather, second pass (the first is MVTV_K_GATHER) */
     MVTV_K_DCT_FOLD = 13,     /* spectral solve, first pass from the folded s (b = oty + s; + D^T u after a rho change) */
-    MVTV_K_COUNT = 14
+    MVTV_K_ADMM_FUSED4 = 14,  /* 4-D: edge update + the gather's first pass in one pass over the edge state */
+    MVTV_K_COUNT = 15
 } mvtv_kernel_id;
 mvtv_status mvtv_timing_enable(mvtv_problem* prob, int32_t on);
 mvtv_status mvtv_timing_get(mvtv_problem* prob, int32_t kernel_id, double* total_ms, int64_t* launches,

@@ -21,7 +21,8 @@ MVTV_HIP_ERROR, MVTV_NO_DEVICE, MVTV_OUT_OF_MEMORY, MVTV_PCG_NOT_CONVERGED = 4, 
 VARIANT_RCPP, VARIANT_CPP, VARIANT_PY = 0, 1, 2
 ORDER_CPP, ORDER_PY = 0, 1
 KERNELS = ["edge_update", "gather_Dt", "pcg_init", "pcg_apply_A", "pcg_update", "pcg_direction", "reduce", "other",
-           "pcg_fused3d", "dct_first", "dct", "admm_fused", "gather4_b", "dct_first_fold"]
+           "pcg_fused3d", "dct_first", "dct", "admm_fused", "gather4_b", "dct_first_fold",
+           "admm_fused4"]
 SOLVER_AUTO, SOLVER_PCG, SOLVER_SPECTRAL, SOLVER_PCG_SPECTRAL = 0, 1, 2, 3
 
 _dp = C.POINTER(C.c_double)

@@ -272,7 +272,7 @@ hipError_t launch_gather4d(const Geom& g, int order, int umode, hipStream_t s, c
 bool gather4_ok(const Geom& g);
 hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                           double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
-                          int* nparts, const AdmmCtl* ctl, double* scratch, bool fold);
+                          int* nparts, const AdmmCtl* ctl, double* scratch, bool fold, int passes = 3);
 
 bool edge3d_ok(const Geom& g) {
     if (g.p == 4) return edge4d_ok(g);
@@ -1280,7 +1280,7 @@ static int g4_ty() {
 
 hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, const double* edges, double t,
                           double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
-                          int* nparts, const AdmmCtl* ctl, double* scratch, bool fold) {
+                          int* nparts, const AdmmCtl* ctl, double* scratch, bool fold, int passes) {
     Gather4Args a{};
     a.g = g;
     a.fold = fold ? 1 : 0;
@@ -1301,6 +1301,8 @@ hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, co
     a.whi = int(g.iend / pl);
     a.wa = std::max(0, a.wlo - 1);   // Gw of the plane below the owned range (slab ghost) too
     a.wb = a.whi;
+    if (passes & 4) a.wb = a.wlo;    // pass A on that ghost plane only (the fused 4-D slab pass did the owned ones)
+    if ((passes & 4) && a.wb <= a.wa) passes &= ~4;
     a.tiles_x = int((g.m[0] + g4::TX - 1) / g4::TX);
     a.tiles_y = int((g.m[1] + g4_ty() - 1) / g4_ty());
     const int per_w = a.tiles_x * a.tiles_y;
@@ -1329,9 +1331,11 @@ hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, co
         return expl ? goa(k_gather4a<1, U_EXPLICIT, 15, T>) : goa(k_gather4a<1, U_FROM_Z, 15, T>);
     };
     const int ty = g4_ty();
-    const hipError_t e = ty == 16 ? pick(std::integral_constant<int, 16>{})
-                                  : (ty == 8 ? pick(std::integral_constant<int, 8>{}) : pick(std::integral_constant<int, 4>{}));
-    if (e != hipSuccess) return e;
+    const hipError_t e = !(passes & 5) ? hipSuccess
+                                       : (ty == 16 ? pick(std::integral_constant<int, 16>{})
+                                                   : (ty == 8 ? pick(std::integral_constant<int, 8>{})
+                                                              : pick(std::integral_constant<int, 4>{})));
+    if (e != hipSuccess || !(passes & 2)) return e;
     if (g_timed_b.start) {   // the caller timed both passes
         g_timed = g_timed_b;
         g_timed_b = TimedLaunch{};
@@ -1345,6 +1349,275 @@ hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, co
     };
     if (expl) return prev ? gob(k_gather4b<U_EXPLICIT, true>) : gob(k_gather4b<U_EXPLICIT, false>);
     return prev ? gob(k_gather4b<U_FROM_Z, true>) : gob(k_gather4b<U_FROM_Z, false>);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_admm4a (4-D, config 5): the edge update and the gather's pass A in ONE pass over the edge state, the
+// k_admm3a scheme one dimension up. A workgroup owns a 64 x 6 tile of the (dim 0, dim 1) plane at a fixed w
+// (dim 3) and marches dim 2 over a chunk of z planes: at every step it forms z_new of its cells (theta at the 16
+// corners (x + a, y + b, z + c, w + d): the w + 1 corners are a second theta row, the z + 1 ones the next step's
+// plane, carried), stores it to the ping-pong partner buffer, stages the blocks whose S' has dim 0 or 1 in LDS,
+// and forms pass A's outputs from the in-plane backward corners (x - 1, y - 1 from the image; the halo row and
+// the halo column recompute the neighbouring tiles' z_new from the previous iterate and never store it) and the
+// dim-2 corner from per-group sums carried from the previous plane: G0 (blocks without dim 3 in S') and Gw
+// (with), alpha and u parts. k_gather4b then takes the dim-3 difference as before. Against k_edge4d + k_gather4a
+// the edge state is read once instead of twice: 8 (2E + 5N) bytes instead of 8 (3E + 5N) (+ theta twice: the
+// w + 1 corners come from another plane, 16 MB away at 128^4, read as a second stream).
+// 512 threads: waves 0..6 hold image rows 0..6 (row 0 the y - 1 halo), wave 7 the x - 1 halo column (lanes
+// 0..6); the image holds 13 of the 15 blocks (S' = {2} and {3} are read by their own cell only) in two plane
+// buffers: 13 x 7 x 65 x 8 B x 2 = 95 KB, one workgroup per CU, up to 256 VGPRs a lane (the 1024-thread form of
+// round 2 spilled at 128).
+namespace f4a {
+constexpr int IW = 65, IH = 7, TY = IH - 1, NT = 512;
+}
+
+template <int NB, int ORD>
+__host__ __device__ constexpr int f4a_nimg() {
+    int n = 0;
+    for (int k = 0; k < NB; ++k)
+        if ((sprime_mask(block_code(k, 4, ORD), 4) & 3) != 0) ++n;
+    return n;
+}
+template <int NB, int ORD>
+__host__ __device__ constexpr int f4a_slot(int k) {
+    int n = 0;
+    for (int j = 0; j < k; ++j)
+        if ((sprime_mask(block_code(j, 4, ORD), 4) & 3) != 0) ++n;
+    return (sprime_mask(block_code(k, 4, ORD), 4) & 3) != 0 ? n : -1;
+}
+
+struct Fused4Args {
+    Geom g;
+    const double* theta;
+    const double* z_old;
+    double* z_new;
+    const double* theta_old;
+    double* s0a;   // pass A's outputs (k_gather4b's inputs): G0 / Gw, alpha and u parts
+    double* s0u;
+    double* swa;
+    double* swu;
+    double* partials;
+    const AdmmCtl* ctl;
+    double t_old, c_old, t_new;
+    int tiles_x, tiles_y, zchunk, nzc, nblocks, wa;
+};
+
+template <int ORD, int UM, bool DTH, int NB>
+__global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
+    constexpr int P = 4, NC = 16, IW = f4a::IW, IH = f4a::IH, NI = f4a_nimg<NB, ORD>();
+    double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        t_old = a.ctl->t_z;
+        c_old = a.ctl->c_prev;
+        t_new = a.ctl->t_next;
+    }
+    __shared__ double szr[2 * NI * IH * IW];
+    double red[ER_N] = {0.0, 0.0, 0.0, 0.0};
+    const Geom& g = a.g;
+    const int bid = int((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3));   // XCD runs of tiles
+    if (bid < a.nblocks) {
+        const int nt = a.tiles_x * a.tiles_y;
+        const int tw = bid / (nt * a.nzc);
+        int rem = bid - tw * nt * a.nzc;
+        const int tz = rem / nt;
+        rem -= tz * nt;
+        const int tyi = rem / a.tiles_x, txi = rem - tyi * a.tiles_x;
+        const int X0 = txi * 64, Yh = tyi * f4a::TY - 1;
+        const int w = a.wa + tw;
+        const int m0 = int(g.m[0]), m1 = int(g.m[1]), m2 = int(g.m[2]), m3 = int(g.m[3]);
+        const int z0 = tz * a.zchunk, z1 = min(m2, z0 + a.zchunk);
+        const int wv = int(threadIdx.x) >> 6, ln = int(threadIdx.x) & 63;
+        const bool hcol = wv == IH;
+        const int row = hcol ? ln : wv;
+        const int col = hcol ? 0 : ln + 1;
+        const int x = hcol ? X0 - 1 : X0 + ln, y = Yh + row;
+        const bool active = row < IH;
+        const bool cell = active && x >= 0 && y >= 0 && x < m0 && y < m1;
+        const bool inner = cell && !hcol && row > 0;
+        const bool hrow = row == 0;
+        const uint32_t pl = uint32_t(m0) * uint32_t(m1), pl3 = pl * uint32_t(m2);
+        const int xc = min(max(x, 0), m0 - 1), yc = min(max(y, 0), m1 - 1);
+        const uint32_t xo[2] = {uint32_t(xc), uint32_t(min(xc + 1, m0 - 1))};
+        const uint32_t yo[2] = {uint32_t(yc) * uint32_t(m0), uint32_t(min(yc + 1, m1 - 1)) * uint32_t(m0)};
+        const uint32_t wo[2] = {uint32_t(w) * pl3, uint32_t(min(w + 1, m3 - 1)) * pl3};
+        const uint32_t ixy = yo[0] + xo[0];
+        const bool okx = x > 0, oky = y > 0;
+        auto sidx = [&](int buf, int slot, int r, int c) { return ((buf * NI + slot) * IH + r) * IW + c; };
+
+        // theta at (x + a, y + b, w + d) of plane e: index a | b << 1 | d << 2
+        auto load_theta = [&](double (&th)[8], int e) {
+            const uint32_t zo = uint32_t(e) * pl;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) th[q] = cell ? a.theta[wo[q >> 2] + zo + yo[(q >> 1) & 1] + xo[q & 1]] : 0.0;
+        };
+        auto load_z = [&](double (&zo)[NB], int e) {
+            const uint32_t i = wo[0] + uint32_t(e) * pl + ixy;
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                const bool need = cell && (!hrow || (S & 2)) && (!hcol || (S & 1));
+                zo[k] = need ? a.z_old[eix(g, k, i)] : 0.0;
+            });
+        };
+        auto edge_cell = [&](int e, const double (&th0)[8], const double (&th1)[8], const double (&zo)[NB],
+                             double (&zn)[NB], bool own) {
+            const uint32_t i = wo[0] + uint32_t(e) * pl + ixy;
+            double v[NC];   // corner a | b << 1 | c << 2 | d << 3
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int qq = (q & 3) | ((q & 4) << 1);
+                v[qq] = th0[q];
+                v[qq | 4] = th1[q];
+            }
+            if constexpr (DTH)
+                if (own) red[ER_DTH] = fmax(red[ER_DTH], fabs(v[0] - a.theta_old[i]));
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+#pragma unroll
+                for (int q = 0; q < NC; ++q)
+                    if (!((q >> j) & 1)) v[q | (1 << j)] = v[q] - v[q | (1 << j)];
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                const double d = g.w[k] * v[S];
+                const double uo = (UM == U_EXPLICIT) ? zo[k] : -c_old * clampd(zo[k], t_old);
+                const double z = cell ? d - uo : 0.0;
+                zn[k] = z;
+                if (own) {
+                    const double al = z - clampd(z, t_new);
+                    const double r = al - d;
+                    __builtin_nontemporal_store(z, a.z_new + eix(g, k, i));
+                    red[ER_R2] = fma(r, r, red[ER_R2]);
+                    red[ER_D2] = fma(d, d, red[ER_D2]);
+                    red[ER_A2] = fma(al, al, red[ER_A2]);
+                }
+            });
+        };
+        auto to_image = [&](int buf, const double (&zn)[NB]) {
+            if (!active) return;
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int sl = f4a_slot<NB, ORD>(k);
+                if constexpr (sl >= 0) szr[sidx(buf, sl, row, col)] = zn[k];
+            });
+        };
+        auto plane_q = [&](auto kc, int buf, double own_z, double& qa, double& qu) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+            constexpr int SI = S & 3;
+            constexpr int sl = f4a_slot<NB, ORD>(k);
+            qa = 0.0;
+            qu = 0.0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if ((q & ~SI) != 0) continue;
+                double v;
+                if (q == 0) {
+                    v = own_z;
+                } else {
+                    const bool ok = (!(q & 1) || okx) && (!(q & 2) || oky);
+                    if constexpr (sl >= 0) v = ok ? szr[sidx(buf, sl, row - ((q >> 1) & 1), col - (q & 1))] : 0.0;
+                    else v = 0.0;
+                }
+                const bool neg = __builtin_popcount(q) & 1;
+                const double cl = clampd(v, t_new);
+                const double al = v - cl;
+                qa = neg ? qa - al : qa + al;
+                qu = neg ? qu + cl : qu - cl;   // u = -clamp
+            }
+        };
+        // per-group sums of the blocks with dim 2 in S' at the previous plane (G0 / Gw, alpha / u)
+        double ca0 = 0.0, cu0 = 0.0, caw = 0.0, cuw = 0.0;
+        auto carry = [&](int buf, const double (&zn)[NB], double& na0, double& nu0, double& naw, double& nuw) {
+            static_for<0, NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                if constexpr ((S & 4) != 0) {
+                    double qa, qu;
+                    plane_q(kc, buf, zn[k], qa, qu);
+                    if constexpr ((S & 8) != 0) {
+                        naw = fma(g.w[k], qa, naw);
+                        nuw = fma(g.w[k], qu, nuw);
+                    } else {
+                        na0 = fma(g.w[k], qa, na0);
+                        nu0 = fma(g.w[k], qu, nu0);
+                    }
+                }
+            });
+        };
+        double th0[8], th1[8], zo[NB], zn[NB];
+        if (z0 > 0) {   // the carried sums of plane z0 - 1, from its z_new recomputed from the old state
+            load_theta(th0, z0 - 1);
+            load_theta(th1, z0);
+            load_z(zo, z0 - 1);
+            edge_cell(z0 - 1, th0, th1, zo, zn, false);
+            to_image(1, zn);
+            lds_barrier();
+            if (inner) carry(1, zn, ca0, cu0, caw, cuw);
+            lds_barrier();
+        }
+        load_theta(th0, z0);
+        load_theta(th1, min(z0 + 1, m2 - 1));
+        load_z(zo, z0);
+        for (int e = z0; e < z1; ++e) {
+            const int buf = (e - z0) & 1;
+            edge_cell(e, th0, th1, zo, zn, inner);
+            to_image(buf, zn);
+            double nth[8], nzo[NB];   // the next step's loads in flight during this step's gather
+            if (e + 1 < z1) {
+                load_theta(nth, min(e + 2, m2 - 1));
+                load_z(nzo, e + 1);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) nth[q] = 0.0;
+#pragma unroll
+                for (int k = 0; k < NB; ++k) nzo[k] = 0.0;
+            }
+            lds_barrier();
+            if (inner) {
+                double sa0 = 0.0, su0 = 0.0, saw = 0.0, suw = 0.0, na0 = 0.0, nu0 = 0.0, naw = 0.0, nuw = 0.0;
+                static_for<0, NB>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    constexpr int S = sprime_mask(block_code(k, P, ORD), P);
+                    double qa, qu;
+                    plane_q(kc, buf, zn[k], qa, qu);
+                    if constexpr ((S & 8) != 0) {
+                        saw = fma(g.w[k], qa, saw);
+                        suw = fma(g.w[k], qu, suw);
+                        if constexpr ((S & 4) != 0) {
+                            naw = fma(g.w[k], qa, naw);
+                            nuw = fma(g.w[k], qu, nuw);
+                        }
+                    } else {
+                        sa0 = fma(g.w[k], qa, sa0);
+                        su0 = fma(g.w[k], qu, su0);
+                        if constexpr ((S & 4) != 0) {
+                            na0 = fma(g.w[k], qa, na0);
+                            nu0 = fma(g.w[k], qu, nu0);
+                        }
+                    }
+                });
+                const uint32_t i = wo[0] + uint32_t(e) * pl + ixy;
+                __builtin_nontemporal_store(sa0 - ca0, a.s0a + i);
+                __builtin_nontemporal_store(su0 - cu0, a.s0u + i);
+                __builtin_nontemporal_store(saw - caw, a.swa + i);
+                __builtin_nontemporal_store(suw - cuw, a.swu + i);
+                ca0 = na0;
+                cu0 = nu0;
+                caw = naw;
+                cuw = nuw;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                th0[q] = th1[q];
+                th1[q] = nth[q];
+            }
+#pragma unroll
+            for (int k = 0; k < NB; ++k) zo[k] = nzo[k];
+        }
+    }
+    block_reduce_store<ER_N, 1, f4a::NT>(red, a.partials);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1596,4 +1869,83 @@ hipError_t launch_admm2d(const Geom& g, int order, int umode, hipStream_t s, con
     return dth ? go(k_admm2d<1, U_FROM_Z, true, 3>) : go(k_admm2d<1, U_FROM_Z, false, 3>);
 }
 
+
+// ------------------------------------------------------------------------------------------------ k_admm4a
+namespace {
+Fused4Args f4a_args(const Geom& g) {
+    Fused4Args a{};
+    a.g = g;
+    const uint32_t pl3 = g.m[0] * g.m[1] * g.m[2];
+    a.wa = int(g.ibeg / pl3);
+    const int nw = std::max(1, int(g.iend / pl3) - a.wa);
+    a.tiles_x = int((g.m[0] + 63) / 64);
+    a.tiles_y = int((int(g.m[1]) + f4a::TY - 1) / f4a::TY);
+    const int tiles = a.tiles_x * a.tiles_y * nw;
+    // z chunks only when the (tile, w) items alone leave the chip under ~4 waves (one workgroup per CU): every chunk
+    // start recomputes one plane
+    a.nzc = std::max(1, std::min(int(g.m[2]), (1024 + tiles - 1) / tiles));
+    a.zchunk = int((g.m[2] + uint32_t(a.nzc) - 1) / uint32_t(a.nzc));
+    a.nzc = int((g.m[2] + uint32_t(a.zchunk) - 1) / uint32_t(a.zchunk));
+    a.nblocks = tiles * a.nzc;
+    return a;
+}
+}  // namespace
+
+bool fused4_ok(const Geom& g) {
+    if (g.p != 4 || probe_env("MVTV_F4D_OFF") || !gather4_ok(g) || g.iend <= g.ibeg) return false;
+    const Fused4Args a = f4a_args(g);
+    // partial rows: ER_N words per workgroup within the partials buffer
+    return size_t((a.nblocks + 7) / 8 * 8) * ER_N <= size_t(kMaxCgBlocks) * kMaxRed;
+}
+
+hipError_t launch_admm4a(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
+                         double* z_new, double t_old, double c_old, double t_new, const double* theta_old,
+                         double* scratch4, double* partials, int* nparts, const AdmmCtl* ctl) {
+    if (!fused4_ok(g) || !scratch4 || z_old == z_new) return hipErrorInvalidValue;
+    Fused4Args a = f4a_args(g);
+    a.t_old = t_old;
+    a.c_old = c_old;
+    a.t_new = t_new;
+    a.theta = theta;
+    a.z_old = z_old;
+    a.z_new = z_new;
+    a.theta_old = theta_old;
+    a.s0a = scratch4;
+    a.s0u = scratch4 + size_t(g.N);
+    a.swa = scratch4 + 2 * size_t(g.N);
+    a.swu = scratch4 + 3 * size_t(g.N);
+    a.partials = partials;
+    a.ctl = ctl;
+    const int grid = (a.nblocks + 7) / 8 * 8;
+    *nparts = grid;
+    const bool dth = theta_old != nullptr;
+    auto go = [&](auto kern) {
+        klaunch(kern, dim3(grid), dim3(f4a::NT), 0, s, a);
+        return hipGetLastError();
+    };
+    if (order == 0) {
+        if (umode == U_EXPLICIT) return dth ? go(k_admm4a<0, U_EXPLICIT, true, 15>) : go(k_admm4a<0, U_EXPLICIT, false, 15>);
+        return dth ? go(k_admm4a<0, U_FROM_Z, true, 15>) : go(k_admm4a<0, U_FROM_Z, false, 15>);
+    }
+    if (g.nb == 14) {
+        if (umode == U_EXPLICIT) return dth ? go(k_admm4a<1, U_EXPLICIT, true, 14>) : go(k_admm4a<1, U_EXPLICIT, false, 14>);
+        return dth ? go(k_admm4a<1, U_FROM_Z, true, 14>) : go(k_admm4a<1, U_FROM_Z, false, 14>);
+    }
+    if (umode == U_EXPLICIT) return dth ? go(k_admm4a<1, U_EXPLICIT, true, 15>) : go(k_admm4a<1, U_EXPLICIT, false, 15>);
+    return dth ? go(k_admm4a<1, U_FROM_Z, true, 15>) : go(k_admm4a<1, U_FROM_Z, false, 15>);
+}
+
+hipError_t launch_gather4b(const Geom& g, int umode, hipStream_t s, double* g_alpha, double* g_u, const double* g_uprev,
+                           double c_prev, double* partials, int* nparts, const AdmmCtl* ctl, double* scratch4,
+                           bool fold) {
+    return launch_gather4(g, 0, umode, s, nullptr, 0.0, g_alpha, g_u, g_uprev, c_prev, partials, nparts, ctl, scratch4,
+                          fold, 2);
+}
+
+hipError_t launch_gather4a_ghost(const Geom& g, int order, hipStream_t s, const double* edges, double* scratch4,
+                                 const AdmmCtl* ctl) {
+    int np = 0;
+    return launch_gather4(g, order, U_FROM_Z, s, edges, 0.0, nullptr, nullptr, nullptr, 1.0, nullptr, &np, ctl, scratch4,
+                          false, 4);
+}
 }  // namespace mvtv

@@ -838,6 +838,7 @@ mvtv_status problem_create_impl(const mvtv_problem_desc* d, const mvtv_slab_desc
     P->e3d = edge3d_ok(g);
     if (s == MVTV_OK && P->e3d && g.p == 4 && gather4_ok(g)) s = alloc(&P->g4, 4 * size_t(N));
     P->f3d = fused3d_ok(g);   // slab problems too: the fused pass runs on the owned planes (Geom.ibeg/iend)
+    P->f4d = P->e3d && g.p == 4 && P->g4 != nullptr && fused4_ok(g);   // slab ranks: on the owned planes
     {   // chunked edge layout for the 3-D fused path (MVTV_EAOS=0 keeps block-major): the fused kernel's
         // launches 2-4 % shorter at 512^3 on the same box (4.21 -> 4.13 ms, 5.2-5.36 -> 5.13 ms)
         const char* e = probe_env("MVTV_EAOS");
@@ -1028,7 +1029,9 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
 
     const bool track_theta = variant != MVTV_VARIANT_RCPP;
     const bool fused = P->f3d;
-    if (fused && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
+    const bool fused4 = P->f4d;   // 4-D: edge update + gather pass A fused, pass B separate
+    const bool pingpong = fused || fused4;
+    if (pingpong && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
     // MVTV_EBUF3=1: z rotates over three buffers (when the third fits with 16 GiB to spare). Opt-in:
     // over five boxes it is as often slower as faster than two (profiles/r01/v8_ebuf3_ab.txt)
     static const int rot3_env = [] {
@@ -1126,6 +1129,26 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
                 P->tstop(hh);
                 return MVTV_OK;
             }
+            if (fused4) {   // z ping-pongs as in the 3-D fused loop; pass B of the gather after the ER reduction
+                int hh = P->tstart(MVTV_K_ADMM_FUSED4);
+                int npe = 0;
+                HIP_TRY(launch_admm4a(P->g, P->order, um, P->stream, P->theta, ebuf[j % nbuf], ebuf[(j + 1) % nbuf], 0.0,
+                                      1.0, 0.0, track_theta ? P->thold : nullptr, P->g4, P->partials, &npe, P->ctl));
+                P->tstop(hh);
+                hh = P->tstart(MVTV_K_REDUCE);
+                HIP_TRY(launch_finalize(P->stream, P->partials, npe, ER_N, 1, 0, P->red, P->st, 0.0, 0, P->ctl));
+                P->tstop(hh);
+                hh = P->tstart(MVTV_K_GATHER4B);
+                int npg = 0;
+                HIP_TRY(launch_gather4b(P->g, U_FROM_Z, P->stream, P->ga, gn, gp, 1.0, P->partials, &npg, P->ctl, P->g4,
+                                        fold));
+                P->tstop(hh);
+                hh = P->tstart(MVTV_K_REDUCE);
+                HIP_TRY(launch_finalize(P->stream, P->partials, npg, GR_N, 0, 0, P->red + ER_N, P->st, 0.0, 0, P->ctl,
+                                        P->ctl, P->red));   // + the control step
+                P->tstop(hh);
+                return MVTV_OK;
+            }
             int hh = P->tstart(MVTV_K_EDGE_UPDATE);
             int npe = L.grid;
             if (P->e3d)
@@ -1219,7 +1242,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
             P->edges = ebuf[it_done % 3];
             P->edges2 = ebuf[(it_done + 1) % 3];
             P->edges3 = ebuf[(it_done + 2) % 3];
-        } else if (fused && (it_done & 1)) {
+        } else if (pingpong && (it_done & 1)) {
             std::swap(P->edges, P->edges2);
         }
         if (it_done > 0) P->edge_mode = U_FROM_Z;
@@ -1303,6 +1326,24 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
             P->tstop(h);
             mode = U_FROM_Z;
             t_z = t_new;
+        } else if (fused4) {   // 4-D: edge update + gather pass A in one pass (z ping-pong), then pass B
+            h = P->tstart(MVTV_K_ADMM_FUSED4);
+            HIP_TRY(launch_admm4a(P->g, P->order, mode, P->stream, P->theta, P->edges, P->edges2, t_z, c_prev, t_new,
+                                  track_theta ? P->thold : nullptr, P->g4, P->partials, &np));
+            P->tstop(h);
+            std::swap(P->edges, P->edges2);
+            h = P->tstart(MVTV_K_REDUCE);
+            HIP_TRY(launch_finalize(P->stream, P->partials, np, ER_N, 1, 0, P->red, P->st));
+            P->tstop(h);
+            mode = U_FROM_Z;
+            t_z = t_new;
+            h = P->tstart(MVTV_K_GATHER4B);
+            HIP_TRY(launch_gather4b(P->g, U_FROM_Z, P->stream, P->ga, gnew, gprev, c_prev, P->partials, &np, nullptr,
+                                    P->g4));
+            P->tstop(h);
+            h = P->tstart(MVTV_K_REDUCE);
+            HIP_TRY(launch_finalize(P->stream, P->partials, np, GR_N, 0, 0, P->red + ER_N, P->st));
+            P->tstop(h);
         } else {
             h = P->tstart(MVTV_K_EDGE_UPDATE);
             np = L.grid;
@@ -1840,6 +1881,7 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
             break;
         case MVTV_K_DCT: b = 8.0 * 2.0 * N; break;                       // x in, x out
         case MVTV_K_ADMM_FUSED: b = 8.0 * (4.0 * N + 2.0 * E); break;    // theta, z, g_uprev in; z', g_alpha, g_u out
+        case MVTV_K_ADMM_FUSED4: b = 8.0 * (5.0 * N + 2.0 * E); break;   // theta, z in; z', 4 pass-A sums out
         default: b = 0.0;
     }
     if (total_ms) *total_ms = P->ms[kid];
@@ -1851,7 +1893,8 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
 const char* mvtv_kernel_name(int32_t kid) {
     static const char* names[MVTV_K_COUNT] = {"edge_update", "gather_Dt", "pcg_init", "pcg_apply_A",
                                                "pcg_update", "pcg_direction", "reduce", "other", "pcg_fused3d",
-                                               "dct_first", "dct", "admm_fused", "gather4_b", "dct_first_fold"};
+                                               "dct_first", "dct", "admm_fused", "gather4_b", "dct_first_fold",
+                                               "admm_fused4"};
     return (kid >= 0 && kid < MVTV_K_COUNT) ? names[kid] : "?";
 }
 

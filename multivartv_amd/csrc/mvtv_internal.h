@@ -325,6 +325,18 @@ hipError_t launch_gather3d(const Geom& g, int order, int umode, hipStream_t s, c
                            double* g_alpha, double* g_u, const double* g_uprev, double c_prev, double* partials,
                            int* nparts, const AdmmCtl* ctl = nullptr, double* scratch4 = nullptr, bool fold = false);
 bool gather4_ok(const Geom& g);
+// fused 4-D edge update + the two-pass gather's pass A (k_admm4a, z ping-pong buffers), then pass B alone:
+// ER partials from the first launch (*nparts rows), GR partials from the second
+bool fused4_ok(const Geom& g);
+hipError_t launch_admm4a(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
+                         double* z_new, double t_old, double c_old, double t_new, const double* theta_old,
+                         double* scratch4, double* partials, int* nparts, const AdmmCtl* ctl = nullptr);
+hipError_t launch_gather4b(const Geom& g, int umode, hipStream_t s, double* g_alpha, double* g_u, const double* g_uprev,
+                           double c_prev, double* partials, int* nparts, const AdmmCtl* ctl, double* scratch4,
+                           bool fold = false);
+// a slab rank's pass A on its lower ghost plane (w = first owned - 1), after the z halo brought that plane's z_new
+hipError_t launch_gather4a_ghost(const Geom& g, int order, hipStream_t s, const double* edges, double* scratch4,
+                                 const AdmmCtl* ctl);
 hipError_t launch_gather_index(hipStream_t s, const double* theta, const int64_t* idx, int64_t n, double* out);
 
 // scattered-data setup (mvtv_scatter.hip)

@@ -84,6 +84,7 @@ struct mvtv_problem {
     bool spec_lead = false;       // dims 0..p-2 are (the slab loop: the last dimension may have any length)
     bool e3d = false;             // z-marching 3-D edge kernels
     bool f3d = false;             // fused 3-D edge update + gather (needs the second edge buffer)
+    bool f4d = false;             // fused 4-D edge update + gather pass A (k_admm4a; second edge buffer, g4)
     double* edges2 = nullptr;     // ping-pong partner of edges for the fused kernel
     bool zpicked = false;         // the z ping-pong pair was chosen by timed probes (pick_zpair)
     double* edges3 = nullptr;     // third z buffer of the spectral loop (MVTV_EBUF3=1). On boxes where the fused

@@ -469,15 +469,16 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         // slot 7: this rank's block of every line can be cut into the line solves' segments (k_tris: <= 64
         // segments of <= 32 rows); checked here, before any rank enters a collective the infeasible one would skip
         const bool lines_ok = G == 1 || tri_slab_ok(sg.nz);
-        double flags[8] = {P->f3d ? 1.0 : 0.0, P->g.eaos ? 1.0 : 0.0, P->e3d ? 1.0 : 0.0, double(sg.plane),
-                           wd ? 1.0 : 0.0, P->wsum_own, P->wsum2_own, lines_ok ? 1.0 : 0.0};
+        double flags[9] = {P->f3d ? 1.0 : 0.0, P->g.eaos ? 1.0 : 0.0, P->e3d ? 1.0 : 0.0, double(sg.plane),
+                           wd ? 1.0 : 0.0, P->wsum_own, P->wsum2_own, lines_ok ? 1.0 : 0.0, P->f4d ? 1.0 : 0.0};
         HIP_TRY(hipMemcpyAsync(P->red, flags, sizeof(flags), hipMemcpyHostToDevice, s));
-        MVTV_TRY(C->allreduce_sum(P->red, 8, s));
-        double sum[8];
+        MVTV_TRY(C->allreduce_sum(P->red, 9, s));
+        double sum[9];
         HIP_TRY(hipMemcpyAsync(sum, P->red, sizeof(sum), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         for (int k = 0; k < 5; ++k)
             if (sum[k] != double(G) * flags[k]) return fail(MVTV_BAD_ARG, "slab ranks disagree on the loop layout");
+        if (sum[8] != double(G) * flags[8]) return fail(MVTV_BAD_ARG, "slab ranks disagree on the loop layout");
         if (sum[7] != double(G))
             return fail(MVTV_BAD_ARG, "slab line solves: a rank's block of the last dimension has no split into <= 64 "
                                       "segments of <= 32 planes (e.g. a prime plane count above 64)");
@@ -492,6 +493,8 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     const double tol = opts->tol > 0 ? opts->tol : 1e-4;
     const int max_counter = opts->max_counter > 0 ? opts->max_counter : 3000;
     const bool fused = P->f3d;
+    const bool fused4 = P->f4d;   // 4-D: edge update + the gather's pass A fused on the owned planes (k_admm4a)
+    const bool pingpong = fused || fused4;
     // folded right-hand side (as mvtv_capi.cpp's loop): the fused kernel stores s = rho (D^T alpha + D^T u) and the
     // next first pass reads oty + s (oty + (rho'/rho) s + rho' (c - 1) D^T u after a rho change)
     const uint32_t m0 = P->g.m[0];
@@ -506,13 +509,13 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     const char* force = std::getenv("MVTV_SLAB_DISTRIBUTED");
     const bool solo = G == 1 && !(force && std::atoi(force) != 0);
     if (!solo && !P->slab_iface) MVTV_TRY(alloc(&P->slab_iface, 16 * size_t(sg.lines)));
-    if (fused && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
+    if (pingpong && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
     const size_t nodes = P->g.N, ebytes = size_t(P->g.nb) * nodes * sizeof(double);
 
     // ---- initial state: theta0 everywhere (ghosts included), u0 = 0, g_alpha = D^T D theta0 -----------
     HIP_TRY(launch_fill(s, P->theta, theta0, nodes));
     HIP_TRY(hipMemsetAsync(P->edges, 0, ebytes, s));
-    if (fused) HIP_TRY(hipMemsetAsync(P->edges2, 0, ebytes, s));
+    if (pingpong) HIP_TRY(hipMemsetAsync(P->edges2, 0, ebytes, s));
     HIP_TRY(hipMemsetAsync(P->guprev, 0, nodes * sizeof(double), s));
     HIP_TRY(launch_apply_A(P->g, P->L(), 1.0, W_NONE, nullptr, P->theta, P->ga, nullptr, nullptr));
     AdmmCtl& c = *P->host_ctl;
@@ -559,7 +562,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     double* lr_recv = lr_send + 2 * ln;       // [chunk s][2][line in chunk]
     const double scale = 1.0 / double(sg.lines);   // the forward transforms along dims 0..p-2 (unnormalised)
     double* gbuf[2] = {P->guprev, P->gu};
-    double* ebuf[2] = {P->edges, fused ? P->edges2 : P->edges};
+    double* ebuf[2] = {P->edges, pingpong ? P->edges2 : P->edges};
     const size_t pl = sg.plane;
     const size_t first_owned = size_t(P->g_lo) * pl, last_owned = first_owned + size_t(sg.nz - 1) * pl;
 
@@ -842,6 +845,29 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
                                   P->partials, &npf, P->ctl, fold));
             P->tstop(h);
             HIP_TRY(launch_finalize(s, P->partials, npf, ER_N + GR_N, -(1 << ER_DTH), 0, P->red, P->st, 0.0, 0, P->ctl));
+        } else if (fused4) {
+            // z_new and pass A's sums of the owned planes in one pass; then the last owned plane of z_new to rank+1's
+            // lower ghost plane, pass A on this rank's ghost plane (pass B at the first owned plane needs its Gw), pass B
+            int h = P->tstart(MVTV_K_ADMM_FUSED4);
+            int npe = 0;
+            HIP_TRY(launch_admm4a(P->g, P->order, um, s, P->theta, zo, zn, 0.0, 1.0, 0.0, nullptr, P->g4, P->partials,
+                                  &npe, P->ctl));
+            P->tstop(h);
+            HIP_TRY(launch_finalize(s, P->partials, npe, ER_N, 1, 0, P->red, P->st, 0.0, 0, P->ctl));
+            if (!solo) {
+                MVTV_TRY(handoff(ev[EV_EDGE], s, sc));
+                MVTV_TRY(C->begin());
+                if (rk < G - 1) MVTV_TRY(edge_plane_xfer(zn, last_owned / pl, rk + 1, true));
+                if (rk > 0) MVTV_TRY(edge_plane_xfer(zn, 0, rk - 1, false));
+                MVTV_TRY(C->end(sc));
+                MVTV_TRY(handoff(ev[EV_EDGED], sc, s));
+                if (rk > 0) HIP_TRY(launch_gather4a_ghost(P->g, P->order, s, zn, P->g4, P->ctl));
+            }
+            h = P->tstart(MVTV_K_GATHER4B);
+            int npg = 0;
+            HIP_TRY(launch_gather4b(P->g, U_FROM_Z, s, P->ga, gn, gp, 1.0, P->partials, &npg, P->ctl, P->g4, fold));
+            P->tstop(h);
+            HIP_TRY(launch_finalize(s, P->partials, npg, GR_N, 0, 0, P->red + ER_N, P->st, 0.0, 0, P->ctl));
         } else {
             int h = P->tstart(MVTV_K_EDGE_UPDATE);
             int npe = P->grid;
@@ -924,7 +950,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     if (opts->fixed_iters <= 0 && c.status == 0) P->admm_hint = it_done + 1;
     if (it_done & 1) {
         std::swap(P->guprev, P->gu);
-        if (fused) std::swap(P->edges, P->edges2);
+        if (pingpong) std::swap(P->edges, P->edges2);
     }
     P->edge_mode = it_done > 0 ? U_FROM_Z : U_EXPLICIT;
     P->t_z = c.t_z;

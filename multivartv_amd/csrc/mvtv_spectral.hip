@@ -2914,18 +2914,11 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
             xcd_def = true;
         }
     }
-    static const int t0 = [] {
-        const char* e = probe_env("MVTV_DCT_T0");
-        return e ? std::atoi(e) : 0;
-    }();
-    static const int t1 = [] {
-        const char* e = probe_env("MVTV_DCT_T1");
-        return e ? std::atoi(e) : 0;
-    }();
-    static const int xcd_env = [] {
-        const char* e = probe_env("MVTV_DCT_XCD");
-        return e ? std::atoi(e) : -1;
-    }();
+    // (probe builds read these per launch, so a probe can vary them within one process)
+    const char* e0 = probe_env("MVTV_DCT_T0");
+    const char* e1 = probe_env("MVTV_DCT_T1");
+    const char* ex = probe_env("MVTV_DCT_XCD");
+    const int t0 = e0 ? std::atoi(e0) : 0, t1 = e1 ? std::atoi(e1) : 0, xcd_env = ex ? std::atoi(ex) : -1;
     if (d0 && t0 > 0) want = t0;
     if (!d0 && t1 > 0) want = t1;
     if (!d0) want = std::min<int>(want, int(a.stride));
@@ -3001,9 +2994,16 @@ hipError_t launch_plane_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, i
 }
 
 // 3-D meshes whose dim-0 lines are 256 - 2048 points (a power of two) and enough dim-2 planes to fill the chip:
-// dim 2 first, then the marching dim-0 transform + dim-1 tridiagonal passes (k_march)
+// dim 2 first, then the marching dim-0 transform + dim-1 tridiagonal passes (k_march). Probe builds only
+// (MVTV_MARCH=1): it moves 9N words per solve instead of 11N, but its two dim-2 passes stride 2 MB (the first one
+// reading three inputs) and run slower than the dim-0 / dim-1 passes they replace, and the march itself, one
+// workgroup per dim-2 plane (8 waves per CU at 512^3), reaches 3.7 TB/s: 512^3 162.5-163.4 ADMM it/s against
+// 165.1-165.8 for the five-pass solve, 165.2-166.4 with 32-line strided tiles, 256^3 1150 against 1170, same
+// process, interleaved (profiles/r04/v2_march).
 bool march_ok(const Geom& g) {
-    if (g.p != 3 || probe_env("MVTV_MARCH_OFF") || probe_env("MVTV_DCT_LDS") || probe_env("MVTV_DCT_MID")) return false;
+    const char* on = probe_env("MVTV_MARCH");
+    if (!on || std::atoi(on) == 0) return false;
+    if (g.p != 3 || probe_env("MVTV_DCT_LDS") || probe_env("MVTV_DCT_MID")) return false;
     const uint32_t m0 = g.m[0];
     if (m0 < 256 || m0 > 2048 || (m0 & (m0 - 1)) != 0) return false;
     const uint32_t nr = 2u * (2048u / m0);

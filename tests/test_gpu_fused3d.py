@@ -58,3 +58,52 @@ def test_folded_rhs_converged_matches_oracle(m, lam):
     assert rho == rs["rho"]
     assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
     assert np.max(np.abs(u - ref_u)) <= 1e-9 * max(1.0, np.max(np.abs(ref_u)))
+
+
+@pytest.mark.parametrize("m,iters,order,weighted,solver",
+                         [([70, 70, 70, 9], 6, "cpp", True, mv.SOLVER_AUTO),
+                          ([13, 13, 13, 6], 8, "cpp", True, mv.SOLVER_AUTO),
+                          ([128, 128, 128, 3], 3, "cpp", True, mv.SOLVER_AUTO),
+                          ([16, 16, 16, 5], 8, "py", True, mv.SOLVER_PCG),
+                          ([16, 16, 16, 5], 8, "py", False, mv.SOLVER_PCG),
+                          ([24, 24, 24, 4], 6, "cpp", True, mv.SOLVER_PCG)],
+                         ids=["ragged_70_zchunks", "bluestein_13_every_plane_a_chunk", "aligned_128",
+                              "py_weighted_14_blocks", "py_unweighted_15_blocks", "pcg_sync_loop"])
+def test_fused4d_matches_oracle(m, iters, order, weighted, solver):
+    """The fused 4-D pass (k_admm4a: edge update + the gather's pass A over one read of the edge state, 64 x 6
+    tiles at a fixed w marching z, then k_gather4b) on ragged tiles (m0 % 64, m1 % 6 != 0), z-chunked grids (every
+    chunk start recomputes a plane from the old state; 13^3 x 6 makes every plane a chunk), both block orders (15 and
+    14 blocks) and the host-synchronous loop of a PCG theta-solve, against the C oracle's variant-B loop
+    (rcpp…/solvers.cpp:96-136): rho exactly, theta and u to 1e-9 of their max."""
+    y = towers(m)
+    o = mv.ORDER_CPP if order == "cpp" else mv.ORDER_PY
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    lam = 1.0
+    th0 = np.full(y.size, y.mean())
+    with mv.Problem(m, y, deltas=deltas, order=o, weighted=weighted) as P:
+        th, u, rho, st = P.admm(lam, th0, u=np.zeros(P.E), rho=lam / 5, fixed_iters=iters, pcg_rtol=1e-13,
+                                theta_solver=solver)
+        E = P.E
+        tm = None
+    ref_th = th0.copy()
+    ref_u = np.zeros(E)
+    rs = c_oracle.admm_rcpp(m, y, lam, ref_th, ref_u, lam / 5, deltas, order=0 if order == "cpp" else 1,
+                            weighted=1 if weighted else 0, fixed_iters=iters, pcg_rtol=1e-13)
+    assert st["iters"] == iters and rho == rs["rho"]
+    assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
+    assert np.max(np.abs(u - ref_u)) <= 1e-9 * max(1.0, np.max(np.abs(ref_u)))
+    del tm
+
+
+def test_fused4d_kernel_is_the_one_timed():
+    """At 4-D the loop's edge work runs in k_admm4a (timing id admm_fused4), not k_edge4d / k_gather4a."""
+    m = [32, 32, 32, 8]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        P.state_set(np.full(y.size, y.mean()), None, 0.2)
+        P.timing(True)
+        P.run(1.0, fixed_iters=4)
+        tm = P.timings()
+    assert tm["admm_fused4"]["launches"] == 4 and tm["edge_update"]["launches"] == 0
+    assert tm["gather4_b"]["launches"] == 4 and tm["gather_Dt"]["launches"] == 1   # D^T u0 only

@@ -117,9 +117,9 @@ def test_uneven_infeasible_line_split_fails_on_every_rank():
 
 
 @pytest.mark.parametrize("m,world", [([60, 60, 45], 3), ([24, 24, 37], 2), ([48, 48, 130], 4), ([40, 100], 4),
-                                     ([31, 31, 40], 2), ([24, 24, 37], 1)],
+                                     ([62, 62, 40], 2), ([24, 24, 37], 1)],
                          ids=["3d_60x60x45_w3_mixed_radix", "3d_24x24x37_w2_prime_last", "3d_48x48x130_w4",
-                              "2d_40x100_w4", "3d_31x31x40_w2_bluestein_lead", "3d_24x24x37_w1_bluestein_last"])
+                              "2d_40x100_w4", "3d_62x62x40_w2_bluestein_lead", "3d_24x24x37_w1_bluestein_last"])
 def test_slab_any_last_dimension_vs_c_oracle(m, world):
     """The last dimension's line solves are substructured over the ranks, so it may have any length (37 is
     prime; 45, 130 not powers of two) and the leading dims any 2-3-5-7 length (k_dctg passes): 12 fixed

@@ -105,12 +105,10 @@ def test_spectral_residual_baseline_sizes(m):
 
 
 @pytest.mark.parametrize("m", [[256, 256, 128], [512, 512, 128], [1024, 1024, 128], [256, 256, 300], [512, 512, 135]])
-def test_marching_passes_residual(m):
-    """3-D meshes solved as dim-2 forward, k_march forward (dim-0 DCT + Thomas forward elimination along dim 1),
-    k_march backward, dim-2 inverse (mvtv_spectral.hip): residual through the stencil operator at sigma = 0 (c1 = 0:
-    the closed form's q = 0 branch), a weak, a moderate and a dominant coupling, with the w0 of a weighted
-    preconditioner solve; 256 / 512 / 1024-point rows, dim-2 lengths a power of two, 300 = 4 3 5^2 (k_dctg) and
-    135 = 27 5 (k_dctg)."""
+def test_3d_solve_residual_extreme_sigma(m):
+    """3-D spectral solves (k_dct8 / k_dctg passes, k_tri along the last dimension) from sigma = 0 (the identity) to a
+    dominant coupling (cond ~ 1e7): residual through the stencil operator within the backward-stable bound;
+    256 / 512 / 1024-point rows, last-dimension lengths a power of two, 300 = 4 3 5^2 and 135 = 27 5 (k_trig)."""
     p = len(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     N = int(np.prod(m))

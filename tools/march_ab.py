@@ -1,5 +1,5 @@
 """Same-process A/B of the k_march 3-D solve (dim 2 first, marching dim-0 transforms + dim-1 Thomas) against the
-five-pass solve (MVTV_MARCH_OFF=1): ADMM it/s without events and the per-kernel times with them, interleaved.
+five-pass solve (MVTV_MARCH=0): ADMM it/s without events and the per-kernel times with them, interleaved.
 Needs the probe build (make PROBES=1 OUT=../lib_probe; MVTV_LIB_PATH=.../lib_probe/libmvtv.so)."""
 import os
 import sys
@@ -23,9 +23,9 @@ def main():
             for rep in range(3):
                 for off in ("0", "1"):
                     if off == "1":
-                        os.environ["MVTV_MARCH_OFF"] = "1"
+                        os.environ.pop("MVTV_MARCH", None)
                     else:
-                        os.environ.pop("MVTV_MARCH_OFF", None)
+                        os.environ["MVTV_MARCH"] = "1"
                     P.state_set(th0, None, 0.2)
                     P.run(1.0, fixed_iters=3)
                     t0 = time.perf_counter()
