@@ -18,7 +18,8 @@ import re
 import sys
 from collections import defaultdict
 
-NAMES = {"k_plane8": "dct_plane", "k_admm3d": "admm_fused", "k_admm3a": "admm_fused", "k_gather4a": "gather_Dt", "k_gather4b": "gather4_b", "k_edge3d": "edge_update", "k_gather3d": "gather_Dt", "k_dct8": "dct",
+NAMES = {"k_plane8": "dct_plane", "k_admm3d": "admm_fused", "k_admm3a": "admm_fused", "k_admm4a": "admm_fused4",
+         "k_gather4a": "gather_Dt", "k_gather4b": "gather4_b", "k_edge3d": "edge_update", "k_gather3d": "gather_Dt", "k_dct8": "dct",
          "k_dct": "dct", "k_dctg": "dct", "k_tri": "dct_tri", "k_trig": "dct_tri",
          "k_cg3d": "pcg_fused3d", "k_edge_update": "edge_update", "k_gather": "gather_Dt",
          "k_apply_A": "pcg_apply_A", "k_pcg_update": "pcg_update", "k_pcg_pupdate": "pcg_direction",
@@ -53,6 +54,15 @@ def read_counter(d: str, counter: str):
     for k, v in per.items():
         hi = max(v)
         real = [x for x in v if x >= 0.02 * hi] or v
+        # the first pass forms b from oty, g_alpha, g_u (4N words: an ADMM run's first iteration, or after a rho
+        # change) or from oty and the folded s (3N): one kernel, two traffic classes, split at the gap so each
+        # launch class reconciles with its own model (mvtv_timing_get's dct_first / dct_first_fold)
+        if k in ("dct_first", "dct_plane_first") and min(real) > 0 and max(real) / min(real) > 1.15:
+            mid = 0.5 * (min(real) + max(real))
+            lo, up = [x for x in real if x < mid], [x for x in real if x >= mid]
+            out[k + "_fold"], cnt[k + "_fold"] = sum(lo) / len(lo), len(lo)
+            out[k], cnt[k] = sum(up) / len(up), len(up)
+            continue
         out[k] = sum(real) / len(real)
         cnt[k] = len(real)
     return out, cnt
@@ -81,8 +91,9 @@ def main(out_dir: str, dest: str | None):
                            "write_factor_16B": w16},
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
-        rd = fetch.get(k, 0.0) * 1024 * (f8 or 1.0)
-        wr = write.get(k, 0.0) * 1024 * (w8 or 1.0)
+        base = k[:-5] if k.endswith("_fold") else k   # a split class's other counter may not have split (equal sizes)
+        rd = fetch.get(k, fetch.get(base, 0.0)) * 1024 * (f8 or 1.0)
+        wr = write.get(k, write.get(base, 0.0)) * 1024 * (w8 or 1.0)
         out["kernels"][k] = {"read_bytes": rd, "write_bytes": wr, "hbm_bytes": rd + wr,
                              "launches_sampled": nf.get(k, 0)}
         out[k] = rd + wr
