@@ -492,11 +492,11 @@ def independent_main(a, D, comm=None):
     opts = dict(fixed_iters=a.warmup, pcg_rtol=a.pcg_rtol, theta_solver=solver)
     if a.warmup > 0:
         P.run(lam, **opts)
-    # Meshes under 2^24 nodes run ~70-200 us iterations, where the per-launch timing events cost ~30 % (1024^2:
-    # 14.1k against 10.1k ADMM it/s, profiles/r04/v1_launch_gap): the value comes from an event-free timed region
-    # and the per-kernel table from a second region of the same length right after it. Larger meshes (the 512^3
-    # headline) time one region with the events in it.
-    event_free = P.N < (1 << 24)
+    # Meshes up to 2^24 nodes run 0.07-0.9 ms iterations, where the per-launch timing events cost 7-30 % (1024^2:
+    # 14.1k against 10.1k ADMM it/s, profiles/r04/v1_launch_gap; 256^3: 1166-1174 against 1086-1113): the value comes
+    # from an event-free timed region and the per-kernel table from a second region of the same length right after
+    # it. Larger meshes (the 512^3 headline: ~1 %) time one region with the events in it.
+    event_free = P.N <= (1 << 24)
     D.barrier()
     P.timing(not event_free)
     t0 = time.perf_counter()

@@ -40,3 +40,41 @@ def test_one_gpu_runs_in_process():
     assert r.returncode == 0
     x = json.loads(r.stdout.strip().splitlines()[-1])
     assert x["env"]["RANK"] is None and x["env"]["WORLD_SIZE"] is None
+
+
+_AGREE = r"""
+import os, sys, time
+sys.path.insert(0, {root!r})
+import bench
+D = bench.Dist("gloo")
+if D.rank == 1 and {stall}:
+    time.sleep(8)            # a peer stuck elsewhere (e.g. inside an RCCL collective) never joins
+    print("peer", flush=True)
+else:
+    t0 = time.time()
+    r = D.allreduce_within([float(D.rank + 1)], 3.0)
+    print("agreed" if r is not None else "none", r, round(time.time() - t0, 1), flush=True)
+"""
+
+
+def _two_ranks(stall):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", _AGREE.format(root=ROOT, stall=stall)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=ROOT))
+    return [p.communicate(timeout=120)[0].strip().splitlines()[-1] for p in procs]   # (after gloo's banner)
+
+
+def test_bounded_agreement_after_a_slab_failure():
+    """bench.py's N > 1 fallback: the agreement after a failed slab run gives up after its bound when a peer never
+    joins (then the failing rank prints what it has and exits non-zero), and agrees when every rank joins."""
+    out = _two_ranks(stall=True)
+    assert out[0].startswith("none") and float(out[0].split()[-1]) < 7.0
+    out = _two_ranks(stall=False)
+    assert out[0].startswith("agreed") and "[2.0]" in out[0]

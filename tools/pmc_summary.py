@@ -33,6 +33,8 @@ def short(kname: str) -> str:
                 return "pcg_init"
             if k in ("k_dct8", "k_dct") and re.search(r"k_dct8?<[^>]*true, true", kname):
                 return "dct_first"   # the pass that forms b on load (FORMB)
+            if k == "k_gather4b" and not re.search(r"k_gather4b<1, true>", kname):
+                return "gather4_b_init"   # D^T u0 at a run's start (explicit u, no g_uprev: 3N), not the loop's 7N
             if k == "k_plane8" and re.search(r"k_plane8<\d+, 0, true>", kname):
                 return "dct_plane_first"   # both in-plane forward passes, b formed on load
             return v
