@@ -233,8 +233,10 @@ mvtv_status pcg_solve(mvtv_problem* P, double sigma, const double* oty, const do
     auto enqueue = [&](int j) -> mvtv_status {
         if (fused) {
             int hh = P->tstart(MVTV_K_PCG_FUSED);
-            HIP_TRY(launch_cg3d(P->g, P->stream, j == 0 ? 1 : 2, sigma, P->wmode, w, x, rb[j & 1], pb[j & 1],
-                                rb[(j + 1) & 1], pb[(j + 1) & 1], oty, ga, ca, gb, cb, P->st, P->partials, &nb));
+            // x moves in odd iterations only (both steps, k_cg3d); k_cg_xflush applies an even last one's
+            HIP_TRY(launch_cg3d(P->g, P->stream, j == 0 ? 1 : ((j & 1) ? 3 : 2), sigma, P->wmode, w, x, rb[j & 1],
+                                pb[j & 1], rb[(j + 1) & 1], pb[(j + 1) & 1], oty, ga, ca, gb, cb, P->st, P->partials,
+                                &nb));
             P->tstop(hh);
             hh = P->tstart(MVTV_K_REDUCE);
             HIP_TRY(launch_finalize(P->stream, P->partials, nb, 4, 0, 5, nullptr, P->st));
@@ -276,6 +278,12 @@ mvtv_status pcg_solve(mvtv_problem* P, double sigma, const double* oty, const do
         P->harvest();
         if (P->host_st->done || enq >= maxit) break;
         batch = 2;
+    }
+    if (fused) {   // an even last iteration's x step (p_i of an even i is in pb[1])
+        h = P->tstart(MVTV_K_OTHER);
+        HIP_TRY(launch_cg_xflush(P->stream, P->g.N, x, pb[1], P->st));
+        P->tstop(h);
+        if (P->timing) P->pcg_xmoves += P->host_st->iter / 2;
     }
     *iters = P->host_st->iter;
     P->pcg_hint = *iters;
@@ -329,7 +337,7 @@ void fft_ld(std::vector<std::complex<long double>>& x) {
 
 // Bluestein tables of one dimension (SpecPlan::blu layout): chirp c[n] = e^{-i pi n^2/m} (n^2 mod 2m exactly), the
 // transforms / M of the kernels b_f[j] = conj c[|j|] (forward DFT, s = -1) and b_i[j] = c[|j|] (inverse, s = +1)
-// wrapped to length M, and the length-M twiddles e^{-2 pi i k/M}, k < M/2
+// wrapped to length M, and the length-M twiddles e^{-2 pi i k/M}, k < M
 void bluestein_tables(uint32_t m, uint32_t M, std::vector<double>& out) {
     const long double pi = 3.141592653589793238462643383279502884L;
     std::vector<std::complex<long double>> c(m), bf(M, 0.0L), bi(M, 0.0L);
@@ -357,7 +365,7 @@ void bluestein_tables(uint32_t m, uint32_t M, std::vector<double>& out) {
             out.push_back(double((*v)[k].real() / (long double)M));
             out.push_back(double((*v)[k].imag() / (long double)M));
         }
-    for (uint32_t k = 0; k < M / 2; ++k) {
+    for (uint32_t k = 0; k < M; ++k) {   // (k_dctb reads k < M/2, k_dctb8's radix-8 stages k < M)
         const long double ang = -2.0L * pi * (long double)k / (long double)M;
         out.push_back(double(cosl(ang)));
         out.push_back(double(sinl(ang)));
@@ -1846,6 +1854,7 @@ mvtv_status mvtv_timing_enable(mvtv_problem* P, int32_t on) {
         P->launches[k] = 0;
     }
     P->fold_fix = 0;
+    P->pcg_xmoves = 0;
     return MVTV_OK;
 }
 
@@ -1874,7 +1883,9 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
         case MVTV_K_PCG_APPLY: b = 8.0 * ((2.0 + w) * N); break;        // p (+W) in, q out
         case MVTV_K_PCG_UPDATE: b = 8.0 * ((6.0 + w) * N); break;       // x, r, p, q (+W) in, x, r out
         case MVTV_K_PCG_DIRECTION: b = 8.0 * ((3.0 + w) * N); break;    // r, p (+W) in, p out
-        case MVTV_K_PCG_FUSED: b = 8.0 * ((6.0 + w) * N); break;        // x, r, p (+W) in, x, r, p out
+        case MVTV_K_PCG_FUSED:   // r, p (+W) in, r, p out; + x in/out in the odd iterations (mean over the launches)
+            b = 8.0 * N * (4.0 + w + (P->launches[kid] > 0 ? 2.0 * double(P->pcg_xmoves) / double(P->launches[kid]) : 0.0));
+            break;
         case MVTV_K_DCT_FIRST: b = 8.0 * 4.0 * N; break;                 // oty, g_alpha, g_u in, x out
         case MVTV_K_DCT_FOLD:   // oty, s in, x out; + g_u in the launches after a rho change (mean over the launches)
             b = 8.0 * N * (3.0 + (P->launches[kid] > 0 ? double(P->fold_fix) / double(P->launches[kid]) : 0.0));

@@ -14,9 +14,13 @@
 //   reductions: gamma = (r_{i+1}, u_{i+1}), delta = (w_{i+1}, u_{i+1}), |r_{i+1}|^2
 //   next (k_finalize op 5): beta = gamma'/gamma, alpha = gamma' / (delta' - beta gamma'/alpha)
 //
-// HBM traffic per iteration is 6N words (read x, r, p; write x, r, p) against 11N for the
-// three-kernel PCG. r and p ping-pong between two buffers: a launch reads neighbour halos of
-// r_i and p_{i-1} that their owning workgroups overwrite.
+// x is needed only at the end, and iteration i+1 reads p_i anyway (as p_{i-1} of its direction), so
+// x moves every other iteration: even iterations leave it alone, odd ones apply both steps,
+// x += alpha_{i-1} p_{i-1} + alpha_i p_i (the same two fmas in the same order as one step per
+// iteration, so x is bit-identical), and k_cg_xflush applies a pending step once the solve ends on
+// an even iteration. HBM traffic per iteration is 4N words (read r, p; write r, p) and 6N (x too)
+// alternately, 5N on average, against 11N for the three-kernel PCG. r and p ping-pong between two
+// buffers: a launch reads neighbour halos of r_i and p_{i-1} that their owning workgroups overwrite.
 //
 // Geometry. A 512-thread workgroup owns a 60 x 20 column of the (dim 0, dim 1) plane over a
 // chunk of dim-2 planes and marches through dim 2. Each plane is staged in LDS as a 64 x 24
@@ -107,7 +111,8 @@ __device__ __forceinline__ void wave_rows(const double* img, const double* K, do
 }
 
 // MODE 0: prologue (r0 = b - A x0 with b = oty + ca ga + cb gb; reductions gamma0, delta0,
-// |r0|^2, |b|^2); MODE 1: first iteration (beta = 0, p_{-1} not read); MODE 2: iteration.
+// |r0|^2, |b|^2); MODE 1: first iteration (beta = 0, p_{-1} not read); MODE 2: iteration;
+// MODE 3: iteration that also moves x by both its own step and the previous one's.
 template <int WM, int MODE, int NWV>
 __global__ __launch_bounds__(cg3d::Shape<NWV>::NT, 32 / NWV) void k_cg3d(const Cg3dArgs a) {
     using namespace cg3d;
@@ -118,7 +123,8 @@ __global__ __launch_bounds__(cg3d::Shape<NWV>::NT, 32 / NWV) void k_cg3d(const C
     __shared__ double sD[8];     // 1 / diag (W = I) or sigma diag(D^T D) (W diagonal), by pattern
     if (MODE != 0 && a.st->done) return;
     const double alpha = MODE == 0 ? 0.0 : a.st->alpha;
-    const double beta = MODE == 2 ? a.st->beta : 0.0;
+    const double alpha_prev = MODE == 3 ? a.st->alpha_prev : 0.0;
+    const double beta = MODE >= 2 ? a.st->beta : 0.0;
     if (threadIdx.x < 8) sD[threadIdx.x] = WM == W_DIAG ? a.acc[threadIdx.x] : 1.0 / (1.0 + a.acc[threadIdx.x]);
 
     const int m0 = a.m0, m1 = a.m1, m2 = a.m2;
@@ -259,12 +265,13 @@ __global__ __launch_bounds__(cg3d::Shape<NWV>::NT, 32 / NWV) void k_cg3d(const C
                 qx[k] = ld(a.x, zoff, k);
             } else {
                 qr[k] = ld(a.r_in, zoff, k);
-                if (MODE == 2) qp[k] = ld(a.p_in, zoff, k);
+                if (MODE >= 2) qp[k] = ld(a.p_in, zoff, k);
                 if (WM == W_DIAG) qw[k] = ld(a.wdiag, zoff, k);
                 // unconditional (every address is valid): a conditional load into the queue
                 // gets its stores merged with a dynamic index, which demotes qx to scratch
-                qx[k] = *reinterpret_cast<const double*>(
-                    reinterpret_cast<const char*>(a.x + zoff + xrowoff[k]) + boff);
+                if (MODE == 3)
+                    qx[k] = *reinterpret_cast<const double*>(
+                        reinterpret_cast<const char*>(a.x + zoff + xrowoff[k]) + boff);
             }
         }
     };
@@ -278,12 +285,12 @@ __global__ __launch_bounds__(cg3d::Shape<NWV>::NT, 32 / NWV) void k_cg3d(const C
                 sP[li + k * IW] = qx[k];
             } else {
                 double pi = minv(qr[k], qw[k], k, zp);
-                if (MODE == 2) pi = fma(beta, qp[k], pi);
+                if (MODE >= 2) pi = fma(beta, qp[k], pi);
                 sP[li + k * IW] = pi;
                 rz[k] = qr[k];
                 if (ownz && own_y[k] && own_x) {
                     st(a.p_out, zoff, k, pi);
-                    st(a.x, zoff, k, fma(alpha, pi, qx[k]));
+                    if (MODE == 3) st(a.x, zoff, k, fma(alpha, pi, fma(alpha_prev, qp[k], qx[k])));
                 }
             }
         }
@@ -416,13 +423,32 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
         if (wmode == W_DIAG) {
             if (mode == 0) return go(k_cg3d<W_DIAG, 0, NV>);
             if (mode == 1) return go(k_cg3d<W_DIAG, 1, NV>);
-            return go(k_cg3d<W_DIAG, 2, NV>);
+            if (mode == 2) return go(k_cg3d<W_DIAG, 2, NV>);
+            return go(k_cg3d<W_DIAG, 3, NV>);
         }
         if (mode == 0) return go(k_cg3d<W_IDENTITY, 0, NV>);
         if (mode == 1) return go(k_cg3d<W_IDENTITY, 1, NV>);
-        return go(k_cg3d<W_IDENTITY, 2, NV>);
+        if (mode == 2) return go(k_cg3d<W_IDENTITY, 2, NV>);
+        return go(k_cg3d<W_IDENTITY, 3, NV>);
     };
+    if (mode < 0 || mode > 3) return hipErrorInvalidValue;
     return nwv == 16 ? pick(std::integral_constant<int, 16>{}) : pick(std::integral_constant<int, 8>{});
+}
+
+// x += alpha_prev p when the solve stopped after an even iteration (st->iter odd): that iteration's step is the one
+// k_cg3d left pending. Enqueued once after the iterations; a no-op otherwise.
+__global__ __launch_bounds__(256) void k_cg_xflush(uint64_t n, double* __restrict__ x, const double* __restrict__ p,
+                                                   const PcgState* __restrict__ st) {
+    if ((st->iter & 1) == 0) return;
+    const double al = st->alpha_prev;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
+        x[i] = fma(al, p[i], x[i]);
+}
+
+hipError_t launch_cg_xflush(hipStream_t s, uint64_t n, double* x, const double* p, const PcgState* st) {
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 8192);
+    klaunch(k_cg_xflush, dim3(uint32_t(std::max<uint64_t>(blocks, 1))), dim3(256), 0, s, n, x, p, st);
+    return hipGetLastError();
 }
 
 

@@ -112,6 +112,7 @@ enum PcgRed { PR_B2 = 0, PR_RZ = 1, PR_R2 = 2, PR_N = 3 };
 struct PcgState {
     double gamma;    // r.z
     double alpha, beta;
+    double alpha_prev;   // the alpha of the last iteration run (k_cg3d's deferred x update, k_cg_xflush)
     double rnorm2, bnorm2;
     double rtol2;
     int32_t iter, maxit;
@@ -216,6 +217,7 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
                        double* x, const double* r_in, const double* p_in, double* r_out, double* p_out,
                        const double* oty, const double* ga, double ca,
                        const double* gb, double cb, const PcgState* st, double* partials, int* nblocks_out);
+hipError_t launch_cg_xflush(hipStream_t s, uint64_t n, double* x, const double* p, const PcgState* st);
 hipError_t launch_maxabsdiff(const Geom& g, const Launch& L, const double* a, const double* b, double* partials);
 hipError_t launch_fill(hipStream_t s, double* x, double v, uint64_t n);
 // CG vector steps of lam_max_pinv (op 0 |x|^2 into partials, 1 x += c p & y -= c t, 2 x = p + c x, 3 y -= c t)
@@ -250,7 +252,7 @@ struct SpecPlan {
     uint32_t* perm = nullptr; // per dim (at lam_off): position of sample k in the mixed-radix FFT's input order
     uint32_t tw_off[kMaxDims] = {0, 0, 0, 0}, twq_off[kMaxDims] = {0, 0, 0, 0}, lam_off[kMaxDims] = {0, 0, 0, 0};
     // lengths without a 2-3-5-7 plan (Bluestein, k_dctb): per such dim, at blu_off (doubles), m complex chirp values
-    // e^{-i pi n^2/m}, then M values each of the forward and inverse kernels' transforms / M, then M/2 twiddles
+    // e^{-i pi n^2/m}, then M values each of the forward and inverse kernels' transforms / M, then M twiddles
     // e^{-2 pi i k/M}; blu_M[j] = M = 2^ceil(log2(2 m_j - 1)), 0 for a planned dim
     double* blu = nullptr;
     uint32_t blu_off[kMaxDims] = {0, 0, 0, 0}, blu_M[kMaxDims] = {0, 0, 0, 0};

@@ -426,10 +426,10 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
                                                    AdmmCtl* ctl_step, const double* step_red) {
     if ((op == 2 || op == 3 || op == 5) && st->done) return;
     if (ctl && ctl->done) return;
-    // lane t sums rows t, t + 1024, ... in order for every slot k, then one halving tree over all slots
-    // (the same per-slot order as one tree per slot; 10 barriers instead of 10 nr). Rows are loaded in
-    // batches of 4 (4 nr loads in flight per lane).
-    __shared__ double sm[kMaxRed][1024];
+    // lane t sums rows t, t + 1024, ... in order for every slot k (rows loaded in batches of 4: 4 nr loads in flight
+    // per lane), then a fixed shuffle tree within each wave and one over the 16 wave sums: one barrier instead of the
+    // 10 of an LDS halving tree (1024^2: the launch 10.6 us, 15 % of an iteration, before)
+    __shared__ double sm[kMaxRed][16];
     __shared__ double res[kMaxRed];
     double acc[kMaxRed];
 #pragma unroll
@@ -450,21 +450,35 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
             for (int k = 0; k < kMaxRed; ++k)
                 if (k < nr && b0 + u * 1024 < nparts) acc[k] = ((mxm >> k) & 1u) ? fmax(acc[k], v[u][k]) : acc[k] + v[u][k];
     }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < kMaxRed; ++k)
-        if (k < nr) sm[k][threadIdx.x] = acc[k];
-    __syncthreads();
-    for (int s = 512; s > 0; s >>= 1) {
-        if (threadIdx.x < s)
+    for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
-            for (int k = 0; k < kMaxRed; ++k)
-                if (k < nr)
-                    sm[k][threadIdx.x] = ((mxm >> k) & 1u) ? fmax(sm[k][threadIdx.x], sm[k][threadIdx.x + s])
-                                                          : sm[k][threadIdx.x] + sm[k][threadIdx.x + s];
-        __syncthreads();
-    }
-    if (threadIdx.x < nr) res[threadIdx.x] = sm[threadIdx.x][0];
+        for (int k = 0; k < kMaxRed; ++k)
+            if (k < nr) {
+                const double o = __shfl_down(acc[k], off, 64);
+                acc[k] = ((mxm >> k) & 1u) ? fmax(acc[k], o) : acc[k] + o;
+            }
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < kMaxRed; ++k)
+            if (k < nr) sm[k][wv] = acc[k];
     __syncthreads();
+    if (wv != 0) return;
+#pragma unroll
+    for (int k = 0; k < kMaxRed; ++k) acc[k] = (k < nr && lane < 16) ? sm[k][lane] : 0.0;
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < kMaxRed; ++k)
+            if (k < nr) {
+                const double o = __shfl_down(acc[k], off, 64);
+                acc[k] = ((mxm >> k) & 1u) ? fmax(acc[k], o) : acc[k] + o;
+            }
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < kMaxRed; ++k)
+            if (k < nr) res[k] = acc[k];
     if (threadIdx.x != 0) return;
     if (out)
         for (int k = 0; k < nr; ++k) out[k] = res[k];
@@ -495,6 +509,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
         st->gamma = res[0];
         st->rnorm2 = res[2];
         st->alpha = res[0] / res[1];
+        st->alpha_prev = 0.0;
         st->beta = 0.0;
         st->rtol2 = rtol2;
         st->maxit = maxit;
@@ -503,6 +518,7 @@ __global__ __launch_bounds__(1024) void k_finalize(const double* __restrict__ pa
     } else if (op == 5) {   // Chronopoulos-Gear scalar recurrences
         const double gnew = res[0], dnew = res[1];
         const double beta = gnew / st->gamma;
+        st->alpha_prev = st->alpha;
         st->alpha = gnew / (dnew - beta * gnew / st->alpha);
         st->beta = beta;
         st->gamma = gnew;

@@ -134,6 +134,7 @@ struct mvtv_problem {
     double ms[MVTV_K_COUNT] = {0};
     int64_t launches[MVTV_K_COUNT] = {0};
     int64_t fold_fix = 0;   // timed folded first passes that also read g_u (a rho change before them)
+    int64_t pcg_xmoves = 0;   // timed fused PCG iterations that also moved x (the odd ones)
 
     Launch L() const { return Launch{stream, grid}; }
 

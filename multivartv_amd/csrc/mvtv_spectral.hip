@@ -2080,8 +2080,234 @@ __global__ __launch_bounds__(dctb::NT) void k_dctb(const SpecArgs a) {
     }
 }
 
+// k_dctb8: the same Bluestein passes with k_dct8's register-resident radix-8 Stockham stages (stages_from) for the
+// length-M FFTs: a thread holds 8 complex values of one complex line (two real lines), LDS carries only the exchanges
+// between stages, both FFTs of a convolution leave natural order. The LDS-staged k_dctb spends ~20x the HBM bytes in
+// LDS traffic (every radix-2^2 stage a round trip through LDS for two length-M FFTs per transform) and runs at ~0.9 TB/s
+// (251^3); this keeps the working set of a stage in registers.
+template <int L, int MODE, bool D0, bool FORMB, int TQW>
+__global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dctb8(const SpecArgs a) {
+    using S = spec8::ShapeK<L, TQW>;
+    constexpr int M = S::M, TPL = S::TPL, NCL = S::NCL, R0 = S::R0;
+    double sigma = a.sigma, ca = a.ca, cb = a.cb;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+        ca = a.ctl->rho;
+        cb = a.ctl->rho * a.ctl->c_prev;
+    }
+    __shared__ double2 buf[NCL * S::LP];
+    __shared__ double lc0[2 * NCL], lc1[2 * NCL];
+    const int m = int(a.m[a.d]);
+    const int t = threadIdx.x;
+    const int j = D0 ? (t % TPL) : (t / NCL);
+    const int c = D0 ? (t / TPL) : (t % NCL);
+    const uint32_t q0 = blockIdx.x * uint32_t(TQW);
+    const int la = 2 * c, lb = 2 * c + 1;
+    const bool va = q0 + uint32_t(la) < a.nlines, vb = q0 + uint32_t(lb) < a.nlines;
+    double2* const X = buf + c * S::LP;
+    const int cx = c & 7;
+    const double2* __restrict__ tw = a.tw;       // length-M twiddles
+    const double2* __restrict__ chirp = a.bchirp;
+
+    for (int l = t; MODE == SPEC_MID && l < TQW; l += S::NT) {   // c0 + c1 lam_d(k) per line (k_dct8)
+        const uint32_t q = a.q_off + q0 + l;
+        double lamv[kMaxDims] = {0, 0, 0, 0};
+        uint32_t rest = (q - a.q_off) < a.nlines ? q : a.q_off;
+        const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
+        for (int jj = 0; jj < a.p; ++jj) {
+            if (jj == a.d) continue;
+            const uint32_t qq = (jj < jlast) ? a.fd[jj].div(rest) : 0u;
+            lamv[jj] = a.lam[a.lam_off[jj] + (rest - qq * a.m[jj])];
+            rest = qq;
+        }
+        double c0 = a.w0, c1 = 0.0;
+        for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
+            if (a.cS[Sm] == 0.0) continue;
+            double prod = sigma * a.cS[Sm];
+            for (int jj = 0; jj < a.p; ++jj)
+                if (jj != a.d && ((Sm >> jj) & 1)) prod *= lamv[jj];
+            if ((Sm >> a.d) & 1) c1 += prod;
+            else c0 += prod;
+        }
+        lc0[l] = c0;
+        lc1[l] = c1;
+    }
+
+    auto gaddr = [&](int ql, uint32_t k) -> uint32_t {
+        const uint32_t q = q0 + uint32_t(ql);
+        if (D0) return q * uint32_t(m) + k;
+        const uint32_t hi = a.fds.div(q);
+        return (q - hi * a.stride) + hi * a.stride * uint32_t(m) + k * a.stride;
+    };
+    auto ld1 = [&](int ql, uint32_t k) -> double {
+        const uint32_t gi = gaddr(ql, k);
+        double v = __builtin_nontemporal_load(a.in + gi);
+        if (FORMB) v += ca * __builtin_nontemporal_load(a.ga + gi) + cb * __builtin_nontemporal_load(a.gb + gi);
+        return v;
+    };
+    auto ld2 = [&](uint32_t k) {
+        return make_double2(va ? ld1(la, k) : 0.0, vb ? ld1(lb, k) : 0.0);
+    };
+    auto st2 = [&](uint32_t k, double2 v) {
+        if (va) __builtin_nontemporal_store(v.x, a.out + gaddr(la, k));
+        if (vb) __builtin_nontemporal_store(v.y, a.out + gaddr(lb, k));
+    };
+    // circular convolution with b (bhat = its transform / M) of u (u_at(n), n < M): natural order in X
+    auto convolve = [&](auto&& u_at, const double2* __restrict__ bhat) {
+        double2 z[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] = u_at(stage_in_pos<L, R0>(j, i));
+        stages_from<L, R0, 1, false, false>(z, j, X, cx, tw);   // DFT, natural order in X
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int n = stage_in_pos<L, R0>(j, i);
+            z[i] = cmul(X[spec8::slot(n, cx)], bhat[n]);
+        }
+        stages_from<L, R0, 1, true, false>(z, j, X, cx, tw);    // inverse DFT, natural order in X
+    };
+    const int half = m >> 1, npl = (m & 1) ? half + 1 : half;
+    // the inverse transform's input: V[k] conj c[k] at k < m (pairs (k, m - k)), zeros at [m, M)
+    auto put_v = [&](int k, double2 Xk, double2 Xmk) {
+        const bool self = k == 0, mid = self && !(m & 1);
+        const int ka = k, kb = self ? half : m - k;
+        const double2 q2 = cconj(a.twq[kb]);
+        if (self) {
+            X[spec8::slot(0, cx)] = cmul(Xk, cconj(chirp[0]));
+            if (mid) {
+                const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xmk.x));
+                const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xmk.y));
+                X[spec8::slot(kb, cx)] = cmul(make_double2(va2.x - vb2.y, va2.y + vb2.x), cconj(chirp[kb]));
+            }
+        } else {
+            const double2 q1 = cconj(a.twq[ka]);
+            const double2 va1 = cmul(q1, make_double2(Xk.x, -Xmk.x));
+            const double2 vb1 = cmul(q1, make_double2(Xk.y, -Xmk.y));
+            const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xk.x));
+            const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xk.y));
+            X[spec8::slot(ka, cx)] = cmul(make_double2(va1.x - vb1.y, va1.y + vb1.x), cconj(chirp[ka]));
+            X[spec8::slot(kb, cx)] = cmul(make_double2(va2.x - vb2.y, va2.y + vb2.x), cconj(chirp[kb]));
+        }
+    };
+    auto zero_pad = [&]() {
+        for (int n = m + j; n < M; n += TPL) X[spec8::slot(n, cx)] = make_double2(0.0, 0.0);
+    };
+
+    if (MODE != SPEC_INV) {
+        // forward: u[n] = y[n] c[n], y the Makhoul sequence of the two lines (sample k(n))
+        convolve(
+            [&](int n) {
+                if (n >= m) return make_double2(0.0, 0.0);
+                const int k = 2 * n < m ? 2 * n : 2 * (m - 1 - n) + 1;
+                return cmul(ld2(uint32_t(k)), chirp[n]);
+            },
+            a.bvf);
+        for (int k = j; k < npl; k += TPL) {   // Z[k] = c[k] conv[k] -> DCT-II coefficients of the pair (k, m - k)
+            const bool self = k == 0, mid = self && !(m & 1);
+            const int ka = k, kb = self ? half : m - k;
+            const double2 Z1 = cmul(X[spec8::slot(ka, cx)], chirp[ka]), q1 = a.twq[ka];
+            double2 Xk, Xmk = make_double2(0.0, 0.0);
+            if (self) {
+                Xk = make_double2(q1.x * Z1.x, q1.x * Z1.y);
+                if (mid) {
+                    const double2 Z2 = cmul(X[spec8::slot(kb, cx)], chirp[kb]), q2 = a.twq[kb];
+                    Xmk = make_double2(q2.x * Z2.x, q2.x * Z2.y);
+                }
+            } else {
+                const double2 Z2 = cmul(X[spec8::slot(kb, cx)], chirp[kb]), q2 = a.twq[kb];
+                const double2 Ap = make_double2(0.5 * (Z1.x + Z2.x), 0.5 * (Z1.y - Z2.y));
+                const double2 Bp = make_double2(0.5 * (Z1.y + Z2.y), -0.5 * (Z1.x - Z2.x));
+                Xk = make_double2(q1.x * Ap.x - q1.y * Ap.y, q1.x * Bp.x - q1.y * Bp.y);
+                Xmk = make_double2(q2.x * Ap.x + q2.y * Ap.y, q2.x * Bp.x + q2.y * Bp.y);
+            }
+            if (MODE == SPEC_FWD) {
+                st2(uint32_t(ka), Xk);
+                if (!self || mid) st2(uint32_t(kb), Xmk);
+                continue;
+            }
+            const double* lamd = a.lam + a.lam_off[a.d];
+            const double l1 = lamd[ka];
+            Xk.x *= a.inv_n / (lc0[la] + lc1[la] * l1);
+            Xk.y *= a.inv_n / (lc0[lb] + lc1[lb] * l1);
+            if (!self || mid) {
+                const double l2 = lamd[kb];
+                Xmk.x *= a.inv_n / (lc0[la] + lc1[la] * l2);
+                Xmk.y *= a.inv_n / (lc0[lb] + lc1[lb] * l2);
+            }
+            put_v(k, Xk, Xmk);
+        }
+        if (MODE == SPEC_FWD) return;
+    } else {
+        for (int k = j; k < npl; k += TPL) {   // coefficients (k, m - k) from HBM
+            const bool self = k == 0, mid = self && !(m & 1);
+            const double2 Xk = ld2(uint32_t(k));
+            const double2 Xmk = (!self || mid) ? ld2(uint32_t(self ? half : m - k)) : make_double2(0.0, 0.0);
+            put_v(k, Xk, Xmk);
+        }
+    }
+    zero_pad();
+    __syncthreads();
+    convolve([&](int n) { return X[spec8::slot(n, cx)]; }, a.bvi);
+    for (int k = j; k < m; k += TPL) {   // sample k = conj c[n] conv[n], n its Makhoul position
+        const int n = (k & 1) ? m - 1 - (k >> 1) : (k >> 1);
+        st2(uint32_t(k), cmul(X[spec8::slot(n, cx)], cconj(chirp[n])));
+    }
+}
+
+// k_dctb8's tile: k_dct8's default real lines per workgroup (16, fewer for M > 512), at least one wave of threads
+template <int L>
+constexpr int dctb8_tq() {
+    constexpr int TQ = spec8::Shape<L>::TQ, TPL = spec8::Shape<L>::TPL;
+    return TQ < 2 ? 2 : ((TQ / 2) * TPL >= 64 ? TQ : 2 * (64 / TPL));
+}
+
+template <int L>
+static void launch_dctb8_l(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
+    constexpr int TQW = dctb8_tq<L>();
+    const dim3 grid((a.nlines + uint32_t(TQW) - 1) / uint32_t(TQW)), block(spec8::ShapeK<L, TQW>::NT);
+#define MVTV_DCTB8(MODE, D0, FB) klaunch(k_dctb8<L, MODE, D0, FB, TQW>, grid, block, 0, s, a)
+    if (mode == SPEC_FWD) {
+        if (d0) {
+            if (formb) MVTV_DCTB8(SPEC_FWD, true, true);
+            else MVTV_DCTB8(SPEC_FWD, true, false);
+        } else if (formb) {
+            MVTV_DCTB8(SPEC_FWD, false, true);
+        } else {
+            MVTV_DCTB8(SPEC_FWD, false, false);
+        }
+    } else if (mode == SPEC_INV) {
+        if (d0) MVTV_DCTB8(SPEC_INV, true, false);
+        else MVTV_DCTB8(SPEC_INV, false, false);
+    } else {
+        if (d0) {
+            if (formb) MVTV_DCTB8(SPEC_MID, true, true);
+            else MVTV_DCTB8(SPEC_MID, true, false);
+        } else if (formb) {
+            MVTV_DCTB8(SPEC_MID, false, true);
+        } else {
+            MVTV_DCTB8(SPEC_MID, false, false);
+        }
+    }
+#undef MVTV_DCTB8
+}
+
 static hipError_t launch_dctb(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
     const int M = 1 << a.L;
+    if (!probe_env("MVTV_DCTB_LDS")) {   // the register-stage form (probe builds: MVTV_DCTB_LDS=1 keeps k_dctb)
+        switch (a.L) {
+            case 5: launch_dctb8_l<5>(a, s, mode, d0, formb); return hipGetLastError();
+            case 6: launch_dctb8_l<6>(a, s, mode, d0, formb); return hipGetLastError();
+            case 7: launch_dctb8_l<7>(a, s, mode, d0, formb); return hipGetLastError();
+            case 8: launch_dctb8_l<8>(a, s, mode, d0, formb); return hipGetLastError();
+            case 9: launch_dctb8_l<9>(a, s, mode, d0, formb); return hipGetLastError();
+            case 10: launch_dctb8_l<10>(a, s, mode, d0, formb); return hipGetLastError();
+            case 11: launch_dctb8_l<11>(a, s, mode, d0, formb); return hipGetLastError();
+            case 12: launch_dctb8_l<12>(a, s, mode, d0, formb); return hipGetLastError();
+            case 13: launch_dctb8_l<13>(a, s, mode, d0, formb); return hipGetLastError();
+            default: break;
+        }
+    }
     // <= 16 lines in <= 64 KB of LDS (two complex lines' worth at least); M = 8192 takes one line pair in 128 KB
     int tq = 16;
     while (tq > 2 && size_t(tq / 2) * size_t(M + spec::PAD) * sizeof(double2) > 65536) tq /= 2;

@@ -69,6 +69,45 @@ def test_pcg_solve(m, deltas, order, unit):
     P.close()
 
 
+def _jacobi_pcg(D, w, sigma, b, x, k):
+    """k iterations of textbook Jacobi-PCG (numpy): the iterates the fused 3-D kernel's single-reduction form
+    reproduces up to rounding (rcpp-code/MultivarTV/src/solvers.cpp:113 solves the same system directly)."""
+    dinv = 1.0 / (w + sigma * np.asarray((D.T @ D).diagonal()).ravel())
+    x = x.copy()
+    r = b - O.apply_A(D, w, sigma, x)
+    z = dinv * r
+    p = z.copy()
+    rz = r @ z
+    for _ in range(k):
+        q = O.apply_A(D, w, sigma, p)
+        al = rz / (p @ q)
+        x += al * p
+        r -= al * q
+        z = dinv * r
+        rz, rz0 = r @ z, rz
+        p = z + (rz / rz0) * p
+    return x
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_fused_pcg_stops_after_odd_and_even_iterations(weighted):
+    """k_cg3d moves x only in odd iterations (both steps); k_cg_xflush applies the step an even last iteration
+    left pending: x after k = 1..6 iterations (rtol unreachable, so max_iter stops the solve) against numpy."""
+    rng = np.random.default_rng(5)
+    m = [9, 9, 9]
+    N = int(np.prod(m))
+    w = rng.uniform(0.5, 2.0, N) if weighted else np.ones(N)
+    P, D, _ = _problem(m, [0.5, 0.25, 0.125], "cpp", False, wdiag=w if weighted else None)
+    b = rng.standard_normal(N)
+    x0 = rng.standard_normal(N)
+    sigma = 2.7
+    for k in range(1, 7):
+        x, it, _ = P.solve(sigma, b, x0=x0, rtol=1e-300, max_iter=k)
+        assert it == k
+        assert _rel(x, _jacobi_pcg(D, w, sigma, b, x0, k)) <= 1e-11, k
+    P.close()
+
+
 def test_dim_mismatch_raises():
     with pytest.raises(mv.DimMismatchError):
         mv.Problem([4, 3, 5], np.zeros(60), deltas=[1, 1, 1])

@@ -6,9 +6,13 @@ R=$GRAFT_REPO_ROOT
 O=${REL_OUT:-gpurun_out/rel}
 mkdir -p $R/$O
 cd $R
-timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1
-rc=$?; tail -2 $O/gpu_tests.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests rc=$rc: stopping"; exit $rc; fi
+# SKIP_TESTS=1: the evidence steps only (the suite in a call of its own: gpurun's 20-minute cap)
+rc=0
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1
+  rc=$?; tail -2 $O/gpu_tests.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests rc=$rc: stopping"; exit $rc; fi
+fi
 timeout -k 10 60 tools/bin/stream_bench > $O/stream.txt 2>&1 &&
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err &&
 cd /tmp && export TMPDIR=/tmp &&
