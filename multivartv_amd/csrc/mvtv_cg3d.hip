@@ -355,13 +355,23 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
     a.tiles_y = (a.m1 + TY - 1) / TY;
     const int tiles = a.tiles_x * a.tiles_y;
     // dim-2 chunks: each costs 3 extra plane steps (halo planes); workgroups run in rounds of
-    // `slots` (2 per CU), so pick the chunk count with the fewest plane steps per slot
+    // `slots` (resident workgroups per CU x CUs), so pick the chunk count with the fewest plane steps per
+    // slot. At 128 VGPRs a CU holds 16 waves: one 1024-thread workgroup (round 2's model assumed two, and
+    // chose 4 chunks = 432 workgroups = 1.7 rounds at 512^3; the occupancy query picks 7 = 2.95 rounds,
+    // 1.209 -> 1.193 ms per launch in a probe sweep, profiles/r04/v8_cg3d_chunks)
     static const int slots = [] {
-        int dev = 0, cus = 256;
+        int dev = 0, cus = 256, per_cu = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
-        return 2 * std::max(1, cus);
+        const hipError_t e = nwv == 16
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg3d<W_IDENTITY, 2, 16>, 1024, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cg3d<W_IDENTITY, 2, 8>, 512, 0);
+        if (e != hipSuccess || per_cu < 1) {
+            (void)hipGetLastError();
+            per_cu = 1;
+        }
+        return per_cu * std::max(1, cus);
     }();
     static const int nz_env = [] {
         const char* e = probe_env("MVTV_CG3D_NZ");

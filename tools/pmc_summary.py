@@ -29,8 +29,10 @@ NAMES = {"k_plane8": "dct_plane", "k_admm3d": "admm_fused", "k_admm3a": "admm_fu
 def short(kname: str) -> str:
     for k, v in NAMES.items():
         if re.search(r"\b" + k + r"\b", kname):
-            if k == "k_cg3d" and re.search(r"k_cg3d<\d+, 0>", kname):
-                return "pcg_init"
+            if k == "k_cg3d":   # <WM, MODE, NWV>: 0 prologue, 1 first iteration, 2 (x untouched), 3 (x moved)
+                mo = re.search(r"k_cg3d<\d+, (\d)", kname)
+                mode = int(mo.group(1)) if mo else 2
+                return {0: "pcg_init", 1: "pcg_fused3d_first", 2: "pcg_fused3d", 3: "pcg_fused3d_x"}[mode]
             if k in ("k_dct8", "k_dct") and re.search(r"k_dct8?<[^>]*true, true", kname):
                 return "dct_first"   # the pass that forms b on load (FORMB)
             if k == "k_gather4b" and not re.search(r"k_gather4b<1, true>", kname):
