@@ -14,7 +14,7 @@ for rep in $(seq 1 ${REPS:-1}); do
   i=0
   for v in NONE=0 ${SWEEP}; do
     env $v timeout -k 10 300 python bench.py --no-cpu --steps ${STEPS:-10} --warmup 3 ${BENCH_EXTRA} > $O/s$i.$rep.json 2> $O/s$i.$rep.err || { echo "bench $v failed"; tail -5 $O/s$i.$rep.err; exit 1; }
-    python -c "import json,sys; d=json.load(open(sys.argv[1])); p=d.get('pcg_leg') or {}; print(sys.argv[2], d['value'], 'pcg_leg', p.get('value'), p.get('kernel_avg_ms'))" $O/s$i.$rep.json "$v.$rep"
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); p=d.get('pcg_leg') or {}; print(sys.argv[2], d['value'], 'pcg_leg', p.get('value'), p.get('kernel_avg_ms'), {k: v['avg_ms'] for k, v in d.get('kernels', {}).items()})" $O/s$i.$rep.json "$v.$rep"
     i=$((i+1))
   done
 done
