@@ -430,12 +430,18 @@ __host__ __device__ constexpr int f3a_slot(int k) {   // image slot of block k (
     return (sprime_mask(block_code(k, 3, ORD), 3) & 3) != 0 ? n : -1;
 }
 
-template <int ORD, int UM, bool DTH, int NB>
+// TW (twin blocks, mvtv_internal.h twin_block): block KD carries the same numbers as block KC (same S', equal weight,
+// equal state; the host checks), so it is neither read nor written nor staged: KC's reductions count twice and its
+// gather terms enter with weight 2 w. The state's KD region is filled from KC once the run ends.
+template <int ORD, int UM, bool DTH, int NB, bool TW>
 __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __restrict__ szr, double (&red)[7], int X0,
                                             int Yh, int z0, int z1, double t_old, double c_old, double t_new,
                                             double c_prev, double rho_f) {
     constexpr int P = 3, NC = 8, IW = f3a::IW, IH = f3a::IH, NI = f3a_nimg<NB, ORD>();
+    constexpr int KD = TW ? twin_block(NB, P, ORD) : -1, KC = TW ? twin_canon(NB, P, ORD) : -1;
+    static_assert(!TW || (KD >= 0 && KC >= 0), "twin blocks");
     const Geom& g = a.g;
+    auto wgt = [&](int k) { return k == KC ? 2.0 * g.w[k] : g.w[k]; };   // exact doubling
     const int wv = int(threadIdx.x) >> 6, ln = int(threadIdx.x) & 63;
     const bool hcol = wv == IH;                 // the halo-column wave
     const int row = hcol ? ln : wv;
@@ -467,7 +473,8 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
             const bool need = cell && (!hrow || (S & 2)) && (!hcol || (S & 1));
-            zo[k] = need ? a.z_old[eix(g, k, i)] : 0.0;
+            if constexpr (k == KD) zo[k] = 0.0;
+            else zo[k] = need ? a.z_old[eix(g, k, i)] : 0.0;
         });
     };
     auto edge_cell = [&](int e, const double (&th0)[4], const double (&th1)[4], const double (&zo)[NB],
@@ -489,17 +496,22 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
         static_for<0, NB>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-            const double d = g.w[k] * v[S];
-            const double uo = (UM == U_EXPLICIT) ? zo[k] : -c_old * clampd(zo[k], t_old);
-            const double z = cell ? d - uo : 0.0;
-            zn[k] = z;
-            if (own) {
-                const double al = z - clampd(z, t_new);
-                const double r = al - d;
-                __builtin_nontemporal_store(z, a.z_new + eix(g, k, i));
-                red[0] = fma(r, r, red[0]);
-                red[1] = fma(d, d, red[1]);
-                red[2] = fma(al, al, red[2]);
+            if constexpr (k == KD) {
+                zn[k] = 0.0;
+            } else {
+                const double d = g.w[k] * v[S];
+                const double uo = (UM == U_EXPLICIT) ? zo[k] : -c_old * clampd(zo[k], t_old);
+                const double z = cell ? d - uo : 0.0;
+                zn[k] = z;
+                if (own) {
+                    const double al = z - clampd(z, t_new);
+                    const double r = al - d;
+                    __builtin_nontemporal_store(z, a.z_new + eix(g, k, i));
+                    constexpr double m = k == KC ? 2.0 : 1.0;   // the twin's rows: the same terms again
+                    red[0] = fma(m * r, r, red[0]);
+                    red[1] = fma(m * d, d, red[1]);
+                    red[2] = fma(m * al, al, red[2]);
+                }
             }
         });
     };
@@ -508,7 +520,7 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
         static_for<0, NB>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             constexpr int sl = f3a_slot<NB, ORD>(k);
-            if constexpr (sl >= 0) szr[sidx(buf, sl, row, col)] = zn[k];
+            if constexpr (sl >= 0 && k != KD) szr[sidx(buf, sl, row, col)] = zn[k];
         });
     };
     // in-plane backward sums Q_k of an owned cell: its own value from the register, the neighbours
@@ -551,11 +563,11 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
             static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                if constexpr ((S & 4) != 0) {
+                if constexpr ((S & 4) != 0 && k != KD) {
                     double qa, qu;
                     plane_q(kc, 1, zn[k], qa, qu);
-                    qa_prev = fma(g.w[k], qa, qa_prev);
-                    qu_prev = fma(g.w[k], qu, qu_prev);
+                    qa_prev = fma(wgt(k), qa, qa_prev);
+                    qu_prev = fma(wgt(k), qu, qu_prev);
                 }
             });
         }
@@ -586,13 +598,15 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
             static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                double qa, qu;
-                plane_q(kc, buf, zn[k], qa, qu);
-                ga = fma(g.w[k], qa, ga);
-                gu = fma(g.w[k], qu, gu);
-                if constexpr ((S & 4) != 0) {
-                    na = fma(g.w[k], qa, na);
-                    nu = fma(g.w[k], qu, nu);
+                if constexpr (k != KD) {
+                    double qa, qu;
+                    plane_q(kc, buf, zn[k], qa, qu);
+                    ga = fma(wgt(k), qa, ga);
+                    gu = fma(wgt(k), qu, gu);
+                    if constexpr ((S & 4) != 0) {
+                        na = fma(wgt(k), qa, na);
+                        nu = fma(wgt(k), qu, nu);
+                    }
                 }
             });
             ga -= qa_prev;
@@ -619,7 +633,7 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
     }
 }
 
-template <int ORD, int UM, bool DTH, int NB>
+template <int ORD, int UM, bool DTH, int NB, bool TW>
 __global__ __launch_bounds__(f3a::NT) void k_admm3a(const Fused3dArgs a) {
     constexpr int NT = f3a::NT, NI = f3a_nimg<NB, ORD>();
     double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new, c_prev = a.c_prev, rho_f = 0.0;
@@ -639,8 +653,8 @@ __global__ __launch_bounds__(f3a::NT) void k_admm3a(const Fused3dArgs a) {
         const int tz = bid / a.tpz, rem = bid - tz * a.tpz;
         const int z0 = a.zlo + tz * a.zchunk, z1 = min(a.zhi, z0 + a.zchunk);
         const int tyi = rem / a.tiles_x, txi = rem - tyi * a.tiles_x;
-        admm3a_tile<ORD, UM, DTH, NB>(a, szr, red, txi * 64, tyi * f3a::TY - 1, z0, z1, t_old, c_old, t_new, c_prev,
-                                      rho_f);
+        admm3a_tile<ORD, UM, DTH, NB, TW>(a, szr, red, txi * 64, tyi * f3a::TY - 1, z0, z1, t_old, c_old, t_new,
+                                          c_prev, rho_f);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -745,8 +759,12 @@ bool fused3d_ok(const Geom& g) {
 hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
                          double* z_new, double t_old, double c_old, double t_new, double c_prev,
                          const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
-                         double* partials, int* nparts, const AdmmCtl* ctl, bool fold) {
+                         double* partials, int* nparts, const AdmmCtl* ctl, bool fold, bool twin) {
     if (fold && ((g.p != 2 && g.p != 3) || !ctl)) return hipErrorInvalidValue;   // the folded b: asynchronous loop
+    if (twin) {   // the twin pair must exist and carry one weight (the host also checks the state)
+        const int kd = twin_block(g.nb, g.p, order), kc = twin_canon(g.nb, g.p, order);
+        if (g.p != 3 || kd < 0 || g.w[kd] != g.w[kc]) return hipErrorInvalidValue;
+    }
     if (g.p == 2)
         return launch_admm2d(g, order, umode, s, theta, z_old, z_new, t_old, c_old, t_new, c_prev, theta_old, g_alpha,
                              g_u, g_uprev, partials, nparts, ctl, fold);
@@ -772,19 +790,36 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
         klaunch(kern, dim3(grid), dim3(f3a::NT), 0, s, a);
         return hipGetLastError();
     };
-    if (order == 0) {
+    auto pick = [&](auto ordc, auto nbc, auto twc) {
+        constexpr int O = decltype(ordc)::value, NB = decltype(nbc)::value;
+        constexpr bool T = decltype(twc)::value;
         if (umode == U_EXPLICIT)
-            return dth ? go(k_admm3a<0, U_EXPLICIT, true, 7>) : go(k_admm3a<0, U_EXPLICIT, false, 7>);
-        return dth ? go(k_admm3a<0, U_FROM_Z, true, 7>) : go(k_admm3a<0, U_FROM_Z, false, 7>);
-    }
-    if (g.nb == 6) {
-        if (umode == U_EXPLICIT)
-            return dth ? go(k_admm3a<1, U_EXPLICIT, true, 6>) : go(k_admm3a<1, U_EXPLICIT, false, 6>);
-        return dth ? go(k_admm3a<1, U_FROM_Z, true, 6>) : go(k_admm3a<1, U_FROM_Z, false, 6>);
-    }
-    if (umode == U_EXPLICIT)
-        return dth ? go(k_admm3a<1, U_EXPLICIT, true, 7>) : go(k_admm3a<1, U_EXPLICIT, false, 7>);
-    return dth ? go(k_admm3a<1, U_FROM_Z, true, 7>) : go(k_admm3a<1, U_FROM_Z, false, 7>);
+            return dth ? go(k_admm3a<O, U_EXPLICIT, true, NB, T>) : go(k_admm3a<O, U_EXPLICIT, false, NB, T>);
+        return dth ? go(k_admm3a<O, U_FROM_Z, true, NB, T>) : go(k_admm3a<O, U_FROM_Z, false, NB, T>);
+    };
+    using std::integral_constant;
+    using T1 = integral_constant<bool, true>;
+    using T0 = integral_constant<bool, false>;
+    if (order == 0)
+        return twin ? pick(integral_constant<int, 0>{}, integral_constant<int, 7>{}, T1{})
+                    : pick(integral_constant<int, 0>{}, integral_constant<int, 7>{}, T0{});
+    if (g.nb == 6)
+        return twin ? pick(integral_constant<int, 1>{}, integral_constant<int, 6>{}, T1{})
+                    : pick(integral_constant<int, 1>{}, integral_constant<int, 6>{}, T0{});
+    return twin ? pick(integral_constant<int, 1>{}, integral_constant<int, 7>{}, T1{})
+                : pick(integral_constant<int, 1>{}, integral_constant<int, 7>{}, T0{});
+}
+
+// Fill block kdst of an edge state from block ksrc (the twin block after a run that skipped it)
+__global__ __launch_bounds__(256) void k_edges_copy_block(const Geom g, double* __restrict__ edges, int kdst, int ksrc) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < g.N; i += gridDim.x * 256u)
+        edges[eix(g, kdst, i)] = edges[eix(g, ksrc, i)];
+}
+
+hipError_t launch_edges_copy_block(const Geom& g, hipStream_t s, double* edges, int kdst, int ksrc) {
+    const uint32_t blocks = std::min<uint32_t>((g.N + 255u) / 256u, 4096u);
+    klaunch(k_edges_copy_block, dim3(std::max(blocks, 1u)), dim3(256), 0, s, g, edges, kdst, ksrc);
+    return hipGetLastError();
 }
 
 // =============================================================================================

@@ -44,7 +44,15 @@ int popcount(int x) { return __builtin_popcount(unsigned(x)); }
 // it and free the rest. Best effort: any failure (allocation, launch) leaves the allocation-order pair in
 // place, frees everything the probe allocated and clears HIP's error state. MVTV_ZPICK=0 turns it off
 // (MVTV_ZPICK=fail: allocate, then take the failure path; tests/test_gpu_zpick.py).
-mvtv_status pick_zpair(mvtv_problem* P, bool track_theta) {
+// The fused 3-D kernel may skip the twin block (mvtv_internal.h twin_block): one GPU, equal twin weights and state.
+// MVTV_TWIN=0 (probe builds) keeps both.
+bool twin_ready(const mvtv_problem* P) {
+    if (P->g.p != 3 || P->slab || !P->f3d || !P->twin_ok || probe_env("MVTV_TWIN_OFF")) return false;
+    const int kd = twin_block(P->g.nb, 3, P->order), kc = twin_canon(P->g.nb, 3, P->order);
+    return kd >= 0 && P->g.w[kd] == P->g.w[kc];
+}
+
+mvtv_status pick_zpair(mvtv_problem* P, bool track_theta, bool twin) {
     P->zpicked = true;
     const char* env = std::getenv("MVTV_ZPICK");
     if ((env && std::atoi(env) == 0) || P->g.p != 3 || P->g.N < (size_t(1) << 24) || !P->edges2) return MVTV_OK;
@@ -80,7 +88,7 @@ mvtv_status pick_zpair(mvtv_problem* P, bool track_theta) {
                 if (hip(hipEventRecord(ev[0], P->stream)) &&
                     hip(launch_admm3d(P->g, P->order, U_FROM_Z, P->stream, P->theta, cand[i], cand[j], 0.0, 1.0, 0.0,
                                       1.0, track_theta ? tmp[2] : nullptr, tmp[0], tmp[1], P->guprev, P->partials,
-                                      &np, nullptr)) &&
+                                      &np, nullptr, false, twin)) &&
                     hip(hipEventRecord(ev[1], P->stream)) && hip(hipEventSynchronize(ev[1])) &&
                     hip(hipEventElapsedTime(&ms, ev[0], ev[1])) && rep > 0)
                     cost[i][j] += ms;
@@ -935,9 +943,18 @@ mvtv_status mvtv_state_set(mvtv_problem* P, const double* theta, const double* u
     if (!P || !theta) return fail(MVTV_BAD_ARG, "null problem/theta");
     DeviceGuard dg(P->device);
     HIP_TRY(hipMemcpyAsync(P->theta, theta, size_t(P->g.N) * sizeof(double), hipMemcpyHostToDevice, P->stream));
+    P->twin_ok = true;
     if (u) {
         MVTV_TRY(import_edges(P, u, P->edges));
         P->u_default = false;
+        const int kd = twin_block(P->g.nb, P->g.p, P->order), kc = twin_canon(P->g.nb, P->g.p, P->order);
+        if (kd >= 0) {   // the twin blocks of the caller's u (reference block layout)
+            uint64_t off_d = 0, off_c = 0;
+            for (int k = 0; k < kd; ++k) off_d += P->blk_len[k];
+            for (int k = 0; k < kc; ++k) off_c += P->blk_len[k];
+            P->twin_ok = P->blk_len[kd] == P->blk_len[kc] &&
+                         std::memcmp(u + off_d, u + off_c, size_t(P->blk_len[kd]) * sizeof(double)) == 0;
+        }
     } else {
         P->u_default = true;
     }
@@ -1065,7 +1082,11 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
                                P->stream));
         std::swap(P->gu, P->guprev);
     }
-    if (fused && spectral && nbuf == 2 && !P->zpicked) MVTV_TRY(pick_zpair(P, track_theta));
+    // the twin block is skipped by the fused kernel and filled from its partner when the run ends
+    const bool twin = fused && twin_ready(P);
+    const int twin_d = twin_block(P->g.nb, P->g.p, P->order), twin_c = twin_canon(P->g.nb, P->g.p, P->order);
+    if (P->timing && fused) P->twin_timed = twin;
+    if (fused && spectral && nbuf == 2 && !P->zpicked) MVTV_TRY(pick_zpair(P, track_theta, twin));
     double dtheta = 0.0;
     if (track_theta) {
         if (!P->thold) MVTV_TRY(alloc(&P->thold, P->g.N));
@@ -1129,7 +1150,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
                 int npf = 0;
                 HIP_TRY(launch_admm3d(P->g, P->order, um, P->stream, P->theta, ebuf[j % nbuf], ebuf[(j + 1) % nbuf], 0.0, 1.0,
                                       0.0, 1.0, track_theta ? P->thold : nullptr, P->ga, gn, gp, P->partials, &npf,
-                                      P->ctl, fold));
+                                      P->ctl, fold, twin));
                 P->tstop(hh);
                 hh = P->tstart(MVTV_K_REDUCE);
                 HIP_TRY(launch_finalize(P->stream, P->partials, npf, ER_N + GR_N, -(1 << ER_DTH), 0, P->red, P->st, 0.0,
@@ -1253,6 +1274,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         } else if (pingpong && (it_done & 1)) {
             std::swap(P->edges, P->edges2);
         }
+        if (twin) HIP_TRY(launch_edges_copy_block(P->g, P->stream, P->edges, twin_d, twin_c));
         if (it_done > 0) P->edge_mode = U_FROM_Z;
         if (it_done > 0) P->t_z = c.t_z;
         P->c_state = c.c_prev;
@@ -1326,7 +1348,8 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         if (fused) {   // edge update + gather in one pass, z ping-pongs between the edge buffers
             h = P->tstart(MVTV_K_ADMM_FUSED);
             HIP_TRY(launch_admm3d(P->g, P->order, mode, P->stream, P->theta, P->edges, P->edges2, t_z, c_prev, t_new,
-                                  c_prev, track_theta ? P->thold : nullptr, P->ga, gnew, gprev, P->partials, &np));
+                                  c_prev, track_theta ? P->thold : nullptr, P->ga, gnew, gprev, P->partials, &np,
+                                  nullptr, false, twin));
             P->tstop(h);
             std::swap(P->edges, P->edges2);
             h = P->tstart(MVTV_K_REDUCE);
@@ -1442,6 +1465,10 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         }
     }
     P->harvest();   // the stream is idle here (last iteration synchronised)
+    if (twin) {
+        HIP_TRY(launch_edges_copy_block(P->g, P->stream, P->edges, twin_d, twin_c));
+        HIP_TRY(hipStreamSynchronize(P->stream));
+    }
     if (o.verbose) std::printf("Lambda= %g, Counter = %d\n", lambda, counter);
     // keep the resident state consistent: g_uprev buffer is P->guprev
     if (gprev != P->guprev) std::swap(P->guprev, P->gu);
@@ -1891,7 +1918,12 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
             b = 8.0 * N * (3.0 + (P->launches[kid] > 0 ? double(P->fold_fix) / double(P->launches[kid]) : 0.0));
             break;
         case MVTV_K_DCT: b = 8.0 * 2.0 * N; break;                       // x in, x out
-        case MVTV_K_ADMM_FUSED: b = 8.0 * (4.0 * N + 2.0 * E); break;    // theta, z, g_uprev in; z', g_alpha, g_u out
+        case MVTV_K_ADMM_FUSED: {   // theta, z, g_uprev in; z', g_alpha, g_u out (z without its twin block: twin_timed)
+            const int kd = twin_block(P->g.nb, P->g.p, P->order);
+            const double et = (P->twin_timed && kd >= 0) ? E - double(P->blk_len[kd]) * (P->slab ? 0.0 : 1.0) : E;
+            b = 8.0 * (4.0 * N + 2.0 * et);
+            break;
+        }
         case MVTV_K_ADMM_FUSED4: b = 8.0 * (5.0 * N + 2.0 * E); break;   // theta, z in; z', 4 pass-A sums out
         default: b = 0.0;
     }

@@ -70,6 +70,22 @@ __host__ __device__ constexpr int block_code(int k, int p, int order) {
     return order == 0 ? (k == 0 ? (1 << p) - 1 : k) : k + 1;
 }
 
+// Twin blocks: under the S' map two codes can share one difference set (3-D: {1,2} -> {0,2}, the same rows as
+// {0,2}); with equal weights and equal state their alpha, u and z are the same numbers. twin_block returns the later
+// block of the first such pair (-1: none) and twin_canon its earlier partner.
+__host__ __device__ constexpr int twin_block(int nb, int p, int order) {
+    for (int k = 0; k < nb; ++k)
+        for (int j = 0; j < k; ++j)
+            if (sprime_mask(block_code(k, p, order), p) == sprime_mask(block_code(j, p, order), p)) return k;
+    return -1;
+}
+__host__ __device__ constexpr int twin_canon(int nb, int p, int order) {
+    for (int k = 0; k < nb; ++k)
+        for (int j = 0; j < k; ++j)
+            if (sprime_mask(block_code(k, p, order), p) == sprime_mask(block_code(j, p, order), p)) return j;
+    return -1;
+}
+
 struct Geom {
     int32_t p;
     int32_t nb;            // number of row blocks of D
@@ -318,7 +334,9 @@ bool fused3d_ok(const Geom& g);
 hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
                          double* z_new, double t_old, double c_old, double t_new, double c_prev,
                          const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
-                         double* partials, int* nparts, const AdmmCtl* ctl = nullptr, bool fold = false);
+                         double* partials, int* nparts, const AdmmCtl* ctl = nullptr, bool fold = false,
+                         bool twin = false);
+hipError_t launch_edges_copy_block(const Geom& g, hipStream_t s, double* edges, int kdst, int ksrc);
 hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
                          double t_old, double c_old, double t_new, const double* theta_old, double* partials,
                          int* nparts, const AdmmCtl* ctl = nullptr);

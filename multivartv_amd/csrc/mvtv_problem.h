@@ -120,6 +120,9 @@ struct mvtv_problem {
     // resident ADMM state
     bool have_state = false;
     bool u_default = true;
+    // the twin blocks (mvtv_internal.h twin_block) hold equal u: true for the variant defaults, checked on import
+    bool twin_ok = true;
+    bool twin_timed = false;   // the timed fused launches skipped the twin block (its bytes are not counted)
     int edge_mode = U_EXPLICIT;
     double t_z = 0.0, c_state = 1.0, rho = 0.0;
 

@@ -107,3 +107,78 @@ def test_fused4d_kernel_is_the_one_timed():
         tm = P.timings()
     assert tm["admm_fused4"]["launches"] == 4 and tm["edge_update"]["launches"] == 0
     assert tm["gather4_b"]["launches"] == 4 and tm["gather_Dt"]["launches"] == 1   # D^T u0 only
+
+
+def _sprime(b, p):
+    S = [j for j in range(p) if (b >> (p - 1 - j)) & 1]
+    if len(S) <= 1 or 0 in S:
+        return tuple(S)
+    return tuple(sorted(set(S) - {min(S)} | {0}))
+
+
+def _blocks(m, order=0):
+    """(S' per block, block lengths) in the reference's block order (cpp-code/utils.cpp:258-267)."""
+    p = len(m)
+    codes = [(1 << p) - 1] + list(range(1, (1 << p) - 1)) if order == 0 else list(range(1, 1 << p))
+    sp = [_sprime(c, p) for c in codes]
+    return sp, [int(np.prod([v - 1 if j in s else v for j, v in enumerate(m)])) for s in sp]
+
+
+def _twin_blocks(m, order=0):
+    """Block indices (canonical, twin) of the pair the S' map gives one difference set (cpp order: {1,2} -> {0,2})."""
+    sp, _ = _blocks(m, order)
+    for k in range(len(sp)):
+        for j in range(k):
+            if sp[k] == sp[j]:
+                return j, k
+    return None
+
+
+@pytest.mark.parametrize("twin_equal", [True, False], ids=["twin_skipped", "twin_differs"])
+def test_twin_block_state_matches_oracle(twin_equal):
+    """Blocks {0,2} and {1,2} of the reference's D share S' = {0,2} and, at equal deltas, their weight: with equal u
+    they carry the same numbers, so k_admm3a streams one of them (and fills the other when the run ends). A caller's
+    u whose twin blocks differ keeps both. Both against the C oracle's variant-B loop: rho exactly, theta and u
+    (every block, the twin included) to 1e-9."""
+    m = [40, 40, 24]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    lam, iters = 1.0, 5
+    th0 = np.full(y.size, y.mean())
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        E = P.E
+        rng = np.random.default_rng(7)
+        u0 = 0.05 * rng.standard_normal(E)
+        _, blen = _blocks(m)
+        assert sum(blen) == E
+        off = np.concatenate([[0], np.cumsum(blen)])
+        kc, kd = _twin_blocks(m)
+        assert blen[kc] == blen[kd]
+        if twin_equal:
+            u0[off[kd]:off[kd + 1]] = u0[off[kc]:off[kc + 1]]
+        th, u, rho, st = P.admm(lam, th0, u=u0.copy(), rho=lam / 5, fixed_iters=iters, pcg_rtol=1e-13)
+    ref_th = th0.copy()
+    ref_u = u0.copy()
+    rs = c_oracle.admm_rcpp(m, y, lam, ref_th, ref_u, lam / 5, deltas, fixed_iters=iters, pcg_rtol=1e-13)
+    assert rho == rs["rho"]
+    assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
+    assert np.max(np.abs(u - ref_u)) <= 1e-9 * max(1.0, np.max(np.abs(ref_u)))
+    if twin_equal:
+        assert np.array_equal(u[off[kd]:off[kd + 1]], u[off[kc]:off[kc + 1]])
+
+
+def test_twin_block_bytes_counted_once():
+    """With the twin block skipped, the fused launch's algorithmic bytes are 8 (4N + 2 (E - E_twin))."""
+    m = [32, 32, 32]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        P.state_set(np.full(y.size, y.mean()), None, 0.2)
+        P.timing(True)
+        P.run(1.0, fixed_iters=3)
+        tm = P.timings()
+        N, E = P.N, P.E
+    et = _blocks(m)[1][_twin_blocks(m)[1]]   # the twin block: S' = {0, 2}, 31 x 32 x 31 rows
+    assert et == 31 * 32 * 31
+    assert tm["admm_fused"]["launches"] == 3
+    assert tm["admm_fused"]["bytes_per_launch"] == pytest.approx(8.0 * (4 * N + 2 * (E - et)), rel=1e-12)
