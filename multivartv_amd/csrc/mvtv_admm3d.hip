@@ -438,10 +438,8 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
                                             int Yh, int z0, int z1, double t_old, double c_old, double t_new,
                                             double c_prev, double rho_f) {
     constexpr int P = 3, NC = 8, IW = f3a::IW, IH = f3a::IH, NI = f3a_nimg<NB, ORD>();
-    constexpr int KD = TW ? twin_block(NB, P, ORD) : -1, KC = TW ? twin_canon(NB, P, ORD) : -1;
-    static_assert(!TW || (KD >= 0 && KC >= 0), "twin blocks");
+    static_assert(!TW || twin_block(NB, P, ORD) >= 0, "twin blocks");
     const Geom& g = a.g;
-    auto wgt = [&](int k) { return k == KC ? 2.0 * g.w[k] : g.w[k]; };   // exact doubling
     const int wv = int(threadIdx.x) >> 6, ln = int(threadIdx.x) & 63;
     const bool hcol = wv == IH;                 // the halo-column wave
     const int row = hcol ? ln : wv;
@@ -473,7 +471,7 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
             const bool need = cell && (!hrow || (S & 2)) && (!hcol || (S & 1));
-            if constexpr (k == KD) zo[k] = 0.0;
+            if constexpr (TW && twin_of(k, P, ORD) != k) zo[k] = 0.0;
             else zo[k] = need ? a.z_old[eix(g, k, i)] : 0.0;
         });
     };
@@ -496,7 +494,7 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
         static_for<0, NB>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-            if constexpr (k == KD) {
+            if constexpr (TW && twin_of(k, P, ORD) != k) {
                 zn[k] = 0.0;
             } else {
                 const double d = g.w[k] * v[S];
@@ -507,7 +505,7 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
                     const double al = z - clampd(z, t_new);
                     const double r = al - d;
                     __builtin_nontemporal_store(z, a.z_new + eix(g, k, i));
-                    constexpr double m = k == KC ? 2.0 : 1.0;   // the twin's rows: the same terms again
+                    constexpr double m = TW ? double(twin_count(k, NB, P, ORD)) : 1.0;   // the twins' rows: the same terms
                     red[0] = fma(m * r, r, red[0]);
                     red[1] = fma(m * d, d, red[1]);
                     red[2] = fma(m * al, al, red[2]);
@@ -520,7 +518,7 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
         static_for<0, NB>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             constexpr int sl = f3a_slot<NB, ORD>(k);
-            if constexpr (sl >= 0 && k != KD) szr[sidx(buf, sl, row, col)] = zn[k];
+            if constexpr (sl >= 0 && !(TW && twin_of(k, P, ORD) != k)) szr[sidx(buf, sl, row, col)] = zn[k];
         });
     };
     // in-plane backward sums Q_k of an owned cell: its own value from the register, the neighbours
@@ -563,11 +561,12 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
             static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                if constexpr ((S & 4) != 0 && k != KD) {
+                if constexpr ((S & 4) != 0 && !(TW && twin_of(k, P, ORD) != k)) {
+                    constexpr double mk = TW ? double(twin_count(k, NB, P, ORD)) : 1.0;   // exact for 2
                     double qa, qu;
                     plane_q(kc, 1, zn[k], qa, qu);
-                    qa_prev = fma(wgt(k), qa, qa_prev);
-                    qu_prev = fma(wgt(k), qu, qu_prev);
+                    qa_prev = fma(mk * g.w[k], qa, qa_prev);
+                    qu_prev = fma(mk * g.w[k], qu, qu_prev);
                 }
             });
         }
@@ -598,14 +597,16 @@ __device__ __forceinline__ void admm3a_tile(const Fused3dArgs& a, double* __rest
             static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                if constexpr (k != KD) {
+                if constexpr (!(TW && twin_of(k, P, ORD) != k)) {
+                    constexpr double mk = TW ? double(twin_count(k, NB, P, ORD)) : 1.0;
+                    const double wk = mk * g.w[k];
                     double qa, qu;
                     plane_q(kc, buf, zn[k], qa, qu);
-                    ga = fma(wgt(k), qa, ga);
-                    gu = fma(wgt(k), qu, gu);
+                    ga = fma(wk, qa, ga);
+                    gu = fma(wk, qu, gu);
                     if constexpr ((S & 4) != 0) {
-                        na = fma(wgt(k), qa, na);
-                        nu = fma(wgt(k), qu, nu);
+                        na = fma(wk, qa, na);
+                        nu = fma(wk, qu, nu);
                     }
                 }
             });
@@ -761,10 +762,8 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
                          const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
                          double* partials, int* nparts, const AdmmCtl* ctl, bool fold, bool twin) {
     if (fold && ((g.p != 2 && g.p != 3) || !ctl)) return hipErrorInvalidValue;   // the folded b: asynchronous loop
-    if (twin) {   // the twin pair must exist and carry one weight (the host also checks the state)
-        const int kd = twin_block(g.nb, g.p, order), kc = twin_canon(g.nb, g.p, order);
-        if (g.p != 3 || kd < 0 || g.w[kd] != g.w[kc]) return hipErrorInvalidValue;
-    }
+    if (twin && (g.p != 3 || !twin_weights_equal(g, order)))   // twins must carry one weight (the host checks the state)
+        return hipErrorInvalidValue;
     if (g.p == 2)
         return launch_admm2d(g, order, umode, s, theta, z_old, z_new, t_old, c_old, t_new, c_prev, theta_old, g_alpha,
                              g_u, g_uprev, partials, nparts, ctl, fold);
@@ -820,6 +819,18 @@ hipError_t launch_edges_copy_block(const Geom& g, hipStream_t s, double* edges, 
     const uint32_t blocks = std::min<uint32_t>((g.N + 255u) / 256u, 4096u);
     klaunch(k_edges_copy_block, dim3(std::max(blocks, 1u)), dim3(256), 0, s, g, edges, kdst, ksrc);
     return hipGetLastError();
+}
+
+// after a run that skipped the twins: fill every twin block of the state from its group's first block
+hipError_t fill_twins(const Geom& g, int order, hipStream_t s, double* edges) {
+    for (int k = 0; k < g.nb; ++k) {
+        const int c = twin_of(k, g.p, order);
+        if (c != k) {
+            const hipError_t e = launch_edges_copy_block(g, s, edges, k, c);
+            if (e != hipSuccess) return e;
+        }
+    }
+    return hipSuccess;
 }
 
 // =============================================================================================
@@ -1437,9 +1448,11 @@ struct Fused4Args {
     int tiles_x, tiles_y, zchunk, nzc, nblocks, wa;
 };
 
-template <int ORD, int UM, bool DTH, int NB>
+// TW: the twin blocks (mvtv_internal.h twin_of) are skipped as in k_admm3a, their group's first block counting for all
+template <int ORD, int UM, bool DTH, int NB, bool TW>
 __global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
     constexpr int P = 4, NC = 16, IW = f4a::IW, IH = f4a::IH, NI = f4a_nimg<NB, ORD>();
+    static_assert(!TW || twin_block(NB, P, ORD) >= 0, "twin blocks");
     double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new;
     if (a.ctl) {
         if (a.ctl->done) return;
@@ -1492,7 +1505,8 @@ __global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
                 const bool need = cell && (!hrow || (S & 2)) && (!hcol || (S & 1));
-                zo[k] = need ? a.z_old[eix(g, k, i)] : 0.0;
+                if constexpr (TW && twin_of(k, P, ORD) != k) zo[k] = 0.0;
+                else zo[k] = need ? a.z_old[eix(g, k, i)] : 0.0;
             });
         };
         auto edge_cell = [&](int e, const double (&th0)[8], const double (&th1)[8], const double (&zo)[NB],
@@ -1515,17 +1529,22 @@ __global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
             static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                const double d = g.w[k] * v[S];
-                const double uo = (UM == U_EXPLICIT) ? zo[k] : -c_old * clampd(zo[k], t_old);
-                const double z = cell ? d - uo : 0.0;
-                zn[k] = z;
-                if (own) {
-                    const double al = z - clampd(z, t_new);
-                    const double r = al - d;
-                    __builtin_nontemporal_store(z, a.z_new + eix(g, k, i));
-                    red[ER_R2] = fma(r, r, red[ER_R2]);
-                    red[ER_D2] = fma(d, d, red[ER_D2]);
-                    red[ER_A2] = fma(al, al, red[ER_A2]);
+                if constexpr (TW && twin_of(k, P, ORD) != k) {
+                    zn[k] = 0.0;
+                } else {
+                    const double d = g.w[k] * v[S];
+                    const double uo = (UM == U_EXPLICIT) ? zo[k] : -c_old * clampd(zo[k], t_old);
+                    const double z = cell ? d - uo : 0.0;
+                    zn[k] = z;
+                    if (own) {
+                        const double al = z - clampd(z, t_new);
+                        const double r = al - d;
+                        __builtin_nontemporal_store(z, a.z_new + eix(g, k, i));
+                        constexpr double m = TW ? double(twin_count(k, NB, P, ORD)) : 1.0;   // the twins' terms
+                        red[ER_R2] = fma(m * r, r, red[ER_R2]);
+                        red[ER_D2] = fma(m * d, d, red[ER_D2]);
+                        red[ER_A2] = fma(m * al, al, red[ER_A2]);
+                    }
                 }
             });
         };
@@ -1534,7 +1553,7 @@ __global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
             static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int sl = f4a_slot<NB, ORD>(k);
-                if constexpr (sl >= 0) szr[sidx(buf, sl, row, col)] = zn[k];
+                if constexpr (sl >= 0 && !(TW && twin_of(k, P, ORD) != k)) szr[sidx(buf, sl, row, col)] = zn[k];
             });
         };
         auto plane_q = [&](auto kc, int buf, double own_z, double& qa, double& qu) {
@@ -1568,15 +1587,17 @@ __global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
             static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                if constexpr ((S & 4) != 0) {
+                if constexpr ((S & 4) != 0 && !(TW && twin_of(k, P, ORD) != k)) {
+                    constexpr double mk = TW ? double(twin_count(k, NB, P, ORD)) : 1.0;
+                    const double wk = mk * g.w[k];
                     double qa, qu;
                     plane_q(kc, buf, zn[k], qa, qu);
                     if constexpr ((S & 8) != 0) {
-                        naw = fma(g.w[k], qa, naw);
-                        nuw = fma(g.w[k], qu, nuw);
+                        naw = fma(wk, qa, naw);
+                        nuw = fma(wk, qu, nuw);
                     } else {
-                        na0 = fma(g.w[k], qa, na0);
-                        nu0 = fma(g.w[k], qu, nu0);
+                        na0 = fma(wk, qa, na0);
+                        nu0 = fma(wk, qu, nu0);
                     }
                 }
             });
@@ -1615,21 +1636,25 @@ __global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
                 static_for<0, NB>([&](auto kc) {
                     constexpr int k = decltype(kc)::value;
                     constexpr int S = sprime_mask(block_code(k, P, ORD), P);
-                    double qa, qu;
-                    plane_q(kc, buf, zn[k], qa, qu);
-                    if constexpr ((S & 8) != 0) {
-                        saw = fma(g.w[k], qa, saw);
-                        suw = fma(g.w[k], qu, suw);
-                        if constexpr ((S & 4) != 0) {
-                            naw = fma(g.w[k], qa, naw);
-                            nuw = fma(g.w[k], qu, nuw);
-                        }
-                    } else {
-                        sa0 = fma(g.w[k], qa, sa0);
-                        su0 = fma(g.w[k], qu, su0);
-                        if constexpr ((S & 4) != 0) {
-                            na0 = fma(g.w[k], qa, na0);
-                            nu0 = fma(g.w[k], qu, nu0);
+                    if constexpr (!(TW && twin_of(k, P, ORD) != k)) {
+                        constexpr double mk = TW ? double(twin_count(k, NB, P, ORD)) : 1.0;
+                        const double wk = mk * g.w[k];
+                        double qa, qu;
+                        plane_q(kc, buf, zn[k], qa, qu);
+                        if constexpr ((S & 8) != 0) {
+                            saw = fma(wk, qa, saw);
+                            suw = fma(wk, qu, suw);
+                            if constexpr ((S & 4) != 0) {
+                                naw = fma(wk, qa, naw);
+                                nuw = fma(wk, qu, nuw);
+                            }
+                        } else {
+                            sa0 = fma(wk, qa, sa0);
+                            su0 = fma(wk, qu, su0);
+                            if constexpr ((S & 4) != 0) {
+                                na0 = fma(wk, qa, na0);
+                                nu0 = fma(wk, qu, nu0);
+                            }
                         }
                     }
                 });
@@ -1935,8 +1960,9 @@ bool fused4_ok(const Geom& g) {
 
 hipError_t launch_admm4a(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
                          double* z_new, double t_old, double c_old, double t_new, const double* theta_old,
-                         double* scratch4, double* partials, int* nparts, const AdmmCtl* ctl) {
+                         double* scratch4, double* partials, int* nparts, const AdmmCtl* ctl, bool twin) {
     if (!fused4_ok(g) || !scratch4 || z_old == z_new) return hipErrorInvalidValue;
+    if (twin && !twin_weights_equal(g, order)) return hipErrorInvalidValue;
     Fused4Args a = f4a_args(g);
     a.t_old = t_old;
     a.c_old = c_old;
@@ -1958,16 +1984,24 @@ hipError_t launch_admm4a(const Geom& g, int order, int umode, hipStream_t s, con
         klaunch(kern, dim3(grid), dim3(f4a::NT), 0, s, a);
         return hipGetLastError();
     };
-    if (order == 0) {
-        if (umode == U_EXPLICIT) return dth ? go(k_admm4a<0, U_EXPLICIT, true, 15>) : go(k_admm4a<0, U_EXPLICIT, false, 15>);
-        return dth ? go(k_admm4a<0, U_FROM_Z, true, 15>) : go(k_admm4a<0, U_FROM_Z, false, 15>);
-    }
-    if (g.nb == 14) {
-        if (umode == U_EXPLICIT) return dth ? go(k_admm4a<1, U_EXPLICIT, true, 14>) : go(k_admm4a<1, U_EXPLICIT, false, 14>);
-        return dth ? go(k_admm4a<1, U_FROM_Z, true, 14>) : go(k_admm4a<1, U_FROM_Z, false, 14>);
-    }
-    if (umode == U_EXPLICIT) return dth ? go(k_admm4a<1, U_EXPLICIT, true, 15>) : go(k_admm4a<1, U_EXPLICIT, false, 15>);
-    return dth ? go(k_admm4a<1, U_FROM_Z, true, 15>) : go(k_admm4a<1, U_FROM_Z, false, 15>);
+    auto pick = [&](auto ordc, auto nbc, auto twc) {
+        constexpr int O = decltype(ordc)::value, NB = decltype(nbc)::value;
+        constexpr bool T = decltype(twc)::value;
+        if (umode == U_EXPLICIT)
+            return dth ? go(k_admm4a<O, U_EXPLICIT, true, NB, T>) : go(k_admm4a<O, U_EXPLICIT, false, NB, T>);
+        return dth ? go(k_admm4a<O, U_FROM_Z, true, NB, T>) : go(k_admm4a<O, U_FROM_Z, false, NB, T>);
+    };
+    using std::integral_constant;
+    using T1 = integral_constant<bool, true>;
+    using T0 = integral_constant<bool, false>;
+    if (order == 0)
+        return twin ? pick(integral_constant<int, 0>{}, integral_constant<int, 15>{}, T1{})
+                    : pick(integral_constant<int, 0>{}, integral_constant<int, 15>{}, T0{});
+    if (g.nb == 14)
+        return twin ? pick(integral_constant<int, 1>{}, integral_constant<int, 14>{}, T1{})
+                    : pick(integral_constant<int, 1>{}, integral_constant<int, 14>{}, T0{});
+    return twin ? pick(integral_constant<int, 1>{}, integral_constant<int, 15>{}, T1{})
+                : pick(integral_constant<int, 1>{}, integral_constant<int, 15>{}, T0{});
 }
 
 hipError_t launch_gather4b(const Geom& g, int umode, hipStream_t s, double* g_alpha, double* g_u, const double* g_uprev,

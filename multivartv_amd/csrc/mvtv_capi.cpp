@@ -47,9 +47,17 @@ int popcount(int x) { return __builtin_popcount(unsigned(x)); }
 // The fused 3-D kernel may skip the twin block (mvtv_internal.h twin_block): one GPU, equal twin weights and state.
 // MVTV_TWIN=0 (probe builds) keeps both.
 bool twin_ready(const mvtv_problem* P) {
-    if (P->g.p != 3 || P->slab || !P->f3d || !P->twin_ok || probe_env("MVTV_TWIN_OFF")) return false;
-    const int kd = twin_block(P->g.nb, 3, P->order), kc = twin_canon(P->g.nb, 3, P->order);
-    return kd >= 0 && P->g.w[kd] == P->g.w[kc];
+    if (P->slab || !P->twin_ok || probe_env("MVTV_TWIN_OFF")) return false;
+    if (!((P->g.p == 3 && P->f3d) || (P->g.p == 4 && P->f4d))) return false;
+    return twin_weights_equal(P->g, P->order);
+}
+
+// edge words the twins leave out (the twin blocks' lengths)
+double twin_edges(const mvtv_problem* P) {
+    double t = 0.0;
+    for (int k = 0; k < P->g.nb; ++k)
+        if (twin_of(k, P->g.p, P->order) != k) t += double(P->blk_len[k]);
+    return t;
 }
 
 mvtv_status pick_zpair(mvtv_problem* P, bool track_theta, bool twin) {
@@ -947,13 +955,13 @@ mvtv_status mvtv_state_set(mvtv_problem* P, const double* theta, const double* u
     if (u) {
         MVTV_TRY(import_edges(P, u, P->edges));
         P->u_default = false;
-        const int kd = twin_block(P->g.nb, P->g.p, P->order), kc = twin_canon(P->g.nb, P->g.p, P->order);
-        if (kd >= 0) {   // the twin blocks of the caller's u (reference block layout)
-            uint64_t off_d = 0, off_c = 0;
-            for (int k = 0; k < kd; ++k) off_d += P->blk_len[k];
-            for (int k = 0; k < kc; ++k) off_c += P->blk_len[k];
-            P->twin_ok = P->blk_len[kd] == P->blk_len[kc] &&
-                         std::memcmp(u + off_d, u + off_c, size_t(P->blk_len[kd]) * sizeof(double)) == 0;
+        uint64_t off[kMaxBlocks + 1] = {0};   // the twin blocks of the caller's u (reference block layout)
+        for (int k = 0; k < P->g.nb; ++k) off[k + 1] = off[k] + P->blk_len[k];
+        for (int k = 0; k < P->g.nb && P->twin_ok; ++k) {
+            const int c = twin_of(k, P->g.p, P->order);
+            if (c != k)
+                P->twin_ok = P->blk_len[k] == P->blk_len[c] &&
+                             std::memcmp(u + off[k], u + off[c], size_t(P->blk_len[k]) * sizeof(double)) == 0;
         }
     } else {
         P->u_default = true;
@@ -1082,10 +1090,9 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
                                P->stream));
         std::swap(P->gu, P->guprev);
     }
-    // the twin block is skipped by the fused kernel and filled from its partner when the run ends
-    const bool twin = fused && twin_ready(P);
-    const int twin_d = twin_block(P->g.nb, P->g.p, P->order), twin_c = twin_canon(P->g.nb, P->g.p, P->order);
-    if (P->timing && fused) P->twin_timed = twin;
+    // the twin blocks are skipped by the fused kernels and filled from their group's first block when the run ends
+    const bool twin = (fused || fused4) && twin_ready(P);
+    if (P->timing && (fused || fused4)) P->twin_timed = twin;
     if (fused && spectral && nbuf == 2 && !P->zpicked) MVTV_TRY(pick_zpair(P, track_theta, twin));
     double dtheta = 0.0;
     if (track_theta) {
@@ -1162,7 +1169,8 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
                 int hh = P->tstart(MVTV_K_ADMM_FUSED4);
                 int npe = 0;
                 HIP_TRY(launch_admm4a(P->g, P->order, um, P->stream, P->theta, ebuf[j % nbuf], ebuf[(j + 1) % nbuf], 0.0,
-                                      1.0, 0.0, track_theta ? P->thold : nullptr, P->g4, P->partials, &npe, P->ctl));
+                                      1.0, 0.0, track_theta ? P->thold : nullptr, P->g4, P->partials, &npe, P->ctl,
+                                      twin));
                 P->tstop(hh);
                 hh = P->tstart(MVTV_K_REDUCE);
                 HIP_TRY(launch_finalize(P->stream, P->partials, npe, ER_N, 1, 0, P->red, P->st, 0.0, 0, P->ctl));
@@ -1274,7 +1282,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         } else if (pingpong && (it_done & 1)) {
             std::swap(P->edges, P->edges2);
         }
-        if (twin) HIP_TRY(launch_edges_copy_block(P->g, P->stream, P->edges, twin_d, twin_c));
+        if (twin) HIP_TRY(fill_twins(P->g, P->order, P->stream, P->edges));
         if (it_done > 0) P->edge_mode = U_FROM_Z;
         if (it_done > 0) P->t_z = c.t_z;
         P->c_state = c.c_prev;
@@ -1360,7 +1368,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         } else if (fused4) {   // 4-D: edge update + gather pass A in one pass (z ping-pong), then pass B
             h = P->tstart(MVTV_K_ADMM_FUSED4);
             HIP_TRY(launch_admm4a(P->g, P->order, mode, P->stream, P->theta, P->edges, P->edges2, t_z, c_prev, t_new,
-                                  track_theta ? P->thold : nullptr, P->g4, P->partials, &np));
+                                  track_theta ? P->thold : nullptr, P->g4, P->partials, &np, nullptr, twin));
             P->tstop(h);
             std::swap(P->edges, P->edges2);
             h = P->tstart(MVTV_K_REDUCE);
@@ -1466,7 +1474,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     }
     P->harvest();   // the stream is idle here (last iteration synchronised)
     if (twin) {
-        HIP_TRY(launch_edges_copy_block(P->g, P->stream, P->edges, twin_d, twin_c));
+        HIP_TRY(fill_twins(P->g, P->order, P->stream, P->edges));
         HIP_TRY(hipStreamSynchronize(P->stream));
     }
     if (o.verbose) std::printf("Lambda= %g, Counter = %d\n", lambda, counter);
@@ -1891,8 +1899,9 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
     MVTV_TRY(P->sync());
     double N = double(P->g.N), E = double(P->E);
     const double w = P->wmode == W_DIAG ? 1.0 : 0.0;
+    double own = 1.0;
     if (P->slab) {   // a slab rank's kernels work on its owned planes (ghost planes are read only as halos)
-        const double own = double(P->ze - P->zb) / double(P->g.m[P->g.p - 1]);
+        own = double(P->ze - P->zb) / double(P->g.m[P->g.p - 1]);
         N *= own;
         E *= own;
     }
@@ -1918,13 +1927,12 @@ mvtv_status mvtv_timing_get(mvtv_problem* P, int32_t kid, double* total_ms, int6
             b = 8.0 * N * (3.0 + (P->launches[kid] > 0 ? double(P->fold_fix) / double(P->launches[kid]) : 0.0));
             break;
         case MVTV_K_DCT: b = 8.0 * 2.0 * N; break;                       // x in, x out
-        case MVTV_K_ADMM_FUSED: {   // theta, z, g_uprev in; z', g_alpha, g_u out (z without its twin block: twin_timed)
-            const int kd = twin_block(P->g.nb, P->g.p, P->order);
-            const double et = (P->twin_timed && kd >= 0) ? E - double(P->blk_len[kd]) * (P->slab ? 0.0 : 1.0) : E;
-            b = 8.0 * (4.0 * N + 2.0 * et);
+        case MVTV_K_ADMM_FUSED:   // theta, z, g_uprev in; z', g_alpha, g_u out (z without its twin blocks: twin_timed)
+            b = 8.0 * (4.0 * N + 2.0 * (P->twin_timed ? E - twin_edges(P) * own : E));
             break;
-        }
-        case MVTV_K_ADMM_FUSED4: b = 8.0 * (5.0 * N + 2.0 * E); break;   // theta, z in; z', 4 pass-A sums out
+        case MVTV_K_ADMM_FUSED4:   // theta, z in; z', 4 pass-A sums out (z without its twin blocks: twin_timed)
+            b = 8.0 * (5.0 * N + 2.0 * (P->twin_timed ? E - twin_edges(P) * own : E));
+            break;
         default: b = 0.0;
     }
     if (total_ms) *total_ms = P->ms[kid];

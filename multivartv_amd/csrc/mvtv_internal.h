@@ -70,22 +70,30 @@ __host__ __device__ constexpr int block_code(int k, int p, int order) {
     return order == 0 ? (k == 0 ? (1 << p) - 1 : k) : k + 1;
 }
 
-// Twin blocks: under the S' map two codes can share one difference set (3-D: {1,2} -> {0,2}, the same rows as
-// {0,2}); with equal weights and equal state their alpha, u and z are the same numbers. twin_block returns the later
-// block of the first such pair (-1: none) and twin_canon its earlier partner.
+// Twin blocks: under the S' map several codes can share one difference set (3-D: {1,2} -> {0,2}, the rows of {0,2};
+// 4-D: {1,2} -> {0,2}, {1,3}, {2,3} -> {0,3}, {1,2,3} -> {0,2,3}); with equal weights and equal state their alpha, u
+// and z are the same numbers. twin_of(k) is the first block of k's group (k itself for the first), twin_count(k) the
+// size of k's group; twin_block / twin_canon name the first pair (-1: none).
+__host__ __device__ constexpr int twin_of(int k, int p, int order) {
+    for (int j = 0; j < k; ++j)
+        if (sprime_mask(block_code(k, p, order), p) == sprime_mask(block_code(j, p, order), p)) return j;
+    return k;
+}
+__host__ __device__ constexpr int twin_count(int k, int nb, int p, int order) {
+    int n = 0;
+    for (int j = 0; j < nb; ++j)
+        if (sprime_mask(block_code(k, p, order), p) == sprime_mask(block_code(j, p, order), p)) ++n;
+    return n;
+}
 __host__ __device__ constexpr int twin_block(int nb, int p, int order) {
     for (int k = 0; k < nb; ++k)
-        for (int j = 0; j < k; ++j)
-            if (sprime_mask(block_code(k, p, order), p) == sprime_mask(block_code(j, p, order), p)) return k;
+        if (twin_of(k, p, order) != k) return k;
     return -1;
 }
 __host__ __device__ constexpr int twin_canon(int nb, int p, int order) {
-    for (int k = 0; k < nb; ++k)
-        for (int j = 0; j < k; ++j)
-            if (sprime_mask(block_code(k, p, order), p) == sprime_mask(block_code(j, p, order), p)) return j;
-    return -1;
+    const int k = twin_block(nb, p, order);
+    return k < 0 ? -1 : twin_of(k, p, order);
 }
-
 struct Geom {
     int32_t p;
     int32_t nb;            // number of row blocks of D
@@ -105,6 +113,13 @@ struct Geom {
 __host__ __device__ __forceinline__ uint64_t eix(const Geom& g, int k, uint32_t i) {
     return g.eaos ? (((uint64_t(i >> 6) * uint32_t(g.nb) + uint32_t(k)) << 6) | uint64_t(i & 63u))
                   : uint64_t(k) * g.N + i;
+}
+
+// every twin carries its group's first block's weight (bitwise): the twins may then share one state
+inline bool twin_weights_equal(const Geom& g, int order) {
+    for (int k = 0; k < g.nb; ++k)
+        if (g.w[twin_of(k, g.p, order)] != g.w[k]) return false;
+    return twin_block(g.nb, g.p, order) >= 0;
 }
 
 // Per-node multi-index decode (column-major, dim 0 fastest).
@@ -337,6 +352,7 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
                          double* partials, int* nparts, const AdmmCtl* ctl = nullptr, bool fold = false,
                          bool twin = false);
 hipError_t launch_edges_copy_block(const Geom& g, hipStream_t s, double* edges, int kdst, int ksrc);
+hipError_t fill_twins(const Geom& g, int order, hipStream_t s, double* edges);
 hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
                          double t_old, double c_old, double t_new, const double* theta_old, double* partials,
                          int* nparts, const AdmmCtl* ctl = nullptr);
@@ -350,7 +366,7 @@ bool gather4_ok(const Geom& g);
 bool fused4_ok(const Geom& g);
 hipError_t launch_admm4a(const Geom& g, int order, int umode, hipStream_t s, const double* theta, const double* z_old,
                          double* z_new, double t_old, double c_old, double t_new, const double* theta_old,
-                         double* scratch4, double* partials, int* nparts, const AdmmCtl* ctl = nullptr);
+                         double* scratch4, double* partials, int* nparts, const AdmmCtl* ctl = nullptr, bool twin = false);
 hipError_t launch_gather4b(const Geom& g, int umode, hipStream_t s, double* g_alpha, double* g_u, const double* g_uprev,
                            double c_prev, double* partials, int* nparts, const AdmmCtl* ctl, double* scratch4,
                            bool fold = false);

@@ -495,6 +495,11 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     const bool fused = P->f3d;
     const bool fused4 = P->f4d;   // 4-D: edge update + the gather's pass A fused on the owned planes (k_admm4a)
     const bool pingpong = fused || fused4;
+    // twin blocks (mvtv_internal.h twin_block): the run starts from u0 = 0, so the twins are equal whenever their
+    // weights are (the same global deltas on every rank, hence the same choice); filled when the run ends
+    // (3-D only: the 4-D ranks' ghost-plane pass A reads every block of the z halo)
+    const bool twin = fused && p == 3 && twin_weights_equal(P->g, P->order) && !probe_env("MVTV_TWIN_OFF");
+    if (P->timing && (fused || fused4)) P->twin_timed = twin;
     // folded right-hand side (as mvtv_capi.cpp's loop): the fused kernel stores s = rho (D^T alpha + D^T u) and the
     // next first pass reads oty + s (oty + (rho'/rho) s + rho' (c - 1) D^T u after a rho change)
     const uint32_t m0 = P->g.m[0];
@@ -842,7 +847,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
             int h = P->tstart(MVTV_K_ADMM_FUSED);
             int npf = 0;
             HIP_TRY(launch_admm3d(P->g, P->order, um, s, P->theta, zo, zn, 0.0, 1.0, 0.0, 1.0, nullptr, P->ga, gn, gp,
-                                  P->partials, &npf, P->ctl, fold));
+                                  P->partials, &npf, P->ctl, fold, twin));
             P->tstop(h);
             HIP_TRY(launch_finalize(s, P->partials, npf, ER_N + GR_N, -(1 << ER_DTH), 0, P->red, P->st, 0.0, 0, P->ctl));
         } else if (fused4) {
@@ -952,6 +957,11 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         std::swap(P->guprev, P->gu);
         if (pingpong) std::swap(P->edges, P->edges2);
     }
+    if (twin) {
+        HIP_TRY(fill_twins(P->g, P->order, s, P->edges));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    P->twin_ok = true;
     P->edge_mode = it_done > 0 ? U_FROM_Z : U_EXPLICIT;
     P->t_z = c.t_z;
     P->c_state = c.c_prev;

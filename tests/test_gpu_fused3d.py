@@ -96,7 +96,8 @@ def test_fused4d_matches_oracle(m, iters, order, weighted, solver):
 
 
 def test_fused4d_kernel_is_the_one_timed():
-    """At 4-D the loop's edge work runs in k_admm4a (timing id admm_fused4), not k_edge4d / k_gather4a."""
+    """At 4-D the loop's edge work runs in k_admm4a (timing id admm_fused4), not k_edge4d / k_gather4a; its twin
+    blocks ({1,2} of S' {0,2}; {1,3}, {2,3} of {0,3}; {1,2,3} of {0,2,3}) are streamed once: 8 (5N + 2 (E - E_twins))."""
     m = [32, 32, 32, 8]
     y = towers(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
@@ -105,8 +106,13 @@ def test_fused4d_kernel_is_the_one_timed():
         P.timing(True)
         P.run(1.0, fixed_iters=4)
         tm = P.timings()
+        N, E = P.N, P.E
     assert tm["admm_fused4"]["launches"] == 4 and tm["edge_update"]["launches"] == 0
     assert tm["gather4_b"]["launches"] == 4 and tm["gather_Dt"]["launches"] == 1   # D^T u0 only
+    sp, blen = _blocks(m)
+    et = sum(blen[k] for k in range(len(sp)) if sp[k] in sp[:k])
+    assert sum(1 for k in range(len(sp)) if sp[k] in sp[:k]) == 4
+    assert tm["admm_fused4"]["bytes_per_launch"] == pytest.approx(8.0 * (5 * N + 2 * (E - et)), rel=1e-12)
 
 
 def _sprime(b, p):
@@ -134,13 +140,13 @@ def _twin_blocks(m, order=0):
     return None
 
 
+@pytest.mark.parametrize("m", [[40, 40, 24], [12, 12, 12, 6]], ids=["3d", "4d"])
 @pytest.mark.parametrize("twin_equal", [True, False], ids=["twin_skipped", "twin_differs"])
-def test_twin_block_state_matches_oracle(twin_equal):
-    """Blocks {0,2} and {1,2} of the reference's D share S' = {0,2} and, at equal deltas, their weight: with equal u
-    they carry the same numbers, so k_admm3a streams one of them (and fills the other when the run ends). A caller's
-    u whose twin blocks differ keeps both. Both against the C oracle's variant-B loop: rho exactly, theta and u
-    (every block, the twin included) to 1e-9."""
-    m = [40, 40, 24]
+def test_twin_block_state_matches_oracle(twin_equal, m):
+    """Blocks {0,2} and {1,2} of the reference's D share S' = {0,2} (4-D: three such groups) and, at equal deltas,
+    their weight: with equal u they carry the same numbers, so k_admm3a / k_admm4a stream one block per group (and
+    fill the others when the run ends). A caller's u whose twin blocks differ keeps them all. Both against the C
+    oracle's variant-B loop: rho exactly, theta and u (every block, the twins included) to 1e-9."""
     y = towers(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     lam, iters = 1.0, 5
@@ -152,10 +158,12 @@ def test_twin_block_state_matches_oracle(twin_equal):
         _, blen = _blocks(m)
         assert sum(blen) == E
         off = np.concatenate([[0], np.cumsum(blen)])
-        kc, kd = _twin_blocks(m)
-        assert blen[kc] == blen[kd]
-        if twin_equal:
-            u0[off[kd]:off[kd + 1]] = u0[off[kc]:off[kc + 1]]
+        sp = _blocks(m)[0]
+        twins = [(sp.index(sp[k]), k) for k in range(len(sp)) if sp[k] in sp[:k]]   # (first of the group, twin)
+        assert twins and all(blen[c] == blen[k] for c, k in twins)
+        for c, k in twins:
+            if twin_equal:
+                u0[off[k]:off[k + 1]] = u0[off[c]:off[c + 1]]
         th, u, rho, st = P.admm(lam, th0, u=u0.copy(), rho=lam / 5, fixed_iters=iters, pcg_rtol=1e-13)
     ref_th = th0.copy()
     ref_u = u0.copy()
@@ -164,7 +172,8 @@ def test_twin_block_state_matches_oracle(twin_equal):
     assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
     assert np.max(np.abs(u - ref_u)) <= 1e-9 * max(1.0, np.max(np.abs(ref_u)))
     if twin_equal:
-        assert np.array_equal(u[off[kd]:off[kd + 1]], u[off[kc]:off[kc + 1]])
+        for c, k in twins:
+            assert np.array_equal(u[off[k]:off[k + 1]], u[off[c]:off[c + 1]])
 
 
 def test_twin_block_bytes_counted_once():
