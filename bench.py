@@ -189,6 +189,22 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+def _edge_blocks_note(tim, dims, N, E):
+    """Which blocks of D the fused edge pass streamed: every one, or one per twin group (blocks the S' map gives one
+    difference set, with equal weights and state: the same numbers; DESIGN.md §4.2 'Twin blocks')."""
+    k = {3: "admm_fused", 4: "admm_fused4"}.get(dims)
+    t = tim.get(k) if k else None
+    if not t or not t["launches"]:
+        return None
+    full = 8.0 * ((4.0 if dims == 3 else 5.0) * N + 2.0 * E)
+    if t["bytes_per_launch"] >= full * (1 - 1e-12):
+        return "all blocks streamed"
+    groups = {3: "6 of 7 ({1,2} shares S'={0,2} with {0,2})",
+              4: "one per S' group (groups {0,2}, {0,3}, {0,2,3} hold 2, 3 and 2 blocks)"}[dims]
+    return (f"twin blocks streamed once: {groups}; the twins' state is filled from their partner when the run "
+            f"ends (inside the timed region); bytes_per_launch counts the streamed blocks only")
+
+
 def load_pmc(name):
     """Per-launch HBM bytes of kernel `name` from the last committed rocprofv3 PMC pass of this code
     (profiles/pmc_traffic.json, written by tools/pmc_summary.py): (bytes, source label) or (None, None)."""
@@ -588,6 +604,7 @@ def independent_main(a, D, comm=None):
                                f"lambda={lam}, fixed-iteration mode",
                    "theta_solver": used,
                    "mesh": m, "nodes": N, "edges": E, "pcg_rtol": a.pcg_rtol, "pcg_iters_mean": round(kbar_all, 2),
+                   "edge_blocks": _edge_blocks_note(tim, a.dims, N, E),
                    "parallelism": (f"independent mesh fits, one per GPU (gloo barrier / max-time, residual "
                                    f"all-reduce over {red_via})") if D.world > 1 else "single GPU"},
         "roofline": roof,
