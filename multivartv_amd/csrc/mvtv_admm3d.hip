@@ -809,24 +809,30 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
                 : pick(integral_constant<int, 1>{}, integral_constant<int, 7>{}, T0{});
 }
 
-// Fill block kdst of an edge state from block ksrc (the twin block after a run that skipped it)
-__global__ __launch_bounds__(256) void k_edges_copy_block(const Geom g, double* __restrict__ edges, int kdst, int ksrc) {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < g.N; i += gridDim.x * 256u)
+// Fill block kdst of an edge state from block ksrc at nodes [i0, i1) (the twin block after a run that skipped it)
+__global__ __launch_bounds__(256) void k_edges_copy_block(const Geom g, double* __restrict__ edges, int kdst, int ksrc,
+                                                          uint32_t i0, uint32_t i1) {
+    for (uint32_t i = i0 + blockIdx.x * 256u + threadIdx.x; i < i1; i += gridDim.x * 256u)
         edges[eix(g, kdst, i)] = edges[eix(g, ksrc, i)];
 }
 
-hipError_t launch_edges_copy_block(const Geom& g, hipStream_t s, double* edges, int kdst, int ksrc) {
-    const uint32_t blocks = std::min<uint32_t>((g.N + 255u) / 256u, 4096u);
-    klaunch(k_edges_copy_block, dim3(std::max(blocks, 1u)), dim3(256), 0, s, g, edges, kdst, ksrc);
+hipError_t launch_edges_copy_block(const Geom& g, hipStream_t s, double* edges, int kdst, int ksrc, uint32_t i0,
+                                   uint32_t i1) {
+    i1 = std::min(i1, g.N);
+    if (i0 >= i1) return hipSuccess;
+    const uint32_t blocks = std::min<uint32_t>((i1 - i0 + 255u) / 256u, 4096u);
+    klaunch(k_edges_copy_block, dim3(std::max(blocks, 1u)), dim3(256), 0, s, g, edges, kdst, ksrc, i0, i1);
     return hipGetLastError();
 }
 
-// after a run that skipped the twins: fill every twin block of the state from its group's first block
-hipError_t fill_twins(const Geom& g, int order, hipStream_t s, double* edges) {
+// fill every twin block of the state from its group's first block at nodes [i0, i1): after a run that skipped the
+// twins (the whole state), or before a 4-D slab rank hands its last plane to the next rank (whose ghost-plane pass A
+// reads every block)
+hipError_t fill_twins(const Geom& g, int order, hipStream_t s, double* edges, uint32_t i0, uint32_t i1) {
     for (int k = 0; k < g.nb; ++k) {
         const int c = twin_of(k, g.p, order);
         if (c != k) {
-            const hipError_t e = launch_edges_copy_block(g, s, edges, k, c);
+            const hipError_t e = launch_edges_copy_block(g, s, edges, k, c, i0, i1);
             if (e != hipSuccess) return e;
         }
     }

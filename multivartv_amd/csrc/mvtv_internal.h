@@ -351,8 +351,9 @@ hipError_t launch_admm3d(const Geom& g, int order, int umode, hipStream_t s, con
                          const double* theta_old, double* g_alpha, double* g_u, const double* g_uprev,
                          double* partials, int* nparts, const AdmmCtl* ctl = nullptr, bool fold = false,
                          bool twin = false);
-hipError_t launch_edges_copy_block(const Geom& g, hipStream_t s, double* edges, int kdst, int ksrc);
-hipError_t fill_twins(const Geom& g, int order, hipStream_t s, double* edges);
+hipError_t launch_edges_copy_block(const Geom& g, hipStream_t s, double* edges, int kdst, int ksrc, uint32_t i0 = 0,
+                                   uint32_t i1 = 0xffffffffu);
+hipError_t fill_twins(const Geom& g, int order, hipStream_t s, double* edges, uint32_t i0 = 0, uint32_t i1 = 0xffffffffu);
 hipError_t launch_edge3d(const Geom& g, int order, int umode, hipStream_t s, const double* theta, double* edges,
                          double t_old, double c_old, double t_new, const double* theta_old, double* partials,
                          int* nparts, const AdmmCtl* ctl = nullptr);

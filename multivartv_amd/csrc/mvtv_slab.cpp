@@ -497,8 +497,9 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     const bool pingpong = fused || fused4;
     // twin blocks (mvtv_internal.h twin_block): the run starts from u0 = 0, so the twins are equal whenever their
     // weights are (the same global deltas on every rank, hence the same choice); filled when the run ends
-    // (3-D only: the 4-D ranks' ghost-plane pass A reads every block of the z halo)
-    const bool twin = fused && p == 3 && twin_weights_equal(P->g, P->order) && !probe_env("MVTV_TWIN_OFF");
+    // (4-D: the last owned plane's twins are filled before it goes to the next rank, whose ghost-plane pass A reads
+    // every block of the halo)
+    const bool twin = (fused || fused4) && twin_weights_equal(P->g, P->order) && !probe_env("MVTV_TWIN_OFF");
     if (P->timing && (fused || fused4)) P->twin_timed = twin;
     // folded right-hand side (as mvtv_capi.cpp's loop): the fused kernel stores s = rho (D^T alpha + D^T u) and the
     // next first pass reads oty + s (oty + (rho'/rho) s + rho' (c - 1) D^T u after a rho change)
@@ -856,9 +857,11 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
             int h = P->tstart(MVTV_K_ADMM_FUSED4);
             int npe = 0;
             HIP_TRY(launch_admm4a(P->g, P->order, um, s, P->theta, zo, zn, 0.0, 1.0, 0.0, nullptr, P->g4, P->partials,
-                                  &npe, P->ctl));
+                                  &npe, P->ctl, twin));
             P->tstop(h);
             HIP_TRY(launch_finalize(s, P->partials, npe, ER_N, 1, 0, P->red, P->st, 0.0, 0, P->ctl));
+            if (!solo && twin && rk < G - 1)
+                HIP_TRY(fill_twins(P->g, P->order, s, zn, uint32_t(last_owned), uint32_t(last_owned + pl)));
             if (!solo) {
                 MVTV_TRY(handoff(ev[EV_EDGE], s, sc));
                 MVTV_TRY(C->begin());
