@@ -1419,23 +1419,33 @@ hipError_t launch_gather4(const Geom& g, int order, int umode, hipStream_t s, co
 // 0..6); the image holds 13 of the 15 blocks (S' = {2} and {3} are read by their own cell only) in two plane
 // buffers: 13 x 7 x 65 x 8 B x 2 = 95 KB, one workgroup per CU, up to 256 VGPRs a lane (the 1024-thread form of
 // round 2 spilled at 128).
+// With the twins skipped (TW) the image holds 9 of the 13 blocks, so the tile grows to 10 owned rows (11 image rows,
+// 768 threads: 12 waves a CU instead of 8, 103 KB of LDS, <= 170 VGPRs a lane): 128^4 launch 12.22 -> 11.87 ms, same
+// box (profiles/r04/v16_f4a_tall)).
 namespace f4a {
-constexpr int IW = 65, IH = 7, TY = IH - 1, NT = 512;
+constexpr int IW = 65;
+constexpr int ih(bool tw) { return tw ? 11 : 7; }
+constexpr int nt(bool tw) { return (ih(tw) + 1) * 64; }
 }
 
-template <int NB, int ORD>
+// image slots: the blocks whose S' has dim 0 or 1, minus the twins when they are skipped
+template <int NB, int ORD, bool TW = false>
+__host__ __device__ constexpr bool f4a_in_image(int k) {
+    return (sprime_mask(block_code(k, 4, ORD), 4) & 3) != 0 && !(TW && twin_of(k, 4, ORD) != k);
+}
+template <int NB, int ORD, bool TW = false>
 __host__ __device__ constexpr int f4a_nimg() {
     int n = 0;
     for (int k = 0; k < NB; ++k)
-        if ((sprime_mask(block_code(k, 4, ORD), 4) & 3) != 0) ++n;
+        if (f4a_in_image<NB, ORD, TW>(k)) ++n;
     return n;
 }
-template <int NB, int ORD>
+template <int NB, int ORD, bool TW = false>
 __host__ __device__ constexpr int f4a_slot(int k) {
     int n = 0;
     for (int j = 0; j < k; ++j)
-        if ((sprime_mask(block_code(j, 4, ORD), 4) & 3) != 0) ++n;
-    return (sprime_mask(block_code(k, 4, ORD), 4) & 3) != 0 ? n : -1;
+        if (f4a_in_image<NB, ORD, TW>(j)) ++n;
+    return f4a_in_image<NB, ORD, TW>(k) ? n : -1;
 }
 
 struct Fused4Args {
@@ -1456,8 +1466,8 @@ struct Fused4Args {
 
 // TW: the twin blocks (mvtv_internal.h twin_of) are skipped as in k_admm3a, their group's first block counting for all
 template <int ORD, int UM, bool DTH, int NB, bool TW>
-__global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
-    constexpr int P = 4, NC = 16, IW = f4a::IW, IH = f4a::IH, NI = f4a_nimg<NB, ORD>();
+__global__ __launch_bounds__(f4a::nt(TW)) void k_admm4a(const Fused4Args a) {
+    constexpr int P = 4, NC = 16, IW = f4a::IW, IH = f4a::ih(TW), TY = IH - 1, NI = f4a_nimg<NB, ORD, TW>();
     static_assert(!TW || twin_block(NB, P, ORD) >= 0, "twin blocks");
     double t_old = a.t_old, c_old = a.c_old, t_new = a.t_new;
     if (a.ctl) {
@@ -1477,7 +1487,7 @@ __global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
         const int tz = rem / nt;
         rem -= tz * nt;
         const int tyi = rem / a.tiles_x, txi = rem - tyi * a.tiles_x;
-        const int X0 = txi * 64, Yh = tyi * f4a::TY - 1;
+        const int X0 = txi * 64, Yh = tyi * TY - 1;
         const int w = a.wa + tw;
         const int m0 = int(g.m[0]), m1 = int(g.m[1]), m2 = int(g.m[2]), m3 = int(g.m[3]);
         const int z0 = tz * a.zchunk, z1 = min(m2, z0 + a.zchunk);
@@ -1558,7 +1568,7 @@ __global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
             if (!active) return;
             static_for<0, NB>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
-                constexpr int sl = f4a_slot<NB, ORD>(k);
+                constexpr int sl = f4a_slot<NB, ORD, TW>(k);
                 if constexpr (sl >= 0 && !(TW && twin_of(k, P, ORD) != k)) szr[sidx(buf, sl, row, col)] = zn[k];
             });
         };
@@ -1566,7 +1576,7 @@ __global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
             constexpr int k = decltype(kc)::value;
             constexpr int S = sprime_mask(block_code(k, P, ORD), P);
             constexpr int SI = S & 3;
-            constexpr int sl = f4a_slot<NB, ORD>(k);
+            constexpr int sl = f4a_slot<NB, ORD, TW>(k);
             qa = 0.0;
             qu = 0.0;
 #pragma unroll
@@ -1683,7 +1693,7 @@ __global__ __launch_bounds__(f4a::NT) void k_admm4a(const Fused4Args a) {
             for (int k = 0; k < NB; ++k) zo[k] = nzo[k];
         }
     }
-    block_reduce_store<ER_N, 1, f4a::NT>(red, a.partials);
+    block_reduce_store<ER_N, 1, f4a::nt(TW)>(red, a.partials);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1938,14 +1948,15 @@ hipError_t launch_admm2d(const Geom& g, int order, int umode, hipStream_t s, con
 
 // ------------------------------------------------------------------------------------------------ k_admm4a
 namespace {
-Fused4Args f4a_args(const Geom& g) {
+Fused4Args f4a_args(const Geom& g, bool tw = false) {
     Fused4Args a{};
     a.g = g;
     const uint32_t pl3 = g.m[0] * g.m[1] * g.m[2];
     a.wa = int(g.ibeg / pl3);
     const int nw = std::max(1, int(g.iend / pl3) - a.wa);
+    const int ty = f4a::ih(tw) - 1;
     a.tiles_x = int((g.m[0] + 63) / 64);
-    a.tiles_y = int((int(g.m[1]) + f4a::TY - 1) / f4a::TY);
+    a.tiles_y = int((int(g.m[1]) + ty - 1) / ty);
     const int tiles = a.tiles_x * a.tiles_y * nw;
     // z chunks only when the (tile, w) items alone leave the chip under ~4 waves (one workgroup per CU): every chunk
     // start recomputes one plane
@@ -1969,7 +1980,7 @@ hipError_t launch_admm4a(const Geom& g, int order, int umode, hipStream_t s, con
                          double* scratch4, double* partials, int* nparts, const AdmmCtl* ctl, bool twin) {
     if (!fused4_ok(g) || !scratch4 || z_old == z_new) return hipErrorInvalidValue;
     if (twin && !twin_weights_equal(g, order)) return hipErrorInvalidValue;
-    Fused4Args a = f4a_args(g);
+    Fused4Args a = f4a_args(g, twin);
     a.t_old = t_old;
     a.c_old = c_old;
     a.t_new = t_new;
@@ -1987,7 +1998,7 @@ hipError_t launch_admm4a(const Geom& g, int order, int umode, hipStream_t s, con
     *nparts = grid;
     const bool dth = theta_old != nullptr;
     auto go = [&](auto kern) {
-        klaunch(kern, dim3(grid), dim3(f4a::NT), 0, s, a);
+        klaunch(kern, dim3(grid), dim3(f4a::nt(twin)), 0, s, a);
         return hipGetLastError();
     };
     auto pick = [&](auto ordc, auto nbc, auto twc) {
