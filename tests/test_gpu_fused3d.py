@@ -122,10 +122,13 @@ def _sprime(b, p):
     return tuple(sorted(set(S) - {min(S)} | {0}))
 
 
-def _blocks(m, order=0):
-    """(S' per block, block lengths) in the reference's block order (cpp-code/utils.cpp:258-267)."""
+def _blocks(m, order=0, drop_ones=False):
+    """(S' per block, block lengths) in the reference's block order (cpp-code/utils.cpp:258-267; Python order
+    code/utils.py:138-149, which drops the all-ones block when deltas are given)."""
     p = len(m)
     codes = [(1 << p) - 1] + list(range(1, (1 << p) - 1)) if order == 0 else list(range(1, 1 << p))
+    if drop_ones:
+        codes = [c for c in codes if c != (1 << p) - 1]
     sp = [_sprime(c, p) for c in codes]
     return sp, [int(np.prod([v - 1 if j in s else v for j, v in enumerate(m)])) for s in sp]
 
@@ -191,3 +194,32 @@ def test_twin_block_bytes_counted_once():
     assert et == 31 * 32 * 31
     assert tm["admm_fused"]["launches"] == 3
     assert tm["admm_fused"]["bytes_per_launch"] == pytest.approx(8.0 * (4 * N + 2 * (E - et)), rel=1e-12)
+
+
+def test_twin_block_python_order_matches_oracle():
+    """Python block order with deltas (6 blocks at 3-D, the all-ones block dropped): the twin pair is codes 3 and 5;
+    an explicit u with equal twins takes the twin kernel. Against the C oracle (order 1, weighted)."""
+    m = [36, 36, 20]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    lam, iters = 1.0, 4
+    th0 = np.full(y.size, y.mean())
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_PY, weighted=True) as P:
+        E = P.E
+        sp, blen = _blocks(m, order=1, drop_ones=True)
+        assert sum(blen) == E and len(sp) == 6
+        off = np.concatenate([[0], np.cumsum(blen)])
+        rng = np.random.default_rng(11)
+        u0 = 0.05 * rng.standard_normal(E)
+        for k in range(len(sp)):
+            if sp[k] in sp[:k]:
+                c = sp.index(sp[k])
+                u0[off[k]:off[k + 1]] = u0[off[c]:off[c + 1]]
+        th, u, rho, st = P.admm(lam, th0, u=u0.copy(), rho=lam / 5, fixed_iters=iters, pcg_rtol=1e-13)
+    ref_th = th0.copy()
+    ref_u = u0.copy()
+    rs = c_oracle.admm_rcpp(m, y, lam, ref_th, ref_u, lam / 5, deltas, order=1, weighted=1, fixed_iters=iters,
+                            pcg_rtol=1e-13)
+    assert rho == rs["rho"]
+    assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
+    assert np.max(np.abs(u - ref_u)) <= 1e-9 * max(1.0, np.max(np.abs(ref_u)))
