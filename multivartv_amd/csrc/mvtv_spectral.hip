@@ -3027,13 +3027,22 @@ static void launch_tri(SpecArgs& a, hipStream_t s, int tq) {
             const char* e = probe_env("MVTV_TRI_SEG");
             return e && std::atoi(e) == 32 ? 32 : 16;
         }();
-        static const int tq32 = [] {   // probe: 32-line tiles (256-B rows)
+        // 64 lines of 32-row segments per workgroup (512-B rows: one full run per load instruction of a wave) where
+        // the lines fill >= 256 such workgroups: 512^3 k_tri ~0.49 -> ~0.44 ms, 170.1 / 170.5 -> 171.8 / 172.0 ADMM it/s
+        // on one box (profiles/r04/v18_tri64). Probe builds: MVTV_TRI_TQ=16 / 32 force the 16- / 32-line tiles.
+        static const int tqw = [] {
             const char* e = probe_env("MVTV_TRI_TQ");
-            return e && std::atoi(e) == 32 ? 1 : 0;
+            return e ? std::atoi(e) : 64;
         }();
-        if (tq32 && seg == 16 && a.stride >= 32u) {
+        if (tqw == 32 && seg == 16 && a.stride >= 32u) {
             a.tq = 32;
             launch_tri_seg<16, 32>(a, s);
+        } else if (tqw == 64 && seg == 16 && a.stride >= 64u && a.L >= 7 && a.L <= 9 && a.nlines / 64u >= 256u) {
+            a.tq = 64;
+            const dim3 grid((a.nlines + 63u) / 64u);
+            if (a.L == 7) klaunch(k_tri<7, 32, 64>, grid, dim3(tri::Shape<7, 32, 64>::NT), 0, s, a);
+            else if (a.L == 8) klaunch(k_tri<8, 32, 64>, grid, dim3(tri::Shape<8, 32, 64>::NT), 0, s, a);
+            else klaunch(k_tri<9, 32, 64>, grid, dim3(tri::Shape<9, 32, 64>::NT), 0, s, a);
         } else if (seg == 32) {
             launch_tri_seg<32, tri::TQ>(a, s);
         } else {
