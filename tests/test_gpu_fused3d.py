@@ -223,3 +223,27 @@ def test_twin_block_python_order_matches_oracle():
     assert rho == rs["rho"]
     assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
     assert np.max(np.abs(u - ref_u)) <= 1e-9 * max(1.0, np.max(np.abs(ref_u)))
+
+
+def test_twin_state_carried_across_runs_matches_oracle():
+    """Two resident runs in a row (the lambda path's warm start: theta, u and rho carried, rcpp…/solvers.cpp:212-220):
+    the first run ends by filling the twin block from its partner, the second resumes from the stored z. Against the
+    C oracle called twice on the carried state: rho exactly, theta and u to 1e-9."""
+    m = [40, 40, 24]
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    th0 = np.full(y.size, y.mean())
+    lams = (1.0, 0.6)
+    with mv.Problem(m, y, deltas=deltas, order=mv.ORDER_CPP) as P:
+        E = P.E
+        P.state_set(th0, np.zeros(E), lams[0] / 5)
+        for lam in lams:
+            P.run(lam, fixed_iters=4, pcg_rtol=1e-13)
+        th, u, rho = P.state_get()
+    ref_th, ref_u, ref_rho = th0.copy(), np.zeros(E), lams[0] / 5
+    for lam in lams:
+        rs = c_oracle.admm_rcpp(m, y, lam, ref_th, ref_u, ref_rho, deltas, fixed_iters=4, pcg_rtol=1e-13)
+        ref_rho = rs["rho"]
+    assert rho == ref_rho
+    assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
+    assert np.max(np.abs(u - ref_u)) <= 1e-9 * max(1.0, np.max(np.abs(ref_u)))
