@@ -124,6 +124,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--slab-ranks", type=int, default=1,
                     help="--mode slab without torchrun: ranks of an in-process rehearsal on one GPU (1: RCCL, one rank)")
+    ap.add_argument("--transport", choices=["auto", "rccl", "ipc"], default="auto",
+                    help="slab collectives at N > 1: RCCL (one process per GPU), or ipc (HIP IPC buffers between the "
+                         "rank processes, host-synchronous: ranks sharing a GPU); auto = RCCL unless ranks share a "
+                         "GPU, and ipc when RCCL has no communicator")
     ap.add_argument("--cpu-planes", type=int, default=0,
                     help="cpu_baseline sample: slowest-dim planes of the mesh (0 = a quarter of them)")
     ap.add_argument("--cpu-full", action="store_true", help="cpu_baseline on the whole mesh (no extrapolation)")
@@ -230,6 +234,24 @@ def _cpu_model():
     return None
 
 
+def _usable_cores():
+    """The CPUs this process may run on (its affinity mask): the baseline's OpenMP threads and scipy.fft workers.
+    os.cpu_count() and OMP_NUM_THREADS are reported beside it, not used."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def _cgroup_cpu_max():
+    """cgroup v2 cpu.max ('quota period', or 'max period'): a CPU-time cap the affinity mask does not show."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
 def cpu_baseline(m, lam, pcg_iters, planes, full=False):
     """The CPU oracle on the host cores, one ADMM iteration (variant B) of the same towers problem:
       * spectral (the headline's like-for-like, `value`): oracle/c/mvtv_oracle.c's loop with the exact
@@ -238,7 +260,7 @@ def cpu_baseline(m, lam, pcg_iters, planes, full=False):
       * pcg: the same loop with Jacobi-PCG at the GPU PCG leg's mean iteration count, all cores on the slab
         (or the whole mesh with full=True) and 1 thread on a quarter of that, scaled the same way (labelled)."""
     from oracle import c_oracle
-    ncores = c_oracle.threads()
+    ncores = _usable_cores()
     deltas = [(1.0 + 2e-4) / v for v in m]
     n_full = float(np.prod(m))
 
@@ -265,7 +287,8 @@ def cpu_baseline(m, lam, pcg_iters, planes, full=False):
     dims = lambda sub: "x".join(map(str, sub))   # noqa: E731
     where_s = "the whole mesh" if sc_spec == 1.0 else f"a {dims(sub_s)} slab, rate scaled by {sc_spec:.0f}"
     return dict(value=1.0 / (t_spec * sc_spec), unit="iters/s", cores=ncores, kind="port",
-                cpu_model=_cpu_model(), host_cpus=os.cpu_count(), omp_num_threads=os.environ.get("OMP_NUM_THREADS"),
+                cpu_model=_cpu_model(), affinity_cpus=ncores, host_cpus=os.cpu_count(),
+                omp_num_threads=os.environ.get("OMP_NUM_THREADS"), cgroup_cpu_max=_cgroup_cpu_max(),
                 algorithm="spectral",
                 sample=(f"1 ADMM iteration (variant B) of the same towers problem on {where_s}, {ncores} threads: "
                         f"oracle/c/mvtv_oracle.c loop with the exact theta-solve by scipy.fft DCT ({t_spec:.2f} s)"),
@@ -298,6 +321,17 @@ def _rccl_comm(D, dev):
     return slab.Comm.rccl(dev) if D.dist else slab.Comm.rccl_single(dev)
 
 
+def _slab_comm(a, D, dev):
+    """The slab loop's transport: RCCL (one process per GPU) or the inter-process HIP-IPC group (--transport ipc;
+    auto takes it when ranks share a GPU, where RCCL refuses the communicator)."""
+    from multivartv_amd import slab
+    kind = a.transport
+    if kind == "auto":
+        shared, = D.allreduce([1.0 if D.world > max(1, mv.device_count()) else 0.0], "max")
+        kind = "ipc" if (D.dist and shared) else "rccl"
+    return slab.Comm.ipc(dev) if (kind == "ipc" and D.dist) else _rccl_comm(D, dev)
+
+
 def slab_main(a, D, comm=None):
     """One mesh decomposed over the ranks (the metric at 2/4/8 GPUs): strong scaling.
     Every rank runs the whole ADMM loop inside libmvtv (mvtv_slab_run) with RCCL collectives on its stream.
@@ -312,7 +346,7 @@ def slab_main(a, D, comm=None):
         dev = D.local % max(1, mv.device_count())
         own = comm is None
         if own:
-            comm = _rccl_comm(D, dev)
+            comm = _slab_comm(a, D, dev)
         b = slab.plane_bounds(m[-1], D.world)
         pl = int(np.prod(m[:-1]))
         y = towers(m, start=int(b[D.rank]) * pl, count=int(b[D.rank + 1] - b[D.rank]) * pl)
@@ -330,8 +364,14 @@ def slab_main(a, D, comm=None):
         tim = S.P.timings()
         S.P.timing(False)
         g_elapsed, = D.allreduce([t1 - t0], "max")
-        nranks, rccl_ranks = D.world, comm.size
-        transport = "RCCL" if D.world > 1 else "RCCL (one rank)"
+        nranks = D.world
+        rccl_ranks = comm.size if comm.kind == "rccl" else 0
+        if comm.kind == "ipc":
+            transport = (f"HIP IPC between {D.world} rank processes"
+                         + (" on one GPU" if D.world > max(1, mv.device_count()) else "")
+                         + ", host-synchronous collectives")
+        else:
+            transport = "RCCL" if D.world > 1 else "RCCL (one rank)"
         S.close()
         if own:
             comm.close()
@@ -363,6 +403,7 @@ def slab_main(a, D, comm=None):
                    "parallelism": f"slab x{nranks} ({transport}: halo planes, "
                                   f"{'6+2 numbers per line all-to-all, ' if distributed else ''}7-sum all-reduce)"},
         "rccl_ranks": rccl_ranks, "rccl_library": slab.Comm.library() if rccl_ranks else None,
+        "transport": transport,
         "roofline": _roofline(tim), "kernels_rank0": per,
         "residuals": {"r_norm": st["r_norm"], "s_norm": st["s_norm"]}, "cpu_baseline": None}
 
@@ -598,7 +639,9 @@ def independent_main(a, D, comm=None):
     return {
         "metric": METRIC, "value": round(value, 4), "unit": "iters/s", "n_gpus": D.world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(g_elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        # one fit of the metric's mesh at N = 1; at N > 1 the line is that same mesh slab-decomposed (total work
+        # fixed), so the N = 1 line is the strong-scaling curve's first point
+        "scaling": "strong" if D.world == 1 else "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: 3D towers + 0.5 N(0,1) (splitmix64/Box-Muller, seed 0x4D565456 + rank), O = I",
         "config": {"workload": f"{a.dims}D {a.size}^{a.dims} fp64 mesh-TV ADMM, variant B (rcpp admm_update), "
                                f"lambda={lam}, fixed-iteration mode",
@@ -643,14 +686,29 @@ def main():
         # A failure of the RCCL communicator or of the slab run (the same on every rank: the ranks agree on it
         # over gloo) still leaves the independent fits' line, labelled with the error.
         comm, err = None, None
+        dev = D.local % mv.device_count()
         try:
-            comm = _rccl_comm(D, D.local % mv.device_count())
+            comm = _slab_comm(a, D, dev)
         except Exception as e:  # noqa: BLE001 (reported in the line)
-            err = f"RCCL communicator: {e!r}"
+            err = f"communicator: {e!r}"
         failed, = D.allreduce([1.0 if comm is None else 0.0], "max")
         if failed and comm is not None:
             comm.close()
             comm = None
+        if failed and a.transport == "auto":
+            # RCCL refused on some rank: the same slab loop over the HIP IPC group of the node's processes
+            from multivartv_amd import slab
+            try:
+                comm = slab.Comm.ipc(dev)
+                err = None
+            except Exception as e:  # noqa: BLE001
+                err = f"{err}; ipc communicator: {e!r}"
+            failed, = D.allreduce([1.0 if comm is None else 0.0], "max")
+            if failed and comm is not None:
+                comm.close()
+                comm = None
+            if comm is not None:
+                log(f"rank {D.rank}: RCCL communicator failed, slab loop over the ipc transport")
         ind = independent_main(a, D, comm)
         line = None
         if comm is not None:

@@ -223,10 +223,17 @@ mvtv_status mvtv_comm_create_rccl(const uint8_t* id128, int32_t nranks, int32_t 
 /* in-process loopback group of nranks handles (comms[0..nranks-1]): each rank's mvtv_slab_run on its own
  * host thread, transfers as device copies (rehearsal of the decomposition on one GPU) */
 mvtv_status mvtv_comm_create_local(int32_t nranks, mvtv_comm** comms);
+/* inter-process group over HIP IPC memory (one process per rank; the ranks' devices one GPU or peers of one
+ * node): transfers are device-to-device copies out of the sender's buffer (hipIpcOpenMemHandle), ordered through
+ * a POSIX shared-memory rendezvous segment `name` ("/..."; rank 0 creates it, every rank passes the same name,
+ * it is unlinked once all nranks <= 16 have attached). Host-synchronous inside each collective (no overlap of
+ * the z halo): the multi-process path without RCCL, e.g. several ranks on one GPU, where RCCL refuses. Waits give
+ * up after MVTV_IPC_TIMEOUT seconds (default 300) or when a peer's loop failed. */
+mvtv_status mvtv_comm_create_ipc(const char* name, int32_t nranks, int32_t rank, int32_t device, mvtv_comm** out);
 void mvtv_comm_destroy(mvtv_comm* comm);
 int32_t mvtv_comm_rank(const mvtv_comm* comm);
 int32_t mvtv_comm_size(const mvtv_comm* comm);
-/* sum of n <= 64 host doubles over an RCCL communicator, in place (the global residual all-reduce of
+/* sum of n <= 64 host doubles over an RCCL or ipc communicator, in place (the global residual all-reduce of
  * independent fits); blocking */
 mvtv_status mvtv_comm_allreduce_host(mvtv_comm* comm, double* vals, int32_t n);
 /* the file RCCL was resolved from (ROCm's librccl, which shares libmvtv's HIP runtime); "" when RCCL is

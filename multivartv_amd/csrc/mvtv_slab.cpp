@@ -23,17 +23,27 @@
 // loopback group (every rank on its own host thread, device-to-device copies between the ranks' buffers):
 // the same loop, testable on one GPU.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
+#include <cerrno>
+
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 
 #include "mvtv_problem.h"
 
@@ -50,9 +60,11 @@ struct mvtv_comm {
     virtual mvtv_status recv(double* buf, size_t n, int peer, hipStream_t s) = 0;
     virtual mvtv_status end(hipStream_t s) = 0;
     virtual mvtv_status allreduce_sum(double* buf, size_t n, hipStream_t s) = 0;
-    // a rank whose loop failed tells its peers, so that they fail instead of waiting for it (loopback; an RCCL
-    // peer of a failed process is ended by the launcher)
+    // a rank whose loop failed tells its peers, so that they fail instead of waiting for it (loopback, ipc; an
+    // RCCL peer of a failed process is ended by the launcher)
     virtual void abort() {}
+    // called at the start of every mvtv_slab_run (the ipc transport drops its buffer mappings there)
+    virtual void run_begin() {}
 };
 
 namespace {
@@ -345,6 +357,198 @@ struct LocalComm final : mvtv_comm {
     }
 };
 
+// ---- inter-process group over HIP IPC memory --------------------------------------------------------------
+// One process per rank, the ranks' devices the same GPU or peers on one node. Data moves device to device: the
+// receiver copies straight out of the sender's buffer, which it maps with hipIpcOpenMemHandle (same GPU: an HBM
+// copy; peer GPUs: a P2P read over xGMI). Ordering goes through the host: a rendezvous segment in POSIX shared
+// memory holds, per (sender, receiver) channel, a ring of posted buffers (IPC handle, offset, count) and
+// post / ack counters; the all-reduce is a rank-ordered host sum of every rank's staged vector (bit-identical on
+// every rank, as the loopback's). end() is where a group's transfers happen: the sender waits for its data
+// (its stream), posts every send, the receiver copies every posted buffer it expects, waits for the copies and
+// acks, and the sender returns once its peers have acked, so nothing enqueued after end() can overwrite a
+// source before it was read. The host waits inside a collective, so the z halo does not overlap the next
+// theta-solve as it does under RCCL: this transport is for correctness of the multi-process path (and a
+// fallback when RCCL has no communicator), not the tuned one. Every wait polls the segment's abort flag and
+// gives up after MVTV_IPC_TIMEOUT seconds (default 300), so a dead peer ends the others with an error.
+constexpr int IPC_MAX_RANKS = 16;
+constexpr int IPC_RING = 64;
+constexpr uint64_t IPC_MAGIC = 0x4d5654564950430aull;
+
+struct IpcSlot {
+    hipIpcMemHandle_t handle;
+    uint64_t base_key;   // the sender's allocation base (its mapping cache key on the receiver)
+    uint64_t offset, n;
+};
+struct IpcChan {
+    std::atomic<uint64_t> posted;
+    std::atomic<uint64_t> acked;
+    IpcSlot slot[IPC_RING];
+};
+struct IpcShm {
+    std::atomic<uint64_t> magic;
+    std::atomic<int32_t> size;
+    std::atomic<int32_t> attached;
+    std::atomic<int32_t> aborted;
+    std::atomic<uint64_t> barrier;   // monotone arrival count: the k-th barrier ends at size * k
+    double ar[IPC_MAX_RANKS][64];
+    IpcChan ch[IPC_MAX_RANKS * IPC_MAX_RANKS];
+};
+
+struct IpcComm final : mvtv_comm {
+    IpcShm* shm = nullptr;
+    std::string name;
+    uint64_t nbar = 0;                              // barriers this rank has passed
+    std::vector<uint64_t> sent_n, recv_n;           // per peer: messages posted to / consumed from
+    struct Out { const double* buf; size_t n; int peer; };
+    struct In { double* buf; size_t n; int peer; };
+    std::vector<Out> outs;
+    std::vector<In> ins;
+    SelfCopy self;
+    std::map<uintptr_t, hipIpcMemHandle_t> exported;                    // base -> handle
+    std::map<std::pair<int, uint64_t>, char*> opened;                   // (peer, sender's base) -> mapping
+    double timeout_s = 300.0;
+
+    ~IpcComm() override {
+        close_mappings();
+        if (shm) munmap(shm, sizeof(IpcShm));
+    }
+    void close_mappings() {
+        DeviceGuard dg(device);
+        for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
+        opened.clear();
+        exported.clear();
+    }
+    void abort() override {
+        if (shm) shm->aborted.store(1);
+    }
+    void run_begin() override { close_mappings(); }   // buffers may have been freed and reallocated since
+    // poll until pred() holds; false on abort or timeout
+    template <class F>
+    bool wait(F pred, const char* what, mvtv_status* st) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (long spin = 0;; ++spin) {
+            if (pred()) return true;
+            if (shm->aborted.load()) {
+                *st = fail(MVTV_HIP_ERROR, std::string("ipc transport: a peer rank aborted (") + what + ")");
+                return false;
+            }
+            if (spin > 2000) {
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+                if ((spin & 1023) == 0 &&
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+                    shm->aborted.store(1);
+                    *st = fail(MVTV_HIP_ERROR, std::string("ipc transport: timed out waiting for ") + what);
+                    return false;
+                }
+            }
+        }
+    }
+    mvtv_status host_barrier(const char* what) {
+        ++nbar;
+        shm->barrier.fetch_add(1);
+        mvtv_status st = MVTV_OK;
+        const uint64_t target = nbar * uint64_t(size);
+        if (!wait([&] { return shm->barrier.load() >= target; }, what, &st)) return st;
+        return MVTV_OK;
+    }
+    mvtv_status begin() override {
+        outs.clear();
+        ins.clear();
+        return MVTV_OK;
+    }
+    mvtv_status send(const double* buf, size_t n, int peer, hipStream_t) override {
+        if (peer == rank) {
+            self.q.emplace_back(buf, n);
+            return MVTV_OK;
+        }
+        outs.push_back(Out{buf, n, peer});
+        return MVTV_OK;
+    }
+    mvtv_status recv(double* buf, size_t n, int peer, hipStream_t s) override {
+        if (peer == rank) return self.recv(buf, n, s);   // enqueued now: in order on s, before end()'s copies
+        ins.push_back(In{buf, n, peer});
+        return MVTV_OK;
+    }
+    mvtv_status end(hipStream_t s) override {
+        DeviceGuard dg(device);
+        mvtv_status st = MVTV_OK;
+        if (!outs.empty()) HIP_TRY(hipStreamSynchronize(s));   // every send's data is in place
+        for (const Out& o : outs) {
+            void* base = nullptr;
+            size_t bytes = 0;
+            HIP_TRY(hipMemGetAddressRange(&base, &bytes, const_cast<double*>(o.buf)));
+            auto it = exported.find(reinterpret_cast<uintptr_t>(base));
+            if (it == exported.end()) {
+                hipIpcMemHandle_t h;
+                HIP_TRY(hipIpcGetMemHandle(&h, base));
+                it = exported.emplace(reinterpret_cast<uintptr_t>(base), h).first;
+            }
+            IpcChan& c = shm->ch[rank * IPC_MAX_RANKS + o.peer];
+            const uint64_t k = sent_n[size_t(o.peer)];
+            if (!wait([&] { return k - c.acked.load() < uint64_t(IPC_RING); }, "a free ring slot", &st)) return st;
+            IpcSlot& sl = c.slot[k % IPC_RING];
+            sl.handle = it->second;
+            sl.base_key = reinterpret_cast<uintptr_t>(base);
+            sl.offset = uint64_t(reinterpret_cast<const char*>(o.buf) - static_cast<const char*>(base));
+            sl.n = o.n;
+            c.posted.store(k + 1);   // release: the slot's contents before the count
+            sent_n[size_t(o.peer)] = k + 1;
+        }
+        for (const In& i : ins) {
+            IpcChan& c = shm->ch[i.peer * IPC_MAX_RANKS + rank];
+            const uint64_t k = recv_n[size_t(i.peer)];
+            if (!wait([&] { return c.posted.load() > k; }, "a peer's send", &st)) return st;
+            const IpcSlot& sl = c.slot[k % IPC_RING];
+            if (sl.n != i.n) return fail(MVTV_BAD_ARG, "ipc transfer size mismatch");
+            const auto key = std::make_pair(i.peer, sl.base_key);
+            auto it = opened.find(key);
+            if (it == opened.end()) {
+                void* p = nullptr;
+                HIP_TRY(hipIpcOpenMemHandle(&p, sl.handle, hipIpcMemLazyEnablePeerAccess));
+                it = opened.emplace(key, static_cast<char*>(p)).first;
+            }
+            HIP_TRY(hipMemcpyAsync(i.buf, it->second + sl.offset, i.n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        }
+        if (!ins.empty()) HIP_TRY(hipStreamSynchronize(s));   // the copies have read their sources
+        for (const In& i : ins) {
+            IpcChan& c = shm->ch[i.peer * IPC_MAX_RANKS + rank];
+            recv_n[size_t(i.peer)] += 1;
+            c.acked.store(recv_n[size_t(i.peer)]);
+        }
+        for (const Out& o : outs) {
+            IpcChan& c = shm->ch[rank * IPC_MAX_RANKS + o.peer];
+            const uint64_t k = sent_n[size_t(o.peer)];
+            if (!wait([&] { return c.acked.load() >= k; }, "a peer's ack", &st)) return st;
+        }
+        outs.clear();
+        ins.clear();
+        return MVTV_OK;
+    }
+    mvtv_status allreduce_host_vals(double* v, size_t n) {
+        if (n > 64) return fail(MVTV_BAD_ARG, "ipc all-reduce of more than 64 values");
+        std::memcpy(shm->ar[rank], v, n * sizeof(double));
+        MVTV_TRY(host_barrier("the all-reduce"));          // every vector posted
+        for (size_t i = 0; i < n; ++i) {
+            double acc = 0.0;
+            for (int r = 0; r < size; ++r) acc += shm->ar[r][i];
+            v[i] = acc;
+        }
+        return host_barrier("the all-reduce");             // slots reusable
+    }
+    mvtv_status allreduce_sum(double* buf, size_t n, hipStream_t s) override {
+        if (size == 1) return MVTV_OK;
+        DeviceGuard dg(device);
+        double v[64];
+        if (n > 64) return fail(MVTV_BAD_ARG, "ipc all-reduce of more than 64 values");
+        HIP_TRY(hipMemcpyAsync(v, buf, n * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        MVTV_TRY(allreduce_host_vals(v, n));
+        HIP_TRY(hipMemcpyAsync(buf, v, n * sizeof(double), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        return MVTV_OK;
+    }
+};
+
 }  // namespace
 
 // ============================================================================================ C ABI
@@ -396,12 +600,78 @@ mvtv_status mvtv_comm_create_local(int32_t nranks, mvtv_comm** out) {
     return MVTV_OK;
 }
 
+mvtv_status mvtv_comm_create_ipc(const char* name, int32_t nranks, int32_t rank, int32_t device, mvtv_comm** out) {
+    if (!name || !out || name[0] != '/' || nranks < 1 || nranks > IPC_MAX_RANKS || rank < 0 || rank >= nranks)
+        return fail(MVTV_BAD_ARG, "bad argument (name '/...', 1 <= nranks <= 16)");
+    auto c = std::make_unique<IpcComm>();
+    c->rank = rank;
+    c->size = nranks;
+    c->device = device;
+    c->name = name;
+    c->sent_n.assign(size_t(nranks), 0);
+    c->recv_n.assign(size_t(nranks), 0);
+    if (const char* t = std::getenv("MVTV_IPC_TIMEOUT")) c->timeout_s = std::max(1.0, std::atof(t));
+    const size_t bytes = sizeof(IpcShm);
+    int fd = -1;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto elapsed = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+    if (rank == 0) {
+        fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0) return fail(MVTV_HIP_ERROR, std::string("ipc transport: shm_open(create) ") + name + ": " + std::strerror(errno));
+        if (ftruncate(fd, off_t(bytes)) != 0) {
+            close(fd);
+            shm_unlink(name);
+            return fail(MVTV_HIP_ERROR, "ipc transport: ftruncate failed");
+        }
+    } else {
+        while ((fd = shm_open(name, O_RDWR, 0600)) < 0) {   // rank 0 creates it
+            if (elapsed() > c->timeout_s) return fail(MVTV_HIP_ERROR, std::string("ipc transport: no segment ") + name);
+            std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        }
+        struct stat sb {};
+        while (fstat(fd, &sb) == 0 && size_t(sb.st_size) < bytes) {
+            if (elapsed() > c->timeout_s) {
+                close(fd);
+                return fail(MVTV_HIP_ERROR, "ipc transport: segment never sized");
+            }
+            std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        }
+    }
+    void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) {
+        if (rank == 0) shm_unlink(name);
+        return fail(MVTV_HIP_ERROR, "ipc transport: mmap failed");
+    }
+    c->shm = static_cast<IpcShm*>(m);   // a fresh segment is zero-filled: every counter starts at 0
+    if (rank == 0) {
+        c->shm->size.store(nranks);
+        c->shm->magic.store(IPC_MAGIC);
+    } else {
+        while (c->shm->magic.load() != IPC_MAGIC) {
+            if (elapsed() > c->timeout_s) return fail(MVTV_HIP_ERROR, "ipc transport: segment never initialised");
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        if (c->shm->size.load() != nranks) return fail(MVTV_BAD_ARG, "ipc transport: rank count differs from rank 0's");
+    }
+    c->shm->attached.fetch_add(1);
+    mvtv_status st = MVTV_OK;
+    if (!c->wait([&] { return c->shm->attached.load() >= nranks; }, "every rank to attach", &st)) {
+        if (rank == 0) shm_unlink(name);
+        return st;
+    }
+    if (rank == 0) shm_unlink(name);   // every rank has it mapped: nothing is left in /dev/shm
+    *out = c.release();
+    return MVTV_OK;
+}
+
 void mvtv_comm_destroy(mvtv_comm* c) { delete c; }
 
 mvtv_status mvtv_comm_allreduce_host(mvtv_comm* c, double* vals, int32_t n) {
     if (!c || (!vals && n > 0) || n < 0 || n > 64) return fail(MVTV_BAD_ARG, "bad argument (n <= 64)");
-    if (!dynamic_cast<RcclComm*>(c)) return fail(MVTV_BAD_ARG, "host all-reduce: RCCL communicators only");
     if (n == 0) return MVTV_OK;
+    if (auto* ic = dynamic_cast<IpcComm*>(c)) return ic->size == 1 ? MVTV_OK : ic->allreduce_host_vals(vals, size_t(n));
+    if (!dynamic_cast<RcclComm*>(c)) return fail(MVTV_BAD_ARG, "host all-reduce: RCCL or ipc communicators only");
     DeviceGuard dg(c->device);
     if (!c->stream) HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     if (!c->scratch) MVTV_TRY(alloc(&c->scratch, 64));
@@ -992,6 +1262,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
 extern "C" mvtv_status mvtv_slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, double lambda,
                                      double theta0, double rho0, mvtv_admm_stats* stats) {
     if (!C) return fail(MVTV_BAD_ARG, "null communicator");
+    C->run_begin();
     const mvtv_status st =
         (!P || !opts) ? fail(MVTV_BAD_ARG, "null argument") : slab_run(P, C, opts, lambda, theta0, rho0, stats);
     if (st != MVTV_OK && st != MVTV_MAXITER) C->abort();

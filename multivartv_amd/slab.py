@@ -16,8 +16,11 @@ problem's HIP stream and the adapt_step / stopping decisions taken on the device
   z halo        (p = 3) the new z's last owned plane -> rank+1 (the next chunk-start recompute).
 
 Transports (``Comm``): RCCL over xGMI, one process per GPU (``Comm.rccl``; the 128-byte unique id goes
-through torch.distributed), or an in-process loopback group (``Comm.local_group``): every rank on its own
-host thread, transfers as device copies, so a G-rank decomposition is rehearsed on one GPU.
+through torch.distributed); an inter-process group over HIP IPC memory (``Comm.ipc``: one process per rank,
+the ranks on one GPU or on peer GPUs of a node, device-to-device copies out of the peer's buffer, ordered
+through a shared-memory rendezvous; host-synchronous collectives); or an in-process loopback group
+(``Comm.local_group``): every rank on its own host thread, transfers as device copies, so a G-rank
+decomposition is rehearsed on one GPU.
 """
 from __future__ import annotations
 
@@ -43,6 +46,7 @@ _SIGS = {
     "mvtv_comm_unique_id": (_C.c_int, [_C.c_char_p]),
     "mvtv_comm_create_rccl": (_C.c_int, [_C.c_char_p, _C.c_int32, _C.c_int32, _C.c_int32, _C.POINTER(_C.c_void_p)]),
     "mvtv_comm_create_local": (_C.c_int, [_C.c_int32, _C.POINTER(_C.c_void_p)]),
+    "mvtv_comm_create_ipc": (_C.c_int, [_C.c_char_p, _C.c_int32, _C.c_int32, _C.c_int32, _C.POINTER(_C.c_void_p)]),
     "mvtv_comm_destroy": (None, [_C.c_void_p]),
     "mvtv_comm_rank": (_C.c_int32, [_C.c_void_p]),
     "mvtv_comm_size": (_C.c_int32, [_C.c_void_p]),
@@ -69,8 +73,9 @@ def plane_bounds(m_last: int, world: int):
 class Comm:
     """A transport of mvtv_slab_run (an mvtv_comm handle)."""
 
-    def __init__(self, h):
+    def __init__(self, h, kind="local"):
         self._h = h
+        self.kind = kind   # "rccl", "ipc" or "local"
         self.rank = int(_L().mvtv_comm_rank(h))
         self.size = int(_L().mvtv_comm_size(h))
 
@@ -87,7 +92,7 @@ class Comm:
         dist.broadcast_object_list(buf, src=0, group=group)
         h = _C.c_void_p()
         _lib._check(_L().mvtv_comm_create_rccl(buf[0], world, rank, device, _C.byref(h)))
-        return cls(h)
+        return cls(h, "rccl")
 
     @classmethod
     def rccl_single(cls, device: int):
@@ -96,7 +101,21 @@ class Comm:
         _lib._check(_L().mvtv_comm_unique_id(raw))
         h = _C.c_void_p()
         _lib._check(_L().mvtv_comm_create_rccl(raw.raw, 1, 0, device, _C.byref(h)))
-        return cls(h)
+        return cls(h, "rccl")
+
+    @classmethod
+    def ipc(cls, device: int, group=None):
+        """Inter-process group over HIP IPC memory across the ranks of torch.distributed's (default) group
+        (any backend: only a segment name is broadcast). Works where RCCL refuses, e.g. several ranks on one GPU."""
+        import uuid
+
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        buf = [f"/mvtv_{os.getpid()}_{uuid.uuid4().hex[:12]}" if rank == 0 else None]
+        dist.broadcast_object_list(buf, src=0, group=group)
+        h = _C.c_void_p()
+        _lib._check(_L().mvtv_comm_create_ipc(buf[0].encode(), world, rank, device, _C.byref(h)))
+        return cls(h, "ipc")
 
     @classmethod
     def local_group(cls, n: int):
@@ -106,7 +125,7 @@ class Comm:
         return [cls(_C.c_void_p(hs[i])) for i in range(n)]
 
     def allreduce_host(self, vals):
-        """Sum of a few host doubles over the RCCL communicator (blocking)."""
+        """Sum of a few host doubles over the RCCL or ipc communicator (blocking)."""
         v = np.ascontiguousarray(np.asarray(vals, dtype=np.float64).ravel())
         _lib._check(_L().mvtv_comm_allreduce_host(self._h, v.ctypes.data_as(_dp), v.size))
         return v

@@ -25,3 +25,15 @@ def load_golden(name):
 @pytest.fixture
 def golden():
     return load_golden
+
+
+def log_parity(case, **errs):
+    """Record the achieved error of one parity check: a JSON line in $MVTV_PARITY_LOG (if set), so the
+    errors the suite actually reached on the GPU box can be tabulated."""
+    path = os.environ.get("MVTV_PARITY_LOG")
+    if not path:
+        return
+    rec = {"case": case}
+    rec.update({k: (float(v) if not isinstance(v, (int, str)) else v) for k, v in errs.items()})
+    with open(path, "a") as f:
+        f.write(json.dumps(rec) + "\n")

@@ -32,6 +32,6 @@ def test_spectral_and_pcg_trajectories_agree(m, iters):
     assert ss["theta_solver"] == mv.SOLVER_SPECTRAL and sp["theta_solver"] == mv.SOLVER_PCG
     assert rs == rp
     assert np.max(np.abs(ts - tp)) <= 1e-9 * np.max(np.abs(tp))
-    assert ss["r_norm"] == pytest.approx(sp["r_norm"], rel=1e-8)
-    assert ss["s_norm"] == pytest.approx(sp["s_norm"], rel=1e-8)
+    assert ss["r_norm"] == pytest.approx(sp["r_norm"], rel=1e-9)
+    assert ss["s_norm"] == pytest.approx(sp["s_norm"], rel=1e-9)
 

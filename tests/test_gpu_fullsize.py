@@ -45,8 +45,8 @@ def _two_solvers(m, iters):
     assert ss["iters"] == sp["iters"] == iters
     assert rs == rp
     assert np.max(np.abs(ts - tp)) <= 1e-9 * np.max(np.abs(tp))
-    assert ss["r_norm"] == pytest.approx(sp["r_norm"], rel=1e-8)
-    assert ss["s_norm"] == pytest.approx(sp["s_norm"], rel=1e-8)
+    assert ss["r_norm"] == pytest.approx(sp["r_norm"], rel=1e-9)
+    assert ss["s_norm"] == pytest.approx(sp["s_norm"], rel=1e-9)
     return ss, sp
 
 
@@ -135,8 +135,8 @@ def test_config4_fold_path_2048_vs_c_oracle(solver):
         assert stats[k]["iters"] == iters and stats[k]["theta_solver"] == want
         assert rhos[k] == rho
         assert np.max(np.abs(thetas[k] - th)) <= 1e-9 * np.max(np.abs(th)), k
-        assert stats[k]["r_norm"] == pytest.approx(st["r_norm"], rel=1e-8)
-        assert stats[k]["s_norm"] == pytest.approx(st["s_norm"], rel=1e-8)
+        assert stats[k]["r_norm"] == pytest.approx(st["r_norm"], rel=1e-9)
+        assert stats[k]["s_norm"] == pytest.approx(st["s_norm"], rel=1e-9)
 
 
 def test_metric_512_cubed_eight_rank_decomposition():

@@ -1,25 +1,33 @@
 """GPU parity: the HIP path (through the C ABI) against the CPU oracle and the golden fixtures.
 
 Tolerances (fp64): operators D, D^T, A agree with the oracle's sparse products to
-1e-13 relative (summation order differs); PCG theta-solves run at rtol 1e-12, so
-ADMM iterates agree with the SuperLU oracle to 1e-8 relative of max|theta| and
-iteration counts / final rho must match exactly.
+1e-13 relative (summation order differs); PCG theta-solves run at rtol 1e-13 and the
+spectral solve is exact, so ADMM iterates agree with the SuperLU-driven fixtures to
+SURVEY 8(c)'s 1e-9 relative of max|theta| (u to 1e-9 of max(1, max|u|)), the r / s
+norms to 1e-9 relative, and iteration counts / final rho must match exactly. The
+achieved errors go to $MVTV_PARITY_LOG (conftest.log_parity; table in DESIGN.md 2).
 """
 import numpy as np
 import pytest
 
-from conftest import load_golden
+from conftest import load_golden, log_parity
 from oracle import mvtv_oracle as O
 
 mv = pytest.importorskip("multivartv_amd")
 pytestmark = pytest.mark.gpu
 
 RTOL_OP = 1e-13
-RTOL_THETA = 1e-8
+RTOL_THETA = 1e-9
+RTOL_NORM = 1e-9
 
 
 def _rel(a, b):
     return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / max(1e-300, np.max(np.abs(b))))
+
+
+def _relu(a, b):
+    """u's error relative to max(1, max|u_ref|) (u is 0 on most edges of a converged fit)."""
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b))) / max(1.0, np.max(np.abs(b))))
 
 
 SHAPES = [([9], None, "cpp", False), ([7, 5], [0.3, 0.7], "cpp", False), ([6, 6, 6], [0.5, 0.25, 0.125], "cpp", False),
@@ -139,16 +147,23 @@ def test_rcpp_trajectory(name, solver):
     meta, g = load_golden(name)
     _skip_unless_pow2(meta, solver)
     P = _rcpp_problem(meta, g)
+    errs = {}
     for k in (1, 5, 20):
         th, u, rho, st = P.admm(meta["lam"], g["theta0"], u=np.zeros(P.E), rho=meta["rho0"],
                                 fixed_iters=k, pcg_rtol=1e-13, theta_solver=solver)
-        assert _rel(th, g[f"snap{k}"]) <= RTOL_THETA, k
+        errs[f"theta{k}"] = _rel(th, g[f"snap{k}"])
         assert st["iters"] == k
-    assert rho == float(g["fixed_rho"])
-    assert np.max(np.abs(u - g["fixed_u"])) <= RTOL_THETA * max(1.0, np.max(np.abs(g["fixed_u"])))
     hist = g["fixed_hist"][-1]
-    assert st["r_norm"] == pytest.approx(hist[0], rel=1e-6, abs=1e-12)
-    assert st["s_norm"] == pytest.approx(hist[1], rel=1e-6, abs=1e-12)
+    errs["u20"] = _relu(u, g["fixed_u"])
+    errs["r_norm"] = abs(st["r_norm"] - hist[0]) / max(abs(hist[0]), 1e-300)
+    errs["s_norm"] = abs(st["s_norm"] - hist[1]) / max(abs(hist[1]), 1e-300)
+    log_parity(f"trajectory/{name}/{solver}", **errs)
+    for k in (1, 5, 20):
+        assert errs[f"theta{k}"] <= RTOL_THETA, k
+    assert rho == float(g["fixed_rho"])
+    assert errs["u20"] <= RTOL_THETA
+    assert st["r_norm"] == pytest.approx(hist[0], rel=RTOL_NORM, abs=1e-14)
+    assert st["s_norm"] == pytest.approx(hist[1], rel=RTOL_NORM, abs=1e-14)
     assert st["eps_pri"] == pytest.approx(hist[2], rel=1e-10)
     assert st["eps_dual"] == pytest.approx(hist[3], rel=1e-10)
     P.close()
@@ -162,10 +177,11 @@ def test_rcpp_converged(name, solver):
     P = _rcpp_problem(meta, g)
     th, u, rho, st = P.admm(meta["lam"], g["theta0"], u=np.zeros(P.E), rho=meta["rho0"], pcg_rtol=1e-13,
                             theta_solver=solver)
+    log_parity(f"converged/{name}/{solver}", theta=_rel(th, g["theta"]), u=_relu(u, g["u"]), iters=st["iters"])
     assert st["iters"] == meta["iters"]
     assert rho == meta["rho"]
     assert _rel(th, g["theta"]) <= RTOL_THETA
-    assert np.max(np.abs(u - g["u"])) <= RTOL_THETA * max(1.0, np.max(np.abs(g["u"])))
+    assert _relu(u, g["u"]) <= RTOL_THETA
     P.close()
 
 
@@ -182,10 +198,11 @@ def test_rcpp_warm_path_resident(solver):
         st = P.run(lam, pcg_rtol=1e-13, theta_solver=solver)
         assert st["theta_solver"] == (mv.SOLVER_PCG if solver == mv.SOLVER_PCG else mv.SOLVER_SPECTRAL)
         th, u, rho = P.state_get()
+        log_parity(f"warm_path/{k}/{solver}", theta=_rel(th, g[f"theta{k}"]), u=_relu(u, g[f"u{k}"]))
         assert st["iters"] == int(g[f"iters{k}"])
         assert rho == float(g[f"rho{k}"])
         assert _rel(th, g[f"theta{k}"]) <= RTOL_THETA
-        assert np.max(np.abs(u - g[f"u{k}"])) <= RTOL_THETA * max(1.0, np.max(np.abs(g[f"u{k}"])))
+        assert _relu(u, g[f"u{k}"]) <= RTOL_THETA
     P.close()
 
 
@@ -197,10 +214,11 @@ def test_cpp_variant(name, solver):
     P = mv.Problem(meta["m"], g["y"], deltas=meta["deltas"], order=mv.ORDER_CPP, weighted=not meta["unit"])
     th, u, rho, st = P.admm(meta["lam"], g["theta0"], variant=mv.VARIANT_CPP, ymean=meta["ymean"], pcg_rtol=1e-13,
                             theta_solver=solver)
+    log_parity(f"cpp/{name}/{solver}", theta=_rel(th, g["theta"]), u=_relu(u, g["u"]))
     assert st["iters"] == meta["iters"]
     assert rho == meta["rho"]
     assert _rel(th, g["theta"]) <= RTOL_THETA
-    assert np.max(np.abs(u - g["u"])) <= RTOL_THETA * max(1.0, np.max(np.abs(g["u"])))
+    assert _relu(u, g["u"]) <= RTOL_THETA
     P.close()
 
 
@@ -212,5 +230,6 @@ def test_py_config1(name):
     ym = float(g["y"].mean())
     th, _, _, st = P.admm(meta["lam"], np.full(meta["m"][0], ym), variant=mv.VARIANT_PY, ymean=ym,
                           pcg_rtol=1e-13, return_u=False)
+    log_parity(f"py/{name}", theta=_rel(th, g["theta"]))
     assert _rel(th, g["theta"]) <= RTOL_THETA
     P.close()

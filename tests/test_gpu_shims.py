@@ -23,8 +23,8 @@ def test_config1_through_mbs_one_cache_path(name):
     out = solvers.mbs_one(g["data"], g["y"], m, tune=meta["lam"], cache=cache)
     assert set(out) == {"mesh", "theta.hat", "fitted", "data", "y", "eps", "m", "counter"}
     ref = g["theta"]
-    assert np.max(np.abs(out["theta.hat"].ravel() - ref)) <= 1e-8 * np.max(np.abs(ref))
-    assert np.max(np.abs(out["fitted"].ravel() - g["fitted"])) <= 1e-8 * np.max(np.abs(ref))
+    assert np.max(np.abs(out["theta.hat"].ravel() - ref)) <= 1e-9 * np.max(np.abs(ref))
+    assert np.max(np.abs(out["fitted"].ravel() - g["fitted"])) <= 1e-9 * np.max(np.abs(ref))
     cache.problem.close()
 
 
@@ -52,8 +52,8 @@ def test_mbs_path_with_reference_tuners():
     _, _, tuners, _ = O.mbs_path_py(g["data"], g["y"], meta["m"], ftrue=g["ftrue"], ntune=meta["ntune"])
     out = solvers.mbs(g["data"], g["y"], np.array(meta["m"]), ftrue=g["ftrue"], tuners=tuners)
     assert out["minmse.lam"] == pytest.approx(float(g["minlam"]), rel=1e-12)
-    assert out["minmse"] == pytest.approx(float(g["minmse"]), rel=1e-8)
-    np.testing.assert_allclose(out["minmse.fits"]["theta.hat"].ravel(), g["theta"], rtol=1e-8, atol=1e-10)
+    assert out["minmse"] == pytest.approx(float(g["minmse"]), rel=1e-9)
+    np.testing.assert_allclose(out["minmse.fits"]["theta.hat"].ravel(), g["theta"], rtol=1e-9, atol=1e-10)
 
 
 def test_mbs_one_nocache_reference_lambda_max():
@@ -70,8 +70,8 @@ def test_mbs_path_auto_grid():
     meta, g = load_golden("py_2d_mbs_path")
     out = solvers.mbs(g["data"], g["y"], np.array(meta["m"]), ftrue=g["ftrue"], ntune=meta["ntune"])
     assert out["minmse.lam"] == pytest.approx(float(g["minlam"]), rel=1e-12)
-    assert out["minmse"] == pytest.approx(float(g["minmse"]), rel=1e-8)
-    np.testing.assert_allclose(out["minmse.fits"]["theta.hat"].ravel(), g["theta"], rtol=1e-8, atol=1e-10)
+    assert out["minmse"] == pytest.approx(float(g["minmse"]), rel=1e-9)
+    np.testing.assert_allclose(out["minmse.fits"]["theta.hat"].ravel(), g["theta"], rtol=1e-9, atol=1e-10)
 
 
 def test_cpp_host_api(tmp_path):

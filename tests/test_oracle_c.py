@@ -19,8 +19,9 @@ def test_c_oracle_matches_golden(name):
                             pcg_rtol=1e-13)
     assert st["iters"] == meta["iters"]
     assert st["rho"] == meta["rho"]
-    assert np.max(np.abs(th - g["theta"])) <= 1e-8 * np.max(np.abs(g["theta"]))
-    assert np.max(np.abs(u - g["u"])) <= 1e-8 * max(1.0, np.max(np.abs(g["u"])))
+    # SURVEY 8(c)'s 1e-9 (achieved: 1e-13 .. 8e-13)
+    assert np.max(np.abs(th - g["theta"])) <= 1e-9 * np.max(np.abs(g["theta"]))
+    assert np.max(np.abs(u - g["u"])) <= 1e-9 * max(1.0, np.max(np.abs(g["u"])))
 
 
 @pytest.mark.parametrize("name", ["rcpp_1d_200", "rcpp_2d_32", "rcpp_2d_24x40", "rcpp_3d_12", "rcpp_3d_8x8x11",

@@ -1,98 +1,127 @@
-// Achievable HBM bandwidth for the access mixes of the mvtv kernels (fp64, 512^3-sized arrays):
-// read-only, copy (1R1W), and 3R3W (the fused PCG's x, r, p in / x, r', p' out).
+// Achievable HBM bandwidth on this box for the access mixes of the mvtv kernels (fp64, 512^3-sized arrays, 1 GiB
+// each): read-only, copy (1R1W), 3R3W (the fused PCG's x, r, p in / out) and 2R1W. The ceiling the design quotes
+// kernel fractions against, so each mix is run in the form that moves the most bytes:
+//   * 16-B lanes (a double2 per lane), U independent 16-B loads per lane issued before the first store (memory-level
+//     parallelism: U x 16 B x 64 lanes in flight per wave), non-temporal stores (optional), contiguous tiles of
+//     blockDim x U double2 dealt round-robin over a grid sized from the occupancy query (resident workgroups x CUs x
+//     a small multiple);
+//   * a sweep over U in {1, 2, 4, 8}, block size in {256, 512, 1024}, grid multiple in {1, 2, 4} and nt on / off;
+//     every configuration is printed, then the best of each mix as {"best": ...}.
+// The round-4 form (one 8-B element per lane per grid-stride trip, 4096 x 256 threads) is kept as "legacy_*" rows.
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/bin/stream_bench tools/stream_bench.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <string>
 
-#define CK(x)                                                                   \
-    do {                                                                        \
-        hipError_t e_ = (x);                                                    \
-        if (e_ != hipSuccess) {                                                 \
-            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
-            exit(1);                                                            \
-        }                                                                       \
+#define CK(x)                                                                             \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));     \
+            exit(1);                                                                      \
+        }                                                                                 \
     } while (0)
 
-__global__ void k_read(const double* __restrict__ a, size_t n, double* out) {
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ void st(dvec2* p, dvec2 v) {
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+// one tile = blockDim.x * U double2; lane tid touches tile + k * blockDim.x + tid, k < U (coalesced per k)
+template <int U>
+__global__ void k_read(const dvec2* __restrict__ a, size_t n2, double* out) {
+    const size_t tile = size_t(blockDim.x) * U, ntiles = n2 / tile;
+    dvec2 s = {0.0, 0.0};
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const dvec2* pa = a + t * tile + threadIdx.x;
+        dvec2 v[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) v[k] = pa[size_t(k) * blockDim.x];
+#pragma unroll
+        for (int k = 0; k < U; ++k) s += v[k];
+    }
+    if (s.x + s.y == 12345.678) out[0] = s.x;
+}
+
+template <int U, bool NT>
+__global__ void k_copy(const dvec2* __restrict__ a, dvec2* __restrict__ b, size_t n2) {
+    const size_t tile = size_t(blockDim.x) * U, ntiles = n2 / tile;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t o = t * tile + threadIdx.x;
+        dvec2 v[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) v[k] = a[o + size_t(k) * blockDim.x];
+#pragma unroll
+        for (int k = 0; k < U; ++k) st<NT>(b + o + size_t(k) * blockDim.x, v[k] * 1.0000001);
+    }
+}
+
+template <int U, bool NT>
+__global__ void k_2r1w(const dvec2* __restrict__ a, const dvec2* __restrict__ c, dvec2* __restrict__ b, size_t n2) {
+    const size_t tile = size_t(blockDim.x) * U, ntiles = n2 / tile;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t o = t * tile + threadIdx.x;
+        dvec2 v[U], w[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            v[k] = a[o + size_t(k) * blockDim.x];
+            w[k] = c[o + size_t(k) * blockDim.x];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) st<NT>(b + o + size_t(k) * blockDim.x, v[k] + 0.5 * w[k]);
+    }
+}
+
+template <int U, bool NT>
+__global__ void k_3r3w(const dvec2* __restrict__ a, const dvec2* __restrict__ b, const dvec2* __restrict__ c,
+                       dvec2* __restrict__ d, dvec2* __restrict__ e, dvec2* __restrict__ f, size_t n2) {
+    const size_t tile = size_t(blockDim.x) * U, ntiles = n2 / tile;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t o = t * tile + threadIdx.x;
+        dvec2 x[U], y[U], z[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            x[k] = a[o + size_t(k) * blockDim.x];
+            y[k] = b[o + size_t(k) * blockDim.x];
+            z[k] = c[o + size_t(k) * blockDim.x];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const size_t i = o + size_t(k) * blockDim.x;
+            st<NT>(d + i, x[k] + 0.5 * y[k]);
+            st<NT>(e + i, y[k] - 0.25 * z[k]);
+            st<NT>(f + i, z[k] + x[k]);
+        }
+    }
+}
+
+// round 4's form, for comparison
+__global__ void k_legacy_copy(const double* __restrict__ a, double* __restrict__ b, size_t n) {
+    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
+        b[i] = a[i] * 1.0000001;
+}
+__global__ void k_legacy_read(const double* __restrict__ a, size_t n, double* out) {
     double s = 0.0;
     for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
         s += a[i];
     if (s == 12345.678) out[0] = s;
 }
 
-__global__ void k_copy(const double* __restrict__ a, double* __restrict__ b, size_t n) {
-    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-        b[i] = a[i] * 1.0000001;
-}
-
-__global__ void k_3r3w(const double* __restrict__ a, const double* __restrict__ b, const double* __restrict__ c,
-                       double* __restrict__ d, double* __restrict__ e, double* __restrict__ f, size_t n) {
-    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x) {
-        const double x = a[i], y = b[i], z = c[i];
-        d[i] = x + 0.5 * y;
-        e[i] = y - 0.25 * z;
-        f[i] = z + x;
-    }
-}
-
-// 3R3W in z-marching form: a workgroup owns a 64 x 8 column and walks the planes, like k_cg3d
-__global__ void k_3r3w_march(const double* __restrict__ a, const double* __restrict__ b, const double* __restrict__ c,
-                             double* __restrict__ d, double* __restrict__ e, double* __restrict__ f, int m) {
-    const int tx = blockIdx.x % (m / 64), ty = blockIdx.x / (m / 64);
-    const int x = tx * 64 + (threadIdx.x & 63), y = ty * 8 + (threadIdx.x >> 6);
-    const size_t pl = size_t(m) * m;
-    for (int z = 0; z < m; ++z) {
-        const size_t i = z * pl + size_t(y) * m + x;
-        const double xa = a[i], ya = b[i], za = c[i];
-        d[i] = xa + 0.5 * ya;
-        e[i] = ya - 0.25 * za;
-        f[i] = za + xa;
-    }
-}
-
-typedef double dvec2 __attribute__((ext_vector_type(2)));
-
-__global__ void k_copy16(const dvec2* __restrict__ a, dvec2* __restrict__ b, size_t n2) {
-    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n2; i += size_t(gridDim.x) * blockDim.x)
-        b[i] = a[i] * 1.0000001;
-}
-
-__global__ void k_copy8_nt(const double* __restrict__ a, double* __restrict__ b, size_t n) {
-    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n; i += size_t(gridDim.x) * blockDim.x)
-        __builtin_nontemporal_store(a[i] * 1.0000001, b + i);
-}
-
-__global__ void k_copy16_nt(const dvec2* __restrict__ a, dvec2* __restrict__ b, size_t n2) {
-    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n2; i += size_t(gridDim.x) * blockDim.x)
-        __builtin_nontemporal_store(a[i] * 1.0000001, b + i);
-}
-
-__global__ void k_3r3w16(const dvec2* __restrict__ a, const dvec2* __restrict__ b, const dvec2* __restrict__ c,
-                         dvec2* __restrict__ d, dvec2* __restrict__ e, dvec2* __restrict__ f, size_t n2) {
-    for (size_t i = blockIdx.x * size_t(blockDim.x) + threadIdx.x; i < n2; i += size_t(gridDim.x) * blockDim.x) {
-        const dvec2 x = a[i], y = b[i], z = c[i];
-        d[i] = x + 0.5 * y;
-        e[i] = y - 0.25 * z;
-        f[i] = z + x;
-    }
-}
-
-// 8-B lanes, but a contiguous chunk per wave instead of grid-stride (each wave streams 8 KB runs)
-__global__ void k_copy8_chunk(const double* __restrict__ a, double* __restrict__ b, size_t n) {
-    const size_t per = 1024;
-    const size_t nchunk = n / per;
-    for (size_t c = blockIdx.x * size_t(blockDim.x / 64) + threadIdx.x / 64; c < nchunk; c += size_t(gridDim.x) * (blockDim.x / 64)) {
-        const size_t base = c * per + (threadIdx.x & 63);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) b[base + 64 * k] = a[base + 64 * k] * 1.0000001;
-    }
-}
+struct Best {
+    double gbps = 0.0;
+    std::string cfg;
+};
 
 int main() {
-    const int m = 512;
-    const size_t n = size_t(m) * m * m;
+    const size_t n = size_t(512) * 512 * 512, n2 = n / 2;   // every tile size used divides n2
     double* buf[6];
     for (auto& p : buf) {
         CK(hipMalloc(&p, n * sizeof(double)));
@@ -103,9 +132,12 @@ int main() {
     hipEvent_t t0, t1;
     CK(hipEventCreate(&t0));
     CK(hipEventCreate(&t1));
-    const int grid = 256 * 16, block = 256;
-    auto timeit = [&](const char* name, double bytes, auto launch) {
+    int dev = 0, cus = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    auto timeit = [&](const std::string& name, double bytes, auto launch) -> double {
         for (int w = 0; w < 3; ++w) launch();
+        CK(hipGetLastError());
         CK(hipDeviceSynchronize());
         const int reps = 20;
         CK(hipEventRecord(t0));
@@ -114,29 +146,72 @@ int main() {
         CK(hipEventSynchronize(t1));
         float ms = 0;
         CK(hipEventElapsedTime(&ms, t0, t1));
-        const double per = ms / reps;
-        printf("{\"kernel\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f}\n", name, per, bytes / (per * 1e-3) / 1e9);
+        const double per = ms / reps, gbps = bytes / (per * 1e-3) / 1e9;
+        printf("{\"kernel\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f}\n", name.c_str(), per, gbps);
+        fflush(stdout);
+        return gbps;
     };
-    timeit("read_1", 8.0 * n, [&] { hipLaunchKernelGGL(k_read, dim3(grid), dim3(block), 0, 0, buf[0], n, out); });
-    timeit("copy_1r1w", 16.0 * n, [&] { hipLaunchKernelGGL(k_copy, dim3(grid), dim3(block), 0, 0, buf[0], buf[1], n); });
-    timeit("copy16_1r1w", 16.0 * n, [&] {
-        hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(block), 0, 0, (const dvec2*)buf[0], (dvec2*)buf[1], n / 2);
-    });
-    timeit("copy8_nt", 16.0 * n, [&] { hipLaunchKernelGGL(k_copy8_nt, dim3(grid), dim3(block), 0, 0, buf[0], buf[1], n); });
-    timeit("copy16_nt", 16.0 * n, [&] {
-        hipLaunchKernelGGL(k_copy16_nt, dim3(grid), dim3(block), 0, 0, (const dvec2*)buf[0], (dvec2*)buf[1], n / 2);
-    });
-    timeit("copy8_chunk", 16.0 * n, [&] { hipLaunchKernelGGL(k_copy8_chunk, dim3(grid), dim3(block), 0, 0, buf[0], buf[1], n); });
-    timeit("grid_3r3w16", 48.0 * n, [&] {
-        hipLaunchKernelGGL(k_3r3w16, dim3(grid), dim3(block), 0, 0, (const dvec2*)buf[0], (const dvec2*)buf[1],
-                           (const dvec2*)buf[2], (dvec2*)buf[3], (dvec2*)buf[4], (dvec2*)buf[5], n / 2);
-    });
-    timeit("grid_3r3w", 48.0 * n, [&] {
-        hipLaunchKernelGGL(k_3r3w, dim3(grid), dim3(block), 0, 0, buf[0], buf[1], buf[2], buf[3], buf[4], buf[5], n);
-    });
-    timeit("march_3r3w", 48.0 * n, [&] {
-        hipLaunchKernelGGL(k_3r3w_march, dim3((m / 64) * (m / 8)), dim3(512), 0, 0, buf[0], buf[1], buf[2], buf[3],
-                           buf[4], buf[5], m);
-    });
+    Best best_read, best_copy, best_3r3w, best_2r1w;
+    auto keep = [](Best& b, double g, const std::string& c) {
+        if (g > b.gbps) b = Best{g, c};
+    };
+    const dvec2* a2 = reinterpret_cast<const dvec2*>(buf[0]);
+    auto v2 = [&](int i) { return reinterpret_cast<dvec2*>(buf[i]); };
+
+    auto sweep = [&](auto ucst, auto ntcst) {
+        constexpr int U = decltype(ucst)::value;
+        constexpr bool NT = decltype(ntcst)::value;
+        for (int block : {256, 512, 1024}) {
+            int occ_c = 0, occ_3 = 0;
+            CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_c, k_copy<U, NT>, block, 0));
+            CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_3, k_3r3w<U, NT>, block, 0));
+            for (int mult : {1, 2, 4}) {
+                const int gc = std::max(1, occ_c) * cus * mult, g3 = std::max(1, occ_3) * cus * mult;
+                char tag[96];
+                snprintf(tag, sizeof tag, "U%d_b%d_g%dx%d%s", U, block, std::max(1, occ_c) * cus, mult, NT ? "_nt" : "");
+                keep(best_copy,
+                     timeit(std::string("copy16_") + tag, 16.0 * n,
+                            [&] { hipLaunchKernelGGL((k_copy<U, NT>), dim3(gc), dim3(block), 0, 0, a2, v2(1), n2); }),
+                     tag);
+                keep(best_2r1w,
+                     timeit(std::string("2r1w16_") + tag, 24.0 * n, [&] {
+                         hipLaunchKernelGGL((k_2r1w<U, NT>), dim3(gc), dim3(block), 0, 0, a2, v2(2), v2(1), n2);
+                     }),
+                     tag);
+                snprintf(tag, sizeof tag, "U%d_b%d_g%dx%d%s", U, block, std::max(1, occ_3) * cus, mult, NT ? "_nt" : "");
+                keep(best_3r3w,
+                     timeit(std::string("3r3w16_") + tag, 48.0 * n, [&] {
+                         hipLaunchKernelGGL((k_3r3w<U, NT>), dim3(g3), dim3(block), 0, 0, a2, v2(1), v2(2), v2(3), v2(4),
+                                            v2(5), n2);
+                     }),
+                     tag);
+                if (!NT) {
+                    int occ_r = 0;
+                    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_r, k_read<U>, block, 0));
+                    const int gr = std::max(1, occ_r) * cus * mult;
+                    snprintf(tag, sizeof tag, "U%d_b%d_g%dx%d", U, block, std::max(1, occ_r) * cus, mult);
+                    keep(best_read,
+                         timeit(std::string("read16_") + tag, 8.0 * n,
+                                [&] { hipLaunchKernelGGL((k_read<U>), dim3(gr), dim3(block), 0, 0, a2, n2, out); }),
+                         tag);
+                }
+            }
+        }
+    };
+    sweep(std::integral_constant<int, 1>{}, std::false_type{});
+    sweep(std::integral_constant<int, 2>{}, std::false_type{});
+    sweep(std::integral_constant<int, 4>{}, std::false_type{});
+    sweep(std::integral_constant<int, 8>{}, std::false_type{});
+    sweep(std::integral_constant<int, 2>{}, std::true_type{});
+    sweep(std::integral_constant<int, 4>{}, std::true_type{});
+    sweep(std::integral_constant<int, 8>{}, std::true_type{});
+
+    timeit("legacy_read_1", 8.0 * n, [&] { hipLaunchKernelGGL(k_legacy_read, dim3(4096), dim3(256), 0, 0, buf[0], n, out); });
+    timeit("legacy_copy_1r1w", 16.0 * n,
+           [&] { hipLaunchKernelGGL(k_legacy_copy, dim3(4096), dim3(256), 0, 0, buf[0], buf[1], n); });
+    printf("{\"best\": \"read\", \"GBps\": %.1f, \"cfg\": \"%s\"}\n", best_read.gbps, best_read.cfg.c_str());
+    printf("{\"best\": \"copy_1r1w\", \"GBps\": %.1f, \"cfg\": \"%s\"}\n", best_copy.gbps, best_copy.cfg.c_str());
+    printf("{\"best\": \"2r1w\", \"GBps\": %.1f, \"cfg\": \"%s\"}\n", best_2r1w.gbps, best_2r1w.cfg.c_str());
+    printf("{\"best\": \"3r3w\", \"GBps\": %.1f, \"cfg\": \"%s\"}\n", best_3r3w.gbps, best_3r3w.cfg.c_str());
     return 0;
 }
