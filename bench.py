@@ -235,12 +235,20 @@ def _cpu_model():
 
 
 def _usable_cores():
-    """The CPUs this process may run on (its affinity mask): the baseline's OpenMP threads and scipy.fft workers.
-    os.cpu_count() and OMP_NUM_THREADS are reported beside it, not used."""
+    """The CPUs this process can actually use: its affinity mask, capped by the cgroup's CPU-time quota (cpu.max:
+    on the GPU box the mask shows all 256 host CPUs while the quota grants 16; 256 OpenMP threads under a 16-CPU
+    quota would be throttled, not faster). The baseline's OpenMP threads and scipy.fft workers; os.cpu_count()
+    and OMP_NUM_THREADS are reported beside it, not used."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = _cgroup_cpu_max()
+    if q:
+        quota, _, period = q.partition(" ")
+        if quota not in ("", "max") and period:
+            n = min(n, max(1, int(float(quota) / float(period))))
+    return n
 
 
 def _cgroup_cpu_max():
@@ -287,7 +295,7 @@ def cpu_baseline(m, lam, pcg_iters, planes, full=False):
     dims = lambda sub: "x".join(map(str, sub))   # noqa: E731
     where_s = "the whole mesh" if sc_spec == 1.0 else f"a {dims(sub_s)} slab, rate scaled by {sc_spec:.0f}"
     return dict(value=1.0 / (t_spec * sc_spec), unit="iters/s", cores=ncores, kind="port",
-                cpu_model=_cpu_model(), affinity_cpus=ncores, host_cpus=os.cpu_count(),
+                cpu_model=_cpu_model(), affinity_cpus=len(os.sched_getaffinity(0)), host_cpus=os.cpu_count(),
                 omp_num_threads=os.environ.get("OMP_NUM_THREADS"), cgroup_cpu_max=_cgroup_cpu_max(),
                 algorithm="spectral",
                 sample=(f"1 ADMM iteration (variant B) of the same towers problem on {where_s}, {ncores} threads: "

@@ -45,7 +45,7 @@ int popcount(int x) { return __builtin_popcount(unsigned(x)); }
 // place, frees everything the probe allocated and clears HIP's error state. MVTV_ZPICK=0 turns it off
 // (MVTV_ZPICK=fail: allocate, then take the failure path; tests/test_gpu_zpick.py).
 // The fused 3-D kernel may skip the twin block (mvtv_internal.h twin_block): one GPU, equal twin weights and state.
-// MVTV_TWIN=0 (probe builds) keeps both.
+// MVTV_TWIN_OFF=1 (probe builds) keeps both.
 bool twin_ready(const mvtv_problem* P) {
     if (P->slab || !P->twin_ok || probe_env("MVTV_TWIN_OFF")) return false;
     if (!((P->g.p == 3 && P->f3d) || (P->g.p == 4 && P->f4d))) return false;
@@ -1092,6 +1092,21 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
     }
     // the twin blocks are skipped by the fused kernels and filled from their group's first block when the run ends
     const bool twin = (fused || fused4) && twin_ready(P);
+    // an early return (MVTV_TRY / HIP_TRY) after twin-skipping iterations must not leave a stale twin block behind
+    // twin_ok: fill the twins of both edge buffers (whichever holds the state), best effort; the normal exits
+    // fill them themselves and disarm
+    struct TwinGuard {
+        mvtv_problem* P;
+        bool armed;
+        ~TwinGuard() {
+            if (!armed) return;
+            (void)fill_twins(P->g, P->order, P->stream, P->edges);
+            if (P->edges2) (void)fill_twins(P->g, P->order, P->stream, P->edges2);
+            if (P->edges3) (void)fill_twins(P->g, P->order, P->stream, P->edges3);
+            (void)hipStreamSynchronize(P->stream);
+            (void)hipGetLastError();
+        }
+    } twin_guard{P, twin};
     if (P->timing && (fused || fused4)) P->twin_timed = twin;
     if (fused && spectral && nbuf == 2 && !P->zpicked) MVTV_TRY(pick_zpair(P, track_theta, twin));
     double dtheta = 0.0;
@@ -1140,8 +1155,10 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         const uint32_t m0 = (!P->slab && march_ok(P->g)) ? P->g.m[2] : P->g.m[0];
         const bool fold_path = fused ? (P->g.p == 2 || P->g.p == 3)
                                      : (P->g.p == 4 && P->e3d && P->g4 != nullptr && gather4_ok(P->g));   // two-pass 4-D
+        // on k_march meshes the folded first pass runs along dim 2 at stride m0 * m1, which must be a power of two too
+        const uint64_t fold_stride = (!P->slab && march_ok(P->g)) ? uint64_t(P->g.m[0]) * P->g.m[1] : 1;
         const bool fold = fold_path && variant == MVTV_VARIANT_RCPP && m0 >= 8 && m0 <= 4096 &&
-                          (m0 & (m0 - 1)) == 0 &&
+                          (m0 & (m0 - 1)) == 0 && (fold_stride & (fold_stride - 1)) == 0 &&
                           !probe_env("MVTV_FOLD_OFF") && !probe_env("MVTV_DCT_LDS") && !probe_env("MVTV_DCT_MID");
         auto enqueue = [&](int j) -> mvtv_status {
             double* gp = gbuf[j & 1];
@@ -1226,7 +1243,8 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
             const std::vector<const void*> key = {P->theta, P->oty, P->ga, P->thold, gbuf[0], gbuf[1], ebuf[0], ebuf[1],
                                                   reinterpret_cast<const void*>(uintptr_t(fold)),
                                                   reinterpret_cast<const void*>(uintptr_t(track_theta)),
-                                                  reinterpret_cast<const void*>(uintptr_t(fused))};
+                                                  reinterpret_cast<const void*>(uintptr_t(fused)),
+                                                  reinterpret_cast<const void*>(uintptr_t(twin))};
             auto it = std::find_if(P->graphs.begin(), P->graphs.end(), [&](const auto& lg) { return lg.key == key; });
             if (it == P->graphs.end()) {
                 // capture iterations 1 and 2; any failure leaves stream launches for this key (best effort)
@@ -1282,6 +1300,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         } else if (pingpong && (it_done & 1)) {
             std::swap(P->edges, P->edges2);
         }
+        twin_guard.armed = false;
         if (twin) HIP_TRY(fill_twins(P->g, P->order, P->stream, P->edges));
         if (it_done > 0) P->edge_mode = U_FROM_Z;
         if (it_done > 0) P->t_z = c.t_z;
@@ -1473,6 +1492,7 @@ mvtv_status mvtv_admm_run(mvtv_problem* P, const mvtv_admm_opts* opts_in, double
         }
     }
     P->harvest();   // the stream is idle here (last iteration synchronised)
+    twin_guard.armed = false;
     if (twin) {
         HIP_TRY(fill_twins(P->g, P->order, P->stream, P->edges));
         HIP_TRY(hipStreamSynchronize(P->stream));

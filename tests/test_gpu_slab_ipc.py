@@ -11,6 +11,7 @@ the rendezvous segment's name; the reference theta goes to them through a file."
 import ctypes as C
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -31,23 +32,31 @@ def _fold_mask(m):
     return (np.arange(int(np.prod(m))) % 5 != 2).astype(np.float64)
 
 
-def _rank_main(rank, world, port, q, m, lam, iters, ref_path, weighted, fail_rank):
+def _say(rank, msg):
+    print(f"[ipc rank {rank}] {msg}", file=sys.stderr, flush=True)
+
+
+def _rank_main(rank, world, port, q, m, lam, iters, ref_path, weighted, fail_rank, t0):
+    import faulthandler
+    faulthandler.dump_traceback_later(150, exit=False)   # a stuck rank shows where it is
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    _say(rank, f"up, mesh {m}")
     try:
         from multivartv_amd import _lib, slab
-        y = towers(m)
         deltas = [(1.0 + 2e-4) / v for v in m]
         b = slab.plane_bounds(m[-1], world)
         pl = int(np.prod(m[:-1]))
         own = slice(int(b[rank]) * pl, int(b[rank + 1]) * pl)
-        w = _fold_mask(m) if weighted else None
+        y = towers(m, start=own.start, count=own.stop - own.start)   # this rank's planes only
+        w = _fold_mask(m)[own] if weighted else None
         oty = y if w is None else w * y
-        t0 = float(y.mean()) if w is None else float(y[w > 0].mean())
         comm = slab.Comm.ipc(0)
-        S = slab.SlabADMM(m, oty[own], deltas, t0, comm, device=0, w_owned=None if w is None else w[own])
+        _say(rank, "ipc group created")
+        S = slab.SlabADMM(m, oty, deltas, t0, comm, device=0, w_owned=w)
         del y, oty
+        _say(rank, "slab problem created")
         if rank == fail_rank:   # variant A is refused before any collective: the rank aborts the group
             o = _lib.default_opts(_lib.VARIANT_CPP)
             st = _lib.AdmmStats()
@@ -60,6 +69,7 @@ def _rank_main(rank, world, port, q, m, lam, iters, ref_path, weighted, fail_ran
             except Exception as e:  # noqa: BLE001
                 q.put((rank, None, None, repr(e)))
                 return
+            _say(rank, f"run done: {st['iters']} iterations")
             th = S.theta_owned()
             ref = np.load(ref_path, mmap_mode="r")[own]
             q.put((rank, st, float(np.max(np.abs(th - ref))), None))
@@ -71,15 +81,17 @@ def _rank_main(rank, world, port, q, m, lam, iters, ref_path, weighted, fail_ran
         dist.destroy_process_group()
 
 
-def _run_group(world, m, lam, iters, ref_path, weighted=False, fail_rank=-1, env=None):
+def _run_group(world, m, lam, iters, ref_path, t0, weighted=False, fail_rank=-1, env=None):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    old = {k: os.environ.get(k) for k in (env or {})}
-    os.environ.update(env or {})
+    env = dict(env or {})
+    env.setdefault("MVTV_IPC_TIMEOUT", "90")   # a transport wait that never ends fails the test instead
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
-        procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, m, lam, iters, ref_path, weighted, fail_rank))
+        procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, m, lam, iters, ref_path, weighted, fail_rank, t0))
                  for r in range(world)]
         for p in procs:
             p.start()
@@ -106,36 +118,17 @@ def _one_gpu(m, lam, iters, weighted=False):
         P.state_set(np.full(y.size, t0), None, lam / 5.0)
         st = P.run(lam, fixed_iters=iters, **kw)
         th, _, rho = P.state_get(want_u=False)
-    return th, rho, st
-
-
-@pytest.mark.parametrize("m,world,iters", [([512, 512, 512], 2, 2), ([128, 128, 128, 128], 4, 2),
-                                           ([64, 48, 40], 3, 6), ([96, 80, 33], 2, 0)],
-                         ids=["metric_512cubed_2proc", "config5_128_4d_4proc", "3d_3proc", "tolerance_2proc"])
-def test_slab_processes_match_one_gpu(tmp_path, m, world, iters):
-    lam = 1.0 if iters else 0.4
-    th, rho, st = _one_gpu(m, lam, iters)
-    ref = tmp_path / "theta.npy"
-    np.save(ref, th)
-    scale = float(np.max(np.abs(th)))
-    del th
-    res = _run_group(world, m, lam, iters, str(ref))
-    for rank, o, err, exc in res:
-        assert exc is None, (rank, exc)
-        assert o["iters"] == st["iters"] and o["rho"] == rho, (rank, o["iters"], st["iters"])
-        assert o["r_norm"] == pytest.approx(st["r_norm"], rel=1e-9)
-        assert o["s_norm"] == pytest.approx(st["s_norm"], rel=1e-9)
-        assert err <= 1e-11 * scale, (rank, err / scale)
+    return th, rho, st, t0
 
 
 def test_slab_processes_weighted_fold(tmp_path):
     """W != I: the distributed PCG-spectral theta-solve (a halo of the search direction and an all-reduce per dot
     product, every one across processes) against the one-GPU PCG-spectral run; iterations and rho exact."""
     m, world, iters, lam = [32, 24, 40], 2, 8, 0.6
-    th, rho, st = _one_gpu(m, lam, iters, weighted=True)
+    th, rho, st, t0 = _one_gpu(m, lam, iters, weighted=True)
     ref = tmp_path / "theta.npy"
     np.save(ref, th)
-    res = _run_group(world, m, lam, iters, str(ref), weighted=True)
+    res = _run_group(world, m, lam, iters, str(ref), t0, weighted=True)
     for rank, o, err, exc in res:
         assert exc is None, (rank, exc)
         assert o["iters"] == iters and o["rho"] == rho
@@ -149,7 +142,26 @@ def test_failing_rank_ends_its_peers(tmp_path):
     m = [32, 32, 16]
     ref = tmp_path / "theta.npy"
     np.save(ref, np.zeros(int(np.prod(m))))
-    res = _run_group(2, m, 1.0, 3, str(ref), fail_rank=1, env={"MVTV_IPC_TIMEOUT": "100"})
+    res = _run_group(2, m, 1.0, 3, str(ref), 0.0, fail_rank=1)
     from multivartv_amd import _lib
     assert res[1][1]["status"] == _lib.MVTV_BAD_ARG
     assert res[0][3] is not None and "aborted" in res[0][3]
+
+
+@pytest.mark.parametrize("m,world,iters", [([64, 48, 40], 3, 6), ([96, 80, 33], 2, 0), ([128, 128, 128, 128], 4, 2),
+                                           ([512, 512, 512], 2, 2)],
+                         ids=["3d_3proc", "tolerance_2proc", "config5_128_4d_4proc", "metric_512cubed_2proc"])
+def test_slab_processes_match_one_gpu(tmp_path, m, world, iters):
+    lam = 1.0 if iters else 0.4
+    th, rho, st, t0 = _one_gpu(m, lam, iters)
+    ref = tmp_path / "theta.npy"
+    np.save(ref, th)
+    scale = float(np.max(np.abs(th)))
+    del th
+    res = _run_group(world, m, lam, iters, str(ref), t0)
+    for rank, o, err, exc in res:
+        assert exc is None, (rank, exc)
+        assert o["iters"] == st["iters"] and o["rho"] == rho, (rank, o["iters"], st["iters"])
+        assert o["r_norm"] == pytest.approx(st["r_norm"], rel=1e-9)
+        assert o["s_norm"] == pytest.approx(st["s_norm"], rel=1e-9)
+        assert err <= 1e-11 * scale, (rank, err / scale)
