@@ -787,6 +787,126 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
 }
 
 // =============================================================================================
+// Streamed strided passes (d > 0, FWD or INV, 16-line tiles, every tile full): k_dct8's tile work with the
+// next tile's loads in flight during this tile's FFT. A grid of resident workgroups walks the tiles
+// (blockIdx.x, + gridDim.x, ...); a thread holds this tile's 8 inputs and the next tile's 8 (32 more VGPRs:
+// FWD 78 -> ~110, INV 94 -> ~126, still 4 waves per SIMD at 512 threads) and every barrier orders LDS only
+// (lds_barrier), so the prefetch is never waited for before its tile. In k_dct8 a workgroup's loads are all
+// in flight only before its first stage, and with two workgroups per CU (LDS) both may be computing.
+template <int L, int MODE>
+__global__ __launch_bounds__((spec8::ShapeK<L, 16>::NT), 4) void k_dct8s(const SpecArgs a) {
+    using S = spec8::ShapeK<L, 16>;
+    static_assert(MODE == SPEC_FWD || MODE == SPEC_INV, "forward or inverse passes");
+    if (a.skip && *a.skip) return;
+    if (a.ctl && a.ctl->done) return;
+    constexpr int M = S::M, TPL = S::TPL, NCL = S::NCL, R0 = S::R0;
+    __shared__ double2 buf[NCL * S::LP];
+    int t = threadIdx.x;
+    int j = t / NCL, c = t % NCL;
+    double2* X = buf + c * S::LP;
+    int cx = c & 7;
+    const uint32_t ntiles = a.nlines / 16u;
+    // (line 2c of tile tt, position k) -> global offset; lines 2c, 2c + 1 are adjacent words
+    auto gaddr = [&](uint32_t tt, uint32_t k) -> uint32_t {
+        const uint32_t q = tt * 16u + uint32_t(2 * c);
+        return (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (k << a.ls);
+    };
+    // FWD: the first stage's inputs (Makhoul positions); INV: the coefficient pairs (k, M - k)
+    auto load = [&](uint32_t tt, double2* v) {
+        if constexpr (MODE == SPEC_FWD) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int n = stage_in_pos<L, R0>(j, i);
+                const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
+                v[i] = ldnt2(a.in + gaddr(tt, k));
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = j + s * TPL;
+                v[2 * s] = ldnt2(a.in + gaddr(tt, uint32_t(k)));
+                v[2 * s + 1] = ldnt2(a.in + gaddr(tt, uint32_t(k ? M - k : M / 2)));
+            }
+        }
+    };
+    double2 nx[8];
+    uint32_t tt = blockIdx.x;
+    if (tt < ntiles) load(tt, nx);
+    for (; tt < ntiles; tt += gridDim.x) {
+        // per-thread offsets re-derived from an opaque copy of the thread index every tile, and the twiddle
+        // tables through opaque pointers (hoisted out of the loop they stay live beside the prefetch and the
+        // kernel needs ~166 VGPRs: one workgroup per CU)
+        const double2* tw = a.tw;
+        asm volatile("" : "+s"(tw));
+        asm volatile("" : "+v"(t));
+        j = t / NCL;
+        c = t % NCL;
+        X = buf + c * S::LP;
+        cx = c & 7;
+        double2 z[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] = nx[i];
+        if (tt + gridDim.x < ntiles) load(tt + gridDim.x, nx);
+        if constexpr (MODE == SPEC_FWD) {
+            // its first barrier also ends the previous tile's reads of X
+            stages_from<L, R0, 1, false, false, true>(z, j, X, cx, tw);   // natural-order spectrum in X
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = j + s * TPL;
+                const int ka = k, kb = k ? M - k : M / 2;
+                const double2 Z1 = X[spec8::slot(ka, cx)], Z2 = X[spec8::slot(kb, cx)];
+                const double2 q1 = a.twq[ka], q2 = a.twq[kb];
+                double2 Xk, Xmk;
+                if (k == 0) {
+                    Xk = make_double2(q1.x * Z1.x, q1.x * Z1.y);
+                    Xmk = make_double2(q2.x * Z2.x, q2.x * Z2.y);
+                } else {
+                    const double2 Ap = make_double2(0.5 * (Z1.x + Z2.x), 0.5 * (Z1.y - Z2.y));
+                    const double2 Bp = make_double2(0.5 * (Z1.y + Z2.y), -0.5 * (Z1.x - Z2.x));
+                    Xk = make_double2(q1.x * Ap.x - q1.y * Ap.y, q1.x * Bp.x - q1.y * Bp.y);
+                    Xmk = make_double2(q2.x * Ap.x + q2.y * Ap.y, q2.x * Bp.x + q2.y * Bp.y);
+                }
+                stnt2(a.out + gaddr(tt, uint32_t(ka)), Xk);
+                stnt2(a.out + gaddr(tt, uint32_t(kb)), Xmk);
+            }
+        } else {
+            lds_barrier();   // the previous tile's reads of X are done
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = j + s * TPL;
+                const int ka = k, kb = k ? M - k : M / 2;
+                const double2 Xk = z[2 * s], Xmk = z[2 * s + 1];
+                const double2 q1 = cconj(a.twq[ka]), q2 = cconj(a.twq[kb]);
+                if (k == 0) {
+                    const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xmk.x));
+                    const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xmk.y));
+                    X[spec8::slot(0, cx)] = Xk;
+                    X[spec8::slot(M / 2, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+                } else {
+                    const double2 va1 = cmul(q1, make_double2(Xk.x, -Xmk.x));
+                    const double2 vb1 = cmul(q1, make_double2(Xk.y, -Xmk.y));
+                    const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xk.x));
+                    const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xk.y));
+                    X[spec8::slot(ka, cx)] = make_double2(va1.x - vb1.y, va1.y + vb1.x);
+                    X[spec8::slot(kb, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
+                }
+            }
+            lds_barrier();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, R0>(j, i), cx)];
+            stages_from<L, R0, 1, true, true, true>(z, j, X, cx, tw);
+            using LS = LastStage<L>;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int n = stage_out_pos<L, LS::R, LS::NS>(j, i);
+                const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
+                stnt2(a.out + gaddr(tt, k), z[i]);
+            }
+        }
+    }
+}
+
+// =============================================================================================
 // Two in-plane passes in one launch (m0 = m1 = 2^L, L <= 7): a workgroup owns one (dim 0, dim 1) plane,
 // 128 KB at L = 7, and keeps it on chip between the two 1-D transforms, so the spectral solve of a 4-D
 // 128^4 mesh makes 5 passes over HBM instead of 7 (3 instead of 5 at 128^3). NCL = M / 2 complex lines x
@@ -3134,9 +3254,37 @@ static bool try_tile(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb, 
 // contiguous runs, so the 4 tiles of a 128-B row share one L2. 1024^2: 8355 -> 9650 ADMM it/s (d = 0
 // passes 17.5 -> 14.8 us, strided 18.7 -> 11.8 us); 2048^2: 4797 -> 4862 (profiles/r02/v17_dct_tiles).
 // Probe builds: MVTV_DCT_T0 / _T1 set the d = 0 / d > 0 tile, MVTV_DCT_XCD=0/1 the XCD runs.
+// k_dct8s (streamed strided passes): resident workgroups x CUs, at most one per tile
+template <int L, int MODE>
+static void launch_dct8s(SpecArgs& a, hipStream_t s) {
+    static const uint32_t resident = [] {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dct8s<L, MODE>, spec8::ShapeK<L, 16>::NT, 0) !=
+                hipSuccess)
+            return 512u;
+        return uint32_t(std::max(1, cus) * std::max(1, per_cu));
+    }();
+    a.tq = 16;
+    const uint32_t ntiles = a.nlines / 16u;
+    klaunch(k_dct8s<L, MODE>, dim3(std::min(ntiles, resident)), dim3(spec8::ShapeK<L, 16>::NT), 0, s, a);
+}
+
 template <int L>
 static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
     using S = spec8::Shape<L>;
+    // strided forward / inverse passes of full 16-line tiles over many tiles: the streamed form (probe builds:
+    // MVTV_DCT_STREAM=1)
+    if constexpr (L >= 6 && L <= 9) {
+        static const bool stream = probe_env("MVTV_DCT_STREAM") != nullptr;
+        if (stream && !d0 && !formb && (mode == SPEC_FWD || mode == SPEC_INV) && a.stride >= 16u &&
+            a.nlines % 16u == 0u && a.nlines / 16u >= 2048u && !a.pf.mode) {
+            if (mode == SPEC_FWD) launch_dct8s<L, SPEC_FWD>(a, s);
+            else launch_dct8s<L, SPEC_INV>(a, s);
+            return;
+        }
+    }
     constexpr int TMIN = tile_ok<L>(2) ? 2 : (tile_ok<L>(4) ? 4 : (tile_ok<L>(8) ? 8 : 16));
     int want = S::TQ;
     bool xcd_def = false;

@@ -10,4 +10,14 @@ rc=$?; tail -12 $O/ipc.log
 if [ $rc -ne 0 ]; then echo "ipc tests rc=$rc: stopping"; exit $rc; fi
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; exit 1; }
 timeout -k 10 300 python bench.py --gpus 2 --mode slab --steps 10 --warmup 2 > $O/bench_slab2.json 2> $O/bench_slab2.err
-echo "slab2 rc=$?"
+rc=$?; echo "slab2 rc=$rc"; tail -3 $O/bench_slab2.err
+if [ $rc -gt 1 ]; then exit $rc; fi
+# probe A/B: the in-plane pass pairs per chunk of dim-2 planes (MVTV_ZCHUNK), interleaved, one process each
+export MVTV_LIB_PATH=$GRAFT_REPO_ROOT/multivartv_amd/lib_probe/libmvtv.so
+for rep in 1 2; do
+  for zc in 0 32 64 128; do
+    f=$O/zc$zc.$rep
+    MVTV_ZCHUNK=$zc timeout -k 10 200 python bench.py --no-cpu --pcg-steps 0 --steps 30 --warmup 5 > $f.json 2> $f.err || { tail -5 $f.err; exit 1; }
+    python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2],d['value'],{k:v['avg_ms'] for k,v in d.get('kernels',{}).items()})" $f.json "zchunk=$zc rep $rep"
+  done
+done
