@@ -2641,6 +2641,167 @@ __global__ __launch_bounds__((tri::Shape<L, SEG, TQL>::NT)) void k_tri(const Spe
         __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + (uint32_t(i) << a.ls));
 }
 
+// k_tri_s: k_tri<L, 32, 64> over resident workgroups that walk the tiles (blockIdx.x, + gridDim.x, ...), the first
+// PF rows of the next tile's segments loaded during this tile's solve (PF VGPRs more: 106 -> ~122 at 1024
+// threads), every barrier ordering LDS only so the prefetch is not waited for. k_tri's one workgroup per CU
+// (99 KB of LDS) otherwise has no loads in flight while it computes the line constants and the interface system.
+namespace tri {
+// prefetched rows of a 32-row segment (1024-thread workgroups at L = 9 have 128 VGPRs: 8 fit without spills)
+template <int L>
+constexpr int pf_rows() { return L >= 9 ? 8 : 16; }
+}
+template <int L>
+__global__ __launch_bounds__((tri::Shape<L, 32, 64>::NT)) void k_tri_s(const SpecArgs a) {
+    constexpr int SEG = 32, TQ = 64, PF = tri::pf_rows<L>();
+    using S = tri::Shape<L, SEG, TQ>;
+    constexpr int NSEG = S::NSEG;
+    double sigma = a.sigma;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+    }
+    __shared__ double t_id[SEG][TQ], t_e[SEG][TQ], t_h[SEG][TQ], t_k[SEG][TQ];
+    __shared__ double s_a[TQ];
+    __shared__ double s_u[NSEG][TQ], s_v[NSEG][TQ], s_bu[NSEG][TQ], s_bv[NSEG][TQ];
+    int t = threadIdx.x, c = t % TQ, sj = t / TQ;
+    const uint32_t ntiles = a.nlines / uint32_t(TQ);
+    auto base_of = [&](uint32_t tt) -> uint32_t {
+        const uint32_t q = tt * uint32_t(TQ) + uint32_t(c);
+        return (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (uint32_t(sj * SEG) << a.ls);
+    };
+    double nx[PF];
+    uint32_t tt = blockIdx.x;
+    if (tt < ntiles) {
+        const uint32_t b = base_of(tt);
+#pragma unroll
+        for (int i = 0; i < PF; ++i) nx[i] = __builtin_nontemporal_load(a.in + b + (uint32_t(i) << a.ls));
+    }
+    for (; tt < ntiles; tt += gridDim.x) {
+        asm volatile("" : "+v"(t));   // per-thread offsets re-derived every tile (hoisted, they spill)
+        c = t % TQ;
+        sj = t / TQ;
+        const uint32_t base = base_of(tt);
+        // eigenvalue loads first (the constants wait for them alone), then this tile's remaining rows, then the
+        // next tile's first rows (loads complete in order)
+        double lamv[kMaxDims] = {0, 0, 0, 0};
+        if (t < TQ) {
+            uint32_t rest = a.q_off + tt * uint32_t(TQ) + uint32_t(c);
+            const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
+            for (int jj = 0; jj < a.p; ++jj) {
+                if (jj == a.d) continue;
+                const uint32_t qq = (jj < jlast) ? a.fd[jj].div(rest) : 0u;
+                lamv[jj] = a.lam[a.lam_off[jj] + (rest - qq * a.m[jj])];
+                rest = qq;
+            }
+        }
+        double g[SEG];
+#pragma unroll
+        for (int i = 0; i < PF; ++i) g[i] = nx[i];
+#pragma unroll
+        for (int i = PF; i < SEG; ++i) g[i] = __builtin_nontemporal_load(a.in + base + (uint32_t(i) << a.ls));
+        if (tt + gridDim.x < ntiles) {
+            const uint32_t bn = base_of(tt + gridDim.x);
+#pragma unroll
+            for (int i = 0; i < PF; ++i) nx[i] = __builtin_nontemporal_load(a.in + bn + (uint32_t(i) << a.ls));
+        }
+        if (t < TQ) {
+            double c0 = a.w0, c1 = 0.0;
+            for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
+                if (a.cS[Sm] == 0.0) continue;
+                double prod = sigma * a.cS[Sm];
+                for (int jj = 0; jj < a.p; ++jj)
+                    if (jj != a.d && ((Sm >> jj) & 1)) prod *= lamv[jj];
+                if ((Sm >> a.d) & 1) c1 += prod;
+                else c0 += prod;
+            }
+            const double A = -c1, B = c0 + 2.0 * c1;
+            double e = 0.0, h = 1.0;
+#pragma unroll 1
+            for (int i = 0; i < SEG; ++i) {
+                const double id = 1.0 / (B - A * e);
+                e = A * id;
+                h = -A * h * id;
+                t_id[i][c] = id;
+                t_e[i][c] = e;
+                t_h[i][c] = h;
+            }
+            double H = t_h[SEG - 1][c], K = -t_e[SEG - 1][c];
+            t_k[SEG - 1][c] = K;
+#pragma unroll 1
+            for (int i = SEG - 2; i >= 0; --i) {
+                const double ei = t_e[i][c];
+                H = t_h[i][c] - ei * H;
+                K = -ei * K;
+                t_h[i][c] = H;
+                t_k[i][c] = K;
+            }
+            s_a[c] = A;
+        }
+        lds_barrier();
+        {
+            const double A = s_a[c];
+            g[0] *= t_id[0][c];
+#pragma unroll
+            for (int i = 1; i < SEG; ++i) g[i] = (g[i] - A * g[i - 1]) * t_id[i][c];
+#pragma unroll
+            for (int i = SEG - 2; i >= 0; --i) g[i] -= t_e[i][c] * g[i + 1];
+            s_u[sj][c] = g[0];
+            s_v[sj][c] = g[SEG - 1];
+        }
+        lds_barrier();
+        if (t < TQ) {
+            const double H0 = t_h[0][c], K0 = t_k[0][c], H1 = t_h[SEG - 1][c], K1 = t_k[SEG - 1][c];
+            double av = 0.0, bv = 0.0;
+#pragma unroll 1
+            for (int jb = 0; jb < NSEG - 1; ++jb) {
+                const double g0 = s_u[jb][c], g1 = s_v[jb][c];
+                double au, bu;
+                if (jb == 0) {
+                    const double id = 1.0 / (1.0 - H0);
+                    au = g0 * id;
+                    bu = K0 * id;
+                    av = g1 + H1 * au;
+                    bv = K1 + H1 * bu;
+                } else {
+                    const double id = 1.0 / (1.0 - H0 * bv);
+                    au = (g0 + H0 * av) * id;
+                    bu = K0 * id;
+                    const double nav = g1 + H1 * av + H1 * bv * au;
+                    bv = K1 + H1 * bv * bu;
+                    av = nav;
+                }
+                s_u[jb][c] = au;
+                s_bu[jb][c] = bu;
+                s_v[jb][c] = av;
+                s_bv[jb][c] = bv;
+            }
+            constexpr int J = NSEG - 1;
+            const double a11 = 1.0 - H0 * bv, a12 = -K0, a21 = -H1 * bv, a22 = 1.0 - K1;
+            const double b1 = s_u[J][c] + H0 * av, b2 = s_v[J][c] + H1 * av;
+            const double idet = 1.0 / (a11 * a22 - a12 * a21);
+            double u = (b1 * a22 - a12 * b2) * idet;
+            s_u[J][c] = u;
+            s_v[J][c] = (a11 * b2 - a21 * b1) * idet;
+#pragma unroll 1
+            for (int jb = J - 1; jb >= 0; --jb) {
+                const double un = u;
+                u = s_u[jb][c] + s_bu[jb][c] * un;
+                s_v[jb][c] = s_v[jb][c] + s_bv[jb][c] * un;
+                s_u[jb][c] = u;
+            }
+        }
+        lds_barrier();
+        const double Lj = sj == 0 ? s_u[0][c] : s_v[sj - 1][c];
+        const double Rj = sj == NSEG - 1 ? s_v[NSEG - 1][c] : s_u[sj + 1][c];
+        const double sc = a.inv_n * double(S::M);
+#pragma unroll
+        for (int i = 0; i < SEG; ++i)
+            __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + (uint32_t(i) << a.ls));
+        lds_barrier();   // every read of this tile's constants and interface values before the next tile's writes
+    }
+}
+
 // k_trig: the same solve for any line length m = NSEG * s (segment length s <= 32 chosen at launch,
 // NSEG <= 64) and any line stride (FastDiv addressing): the last-dimension pass of the mixed-radix
 // meshes. Rows past s in the fixed-size register arrays are predicated off.
@@ -3159,6 +3320,21 @@ static void launch_tri(SpecArgs& a, hipStream_t s, int tq) {
             launch_tri_seg<16, 32>(a, s);
         } else if (tqw == 64 && seg == 16 && a.stride >= 64u && a.L >= 7 && a.L <= 9 && a.nlines / 64u >= 256u) {
             a.tq = 64;
+            static const bool tri_stream = probe_env("MVTV_TRI_STREAM") != nullptr;
+            if (tri_stream && a.nlines % 64u == 0u && a.nlines / 64u >= 1024u) {
+                static const uint32_t cus = [] {
+                    int dev = 0, n = 0;
+                    if (hipGetDevice(&dev) != hipSuccess ||
+                        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                        return 256u;
+                    return uint32_t(std::max(1, n));
+                }();
+                const dim3 grid(std::min(a.nlines / 64u, cus));   // one 99-KB workgroup per CU
+                if (a.L == 7) klaunch(k_tri_s<7>, grid, dim3(tri::Shape<7, 32, 64>::NT), 0, s, a);
+                else if (a.L == 8) klaunch(k_tri_s<8>, grid, dim3(tri::Shape<8, 32, 64>::NT), 0, s, a);
+                else klaunch(k_tri_s<9>, grid, dim3(tri::Shape<9, 32, 64>::NT), 0, s, a);
+                return;
+            }
             const dim3 grid((a.nlines + 63u) / 64u);
             if (a.L == 7) klaunch(k_tri<7, 32, 64>, grid, dim3(tri::Shape<7, 32, 64>::NT), 0, s, a);
             else if (a.L == 8) klaunch(k_tri<8, 32, 64>, grid, dim3(tri::Shape<8, 32, 64>::NT), 0, s, a);

@@ -124,7 +124,7 @@ def _one_gpu(m, lam, iters, weighted=False):
 def test_slab_processes_weighted_fold(tmp_path):
     """W != I: the distributed PCG-spectral theta-solve (a halo of the search direction and an all-reduce per dot
     product, every one across processes) against the one-GPU PCG-spectral run; iterations and rho exact."""
-    m, world, iters, lam = [32, 24, 40], 2, 8, 0.6
+    m, world, iters, lam = [32, 32, 40], 2, 8, 0.6
     th, rho, st, t0 = _one_gpu(m, lam, iters, weighted=True)
     ref = tmp_path / "theta.npy"
     np.save(ref, th)
@@ -148,7 +148,7 @@ def test_failing_rank_ends_its_peers(tmp_path):
     assert res[0][3] is not None and "aborted" in res[0][3]
 
 
-@pytest.mark.parametrize("m,world,iters", [([64, 48, 40], 3, 6), ([96, 80, 33], 2, 0), ([128, 128, 128, 128], 4, 2),
+@pytest.mark.parametrize("m,world,iters", [([48, 48, 40], 3, 6), ([80, 80, 33], 2, 0), ([128, 128, 128, 128], 4, 2),
                                            ([512, 512, 512], 2, 2)],
                          ids=["3d_3proc", "tolerance_2proc", "config5_128_4d_4proc", "metric_512cubed_2proc"])
 def test_slab_processes_match_one_gpu(tmp_path, m, world, iters):
