@@ -359,10 +359,13 @@ struct LocalComm final : mvtv_comm {
 
 // ---- inter-process group over HIP IPC memory --------------------------------------------------------------
 // One process per rank, the ranks' devices the same GPU or peers on one node. Data moves device to device: the
-// receiver copies straight out of the sender's buffer, which it maps with hipIpcOpenMemHandle (same GPU: an HBM
-// copy; peer GPUs: a P2P read over xGMI). Ordering goes through the host: a rendezvous segment in POSIX shared
-// memory holds, per (sender, receiver) channel, a ring of posted buffers (IPC handle, offset, count) and
-// post / ack counters; the all-reduce is a rank-ordered host sum of every rank's staged vector (bit-identical on
+// sender copies a group's send buffers into its own staging buffer (one allocation, grown when a group needs more)
+// and the receiver copies out of it, mapped once with hipIpcOpenMemHandle (same GPU: HBM copies; peer GPUs: a P2P
+// read over xGMI). Staging instead of mapping the problem's own buffers: importing an 8 GB edge-state allocation
+// (a 128^4 rank's) never returned on the box, while the staging buffer holds only a message group (<= a few
+// hundred MB: a 4-D rank's z plane). Ordering goes through the host: a rendezvous segment in POSIX shared
+// memory holds, per (sender, receiver) channel, a ring of posted messages (staging handle and generation,
+// offset, count) and post / ack counters; the all-reduce is a rank-ordered host sum of every rank's staged vector (bit-identical on
 // every rank, as the loopback's). end() is where a group's transfers happen: the sender waits for its data
 // (its stream), posts every send, the receiver copies every posted buffer it expects, waits for the copies and
 // acks, and the sender returns once its peers have acked, so nothing enqueued after end() can overwrite a
@@ -375,8 +378,8 @@ constexpr int IPC_RING = 64;
 constexpr uint64_t IPC_MAGIC = 0x4d5654564950430aull;
 
 struct IpcSlot {
-    hipIpcMemHandle_t handle;
-    uint64_t base_key;   // the sender's allocation base (its mapping cache key on the receiver)
+    hipIpcMemHandle_t handle;   // the sender's staging buffer
+    uint64_t gen;               // its allocation generation (the receiver re-maps when it changes)
     uint64_t offset, n;
 };
 struct IpcChan {
@@ -404,24 +407,40 @@ struct IpcComm final : mvtv_comm {
     std::vector<Out> outs;
     std::vector<In> ins;
     SelfCopy self;
-    std::map<uintptr_t, hipIpcMemHandle_t> exported;                    // base -> handle
-    std::map<std::pair<int, uint64_t>, char*> opened;                   // (peer, sender's base) -> mapping
+    double* stage = nullptr;                        // this rank's staging buffer (exported)
+    size_t stage_words = 0;
+    uint64_t stage_gen = 0;
+    hipIpcMemHandle_t stage_handle{};
+    struct Mapped { uint64_t gen = 0; char* ptr = nullptr; };
+    std::vector<Mapped> mapped;                     // per peer: its staging buffer in this process
     double timeout_s = 300.0;
+    bool trace = false;                                                 // MVTV_IPC_TRACE=1: every step to stderr
+    long ncoll = 0;
+    void tr(const char* what, long a = -1, long b = -1) const {
+        if (!trace) return;
+        const double ts = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        std::fprintf(stderr, "[ipc %d %.6f] #%ld %s %ld %ld\n", rank, ts, ncoll, what, a, b);
+        std::fflush(stderr);
+    }
 
     ~IpcComm() override {
         close_mappings();
+        if (stage) {
+            DeviceGuard dg(device);
+            (void)hipFree(stage);
+        }
         if (shm) munmap(shm, sizeof(IpcShm));
     }
     void close_mappings() {
         DeviceGuard dg(device);
-        for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
-        opened.clear();
-        exported.clear();
+        for (auto& mp : mapped)
+            if (mp.ptr) (void)hipIpcCloseMemHandle(mp.ptr);
+        mapped.assign(size_t(size), Mapped{});
     }
     void abort() override {
         if (shm) shm->aborted.store(1);
     }
-    void run_begin() override { close_mappings(); }   // buffers may have been freed and reallocated since
+    void run_begin() override { close_mappings(); }
     // poll until pred() holds; false on abort or timeout
     template <class F>
     bool wait(F pred, const char* what, mvtv_status* st) {
@@ -472,24 +491,37 @@ struct IpcComm final : mvtv_comm {
     mvtv_status end(hipStream_t s) override {
         DeviceGuard dg(device);
         mvtv_status st = MVTV_OK;
-        if (!outs.empty()) HIP_TRY(hipStreamSynchronize(s));   // every send's data is in place
-        for (const Out& o : outs) {
-            void* base = nullptr;
-            size_t bytes = 0;
-            HIP_TRY(hipMemGetAddressRange(&base, &bytes, const_cast<double*>(o.buf)));
-            auto it = exported.find(reinterpret_cast<uintptr_t>(base));
-            if (it == exported.end()) {
-                hipIpcMemHandle_t h;
-                HIP_TRY(hipIpcGetMemHandle(&h, base));
-                it = exported.emplace(reinterpret_cast<uintptr_t>(base), h).first;
-            }
+        ++ncoll;
+        tr("end: sends / recvs", long(outs.size()), long(ins.size()));
+        // the group's sends into the staging buffer (each message 256-B aligned), grown if the group needs more
+        std::vector<size_t> off(outs.size());
+        size_t words = 0;
+        for (size_t i = 0; i < outs.size(); ++i) {
+            off[i] = words;
+            words += (outs[i].n + 31) / 32 * 32;
+        }
+        if (words > stage_words) {
+            if (stage) HIP_TRY(hipFree(stage));
+            stage = nullptr;
+            stage_words = std::max<size_t>(words, size_t(1) << 20);
+            MVTV_TRY(alloc(&stage, stage_words));
+            HIP_TRY(hipIpcGetMemHandle(&stage_handle, stage));
+            ++stage_gen;
+            tr("end: staging (MB)", long((stage_words * 8) >> 20));
+        }
+        for (size_t i = 0; i < outs.size(); ++i)
+            HIP_TRY(hipMemcpyAsync(stage + off[i], outs[i].buf, outs[i].n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        if (!outs.empty()) HIP_TRY(hipStreamSynchronize(s));   // every send's data is staged
+        tr("end: data ready");
+        for (size_t i = 0; i < outs.size(); ++i) {
+            const Out& o = outs[i];
             IpcChan& c = shm->ch[rank * IPC_MAX_RANKS + o.peer];
             const uint64_t k = sent_n[size_t(o.peer)];
             if (!wait([&] { return k - c.acked.load() < uint64_t(IPC_RING); }, "a free ring slot", &st)) return st;
             IpcSlot& sl = c.slot[k % IPC_RING];
-            sl.handle = it->second;
-            sl.base_key = reinterpret_cast<uintptr_t>(base);
-            sl.offset = uint64_t(reinterpret_cast<const char*>(o.buf) - static_cast<const char*>(base));
+            sl.handle = stage_handle;
+            sl.gen = stage_gen;
+            sl.offset = uint64_t(off[i]) * sizeof(double);
             sl.n = o.n;
             c.posted.store(k + 1);   // release: the slot's contents before the count
             sent_n[size_t(o.peer)] = k + 1;
@@ -500,16 +532,22 @@ struct IpcComm final : mvtv_comm {
             if (!wait([&] { return c.posted.load() > k; }, "a peer's send", &st)) return st;
             const IpcSlot& sl = c.slot[k % IPC_RING];
             if (sl.n != i.n) return fail(MVTV_BAD_ARG, "ipc transfer size mismatch");
-            const auto key = std::make_pair(i.peer, sl.base_key);
-            auto it = opened.find(key);
-            if (it == opened.end()) {
+            Mapped& mp = mapped[size_t(i.peer)];
+            if (!mp.ptr || mp.gen != sl.gen) {   // the peer's (new) staging buffer
+                if (mp.ptr) HIP_TRY(hipIpcCloseMemHandle(mp.ptr));
+                mp.ptr = nullptr;
                 void* p = nullptr;
+                tr("end: open peer staging", i.peer, long(sl.gen));
                 HIP_TRY(hipIpcOpenMemHandle(&p, sl.handle, hipIpcMemLazyEnablePeerAccess));
-                it = opened.emplace(key, static_cast<char*>(p)).first;
+                tr("end: opened");
+                mp.ptr = static_cast<char*>(p);
+                mp.gen = sl.gen;
             }
-            HIP_TRY(hipMemcpyAsync(i.buf, it->second + sl.offset, i.n * sizeof(double), hipMemcpyDeviceToDevice, s));
+            tr("end: copy from peer", i.peer, long(i.n));
+            HIP_TRY(hipMemcpyAsync(i.buf, mp.ptr + sl.offset, i.n * sizeof(double), hipMemcpyDeviceToDevice, s));
         }
         if (!ins.empty()) HIP_TRY(hipStreamSynchronize(s));   // the copies have read their sources
+        tr("end: copies done");
         for (const In& i : ins) {
             IpcChan& c = shm->ch[i.peer * IPC_MAX_RANKS + rank];
             recv_n[size_t(i.peer)] += 1;
@@ -520,6 +558,7 @@ struct IpcComm final : mvtv_comm {
             const uint64_t k = sent_n[size_t(o.peer)];
             if (!wait([&] { return c.acked.load() >= k; }, "a peer's ack", &st)) return st;
         }
+        tr("end: acked");
         outs.clear();
         ins.clear();
         return MVTV_OK;
@@ -540,8 +579,11 @@ struct IpcComm final : mvtv_comm {
         DeviceGuard dg(device);
         double v[64];
         if (n > 64) return fail(MVTV_BAD_ARG, "ipc all-reduce of more than 64 values");
+        ++ncoll;
+        tr("allreduce", long(n));
         HIP_TRY(hipMemcpyAsync(v, buf, n * sizeof(double), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        tr("allreduce: staged");
         MVTV_TRY(allreduce_host_vals(v, n));
         HIP_TRY(hipMemcpyAsync(buf, v, n * sizeof(double), hipMemcpyHostToDevice, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -610,7 +652,9 @@ mvtv_status mvtv_comm_create_ipc(const char* name, int32_t nranks, int32_t rank,
     c->name = name;
     c->sent_n.assign(size_t(nranks), 0);
     c->recv_n.assign(size_t(nranks), 0);
+    c->mapped.assign(size_t(nranks), IpcComm::Mapped{});
     if (const char* t = std::getenv("MVTV_IPC_TIMEOUT")) c->timeout_s = std::max(1.0, std::atof(t));
+    if (const char* t = std::getenv("MVTV_IPC_TRACE")) c->trace = std::atoi(t) != 0;
     const size_t bytes = sizeof(IpcShm);
     int fd = -1;
     const auto t0 = std::chrono::steady_clock::now();

@@ -793,23 +793,30 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
 // FWD 78 -> ~110, INV 94 -> ~126, still 4 waves per SIMD at 512 threads) and every barrier orders LDS only
 // (lds_barrier), so the prefetch is never waited for before its tile. In k_dct8 a workgroup's loads are all
 // in flight only before its first stage, and with two workgroups per CU (LDS) both may be computing.
-template <int L, int MODE>
+template <int L, int MODE, bool D0 = false>
 __global__ __launch_bounds__((spec8::ShapeK<L, 16>::NT), 4) void k_dct8s(const SpecArgs a) {
     using S = spec8::ShapeK<L, 16>;
     static_assert(MODE == SPEC_FWD || MODE == SPEC_INV, "forward or inverse passes");
+    static_assert(!D0 || MODE == SPEC_INV, "d = 0: the inverse pass (the forward one forms b)");
     if (a.skip && *a.skip) return;
     if (a.ctl && a.ctl->done) return;
     constexpr int M = S::M, TPL = S::TPL, NCL = S::NCL, R0 = S::R0;
     __shared__ double2 buf[NCL * S::LP];
     int t = threadIdx.x;
-    int j = t / NCL, c = t % NCL;
+    int j = D0 ? t % TPL : t / NCL, c = D0 ? t / TPL : t % NCL;
     double2* X = buf + c * S::LP;
     int cx = c & 7;
     const uint32_t ntiles = a.nlines / 16u;
     // (line 2c of tile tt, position k) -> global offset; lines 2c, 2c + 1 are adjacent words
+    // (d = 0: line 2c's own offset; line 2c + 1 is M words further)
     auto gaddr = [&](uint32_t tt, uint32_t k) -> uint32_t {
         const uint32_t q = tt * 16u + uint32_t(2 * c);
+        if (D0) return (q << L) + k;
         return (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (k << a.ls);
+    };
+    auto ld2 = [&](uint32_t g) -> double2 {
+        if (D0) return make_double2(__builtin_nontemporal_load(a.in + g), __builtin_nontemporal_load(a.in + g + M));
+        return ldnt2(a.in + g);
     };
     // FWD: the first stage's inputs (Makhoul positions); INV: the coefficient pairs (k, M - k)
     auto load = [&](uint32_t tt, double2* v) {
@@ -824,8 +831,8 @@ __global__ __launch_bounds__((spec8::ShapeK<L, 16>::NT), 4) void k_dct8s(const S
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int k = j + s * TPL;
-                v[2 * s] = ldnt2(a.in + gaddr(tt, uint32_t(k)));
-                v[2 * s + 1] = ldnt2(a.in + gaddr(tt, uint32_t(k ? M - k : M / 2)));
+                v[2 * s] = ld2(gaddr(tt, uint32_t(k)));
+                v[2 * s + 1] = ld2(gaddr(tt, uint32_t(k ? M - k : M / 2)));
             }
         }
     };
@@ -839,8 +846,8 @@ __global__ __launch_bounds__((spec8::ShapeK<L, 16>::NT), 4) void k_dct8s(const S
         const double2* tw = a.tw;
         asm volatile("" : "+s"(tw));
         asm volatile("" : "+v"(t));
-        j = t / NCL;
-        c = t % NCL;
+        j = D0 ? t % TPL : t / NCL;
+        c = D0 ? t / TPL : t % NCL;
         X = buf + c * S::LP;
         cx = c & 7;
         double2 z[8];
@@ -894,13 +901,26 @@ __global__ __launch_bounds__((spec8::ShapeK<L, 16>::NT), 4) void k_dct8s(const S
             lds_barrier();
 #pragma unroll
             for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, R0>(j, i), cx)];
-            stages_from<L, R0, 1, true, true, true>(z, j, X, cx, tw);
-            using LS = LastStage<L>;
+            if constexpr (D0) {
+                // the output goes through X so (x[2n], x[2n+1]) of a line leave as one 16-B store
+                stages_from<L, R0, 1, true, false, true>(z, j, X, cx, tw);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int n = stage_out_pos<L, LS::R, LS::NS>(j, i);
-                const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
-                stnt2(a.out + gaddr(tt, k), z[i]);
+                for (int s4 = 0; s4 < 4; ++s4) {
+                    const int n = j + s4 * TPL;
+                    const double2 v0 = X[spec8::slot(n, cx)], v1 = X[spec8::slot(M - 1 - n, cx)];
+                    const uint32_t g = gaddr(tt, uint32_t(2 * n));
+                    stnt2(a.out + g, make_double2(v0.x, v1.x));
+                    stnt2(a.out + g + M, make_double2(v0.y, v1.y));
+                }
+            } else {
+                stages_from<L, R0, 1, true, true, true>(z, j, X, cx, tw);
+                using LS = LastStage<L>;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int n = stage_out_pos<L, LS::R, LS::NS>(j, i);
+                    const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
+                    stnt2(a.out + gaddr(tt, k), z[i]);
+                }
             }
         }
     }
@@ -3431,20 +3451,20 @@ static bool try_tile(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb, 
 // passes 17.5 -> 14.8 us, strided 18.7 -> 11.8 us); 2048^2: 4797 -> 4862 (profiles/r02/v17_dct_tiles).
 // Probe builds: MVTV_DCT_T0 / _T1 set the d = 0 / d > 0 tile, MVTV_DCT_XCD=0/1 the XCD runs.
 // k_dct8s (streamed strided passes): resident workgroups x CUs, at most one per tile
-template <int L, int MODE>
+template <int L, int MODE, bool D0 = false>
 static void launch_dct8s(SpecArgs& a, hipStream_t s) {
     static const uint32_t resident = [] {
         int dev = 0, cus = 0, per_cu = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dct8s<L, MODE>, spec8::ShapeK<L, 16>::NT, 0) !=
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dct8s<L, MODE, D0>, spec8::ShapeK<L, 16>::NT, 0) !=
                 hipSuccess)
             return 512u;
         return uint32_t(std::max(1, cus) * std::max(1, per_cu));
     }();
     a.tq = 16;
     const uint32_t ntiles = a.nlines / 16u;
-    klaunch(k_dct8s<L, MODE>, dim3(std::min(ntiles, resident)), dim3(spec8::ShapeK<L, 16>::NT), 0, s, a);
+    klaunch(k_dct8s<L, MODE, D0>, dim3(std::min(ntiles, resident)), dim3(spec8::ShapeK<L, 16>::NT), 0, s, a);
 }
 
 template <int L>
@@ -3454,9 +3474,10 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
     // MVTV_DCT_STREAM=1)
     if constexpr (L >= 6 && L <= 9) {
         static const bool stream = probe_env("MVTV_DCT_STREAM") != nullptr;
-        if (stream && !d0 && !formb && (mode == SPEC_FWD || mode == SPEC_INV) && a.stride >= 16u &&
-            a.nlines % 16u == 0u && a.nlines / 16u >= 2048u && !a.pf.mode) {
-            if (mode == SPEC_FWD) launch_dct8s<L, SPEC_FWD>(a, s);
+        if (stream && !formb && (mode == SPEC_FWD || mode == SPEC_INV) && (d0 || a.stride >= 16u) &&
+            !(d0 && mode == SPEC_FWD) && a.nlines % 16u == 0u && a.nlines / 16u >= 2048u && !a.pf.mode) {
+            if (d0) launch_dct8s<L, SPEC_INV, true>(a, s);
+            else if (mode == SPEC_FWD) launch_dct8s<L, SPEC_FWD>(a, s);
             else launch_dct8s<L, SPEC_INV>(a, s);
             return;
         }

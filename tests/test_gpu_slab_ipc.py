@@ -38,7 +38,7 @@ def _say(rank, msg):
 
 def _rank_main(rank, world, port, q, m, lam, iters, ref_path, weighted, fail_rank, t0):
     import faulthandler
-    faulthandler.dump_traceback_later(150, exit=False)   # a stuck rank shows where it is
+    faulthandler.dump_traceback_later(100, exit=False)   # a stuck rank shows where it is
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -87,7 +87,7 @@ def _run_group(world, m, lam, iters, ref_path, t0, weighted=False, fail_rank=-1,
     q = ctx.Queue()
     port = _free_port()
     env = dict(env or {})
-    env.setdefault("MVTV_IPC_TIMEOUT", "90")   # a transport wait that never ends fails the test instead
+    env.setdefault("MVTV_IPC_TIMEOUT", "60")   # a transport wait that never ends fails the test instead
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -101,7 +101,7 @@ def _run_group(world, m, lam, iters, ref_path, t0, weighted=False, fail_rank=-1,
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-    res = sorted((q.get(timeout=240) for _ in procs), key=lambda t: t[0])
+    res = sorted((q.get(timeout=180) for _ in procs), key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
