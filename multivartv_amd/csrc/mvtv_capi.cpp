@@ -502,65 +502,6 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
     order[n++] = mid;
     // m0 = m1 <= 128: dims 0 and 1 in one pass each way (k_plane8: the plane stays on chip between them)
     const bool plane = mid >= 2 && plane_pass_ok(P->g);
-    // Probe (MVTV_ZCHUNK=K, K | m2): the in-plane pass pairs run per chunk of K dim-2 planes (dim 0 then dim 1 on
-    // a chunk before the next chunk), so the second pass of a pair reads what the first just wrote while it may
-    // still sit in the 256 MB Infinity Cache, and overwrites it in place there
-    static const int zchunk = [] {
-        const char* e = probe_env("MVTV_ZCHUNK");
-        return e ? std::atoi(e) : 0;
-    }();
-    if (zchunk > 0 && p == 3 && mid == 2 && !plane && !P->slab && P->g.m[2] % uint32_t(zchunk) == 0 &&
-        uint32_t(zchunk) < P->g.m[2]) {
-        Geom gc = P->g;
-        gc.m[2] = uint32_t(zchunk);
-        gc.N = gc.m[0] * gc.m[1] * gc.m[2];
-        const size_t cw = size_t(gc.N);
-        const uint32_t nch = P->g.m[2] / uint32_t(zchunk);
-        for (uint32_t c = 0; c < nch; ++c) {
-            const size_t o = size_t(c) * cw;
-            int h = P->tstart(ga ? (fold ? MVTV_K_DCT_FOLD : MVTV_K_DCT_FIRST) : MVTV_K_DCT);
-            if (ga && fold)
-                HIP_TRY(launch_dct_pass(P->spec, gc, P->stream, 0, 0, oty + o, ga + o, 1.0, gb + o, 0.0, x + o, sigma, w0,
-                                        ctl, 0, 1.0 / double(P->g.N), skip, nullptr, true));
-            else if (ga)
-                HIP_TRY(launch_dct_pass(P->spec, gc, P->stream, 0, 0, oty + o, ga + o, ca, (gb ? gb : ga) + o,
-                                        gb ? cb : 0.0, x + o, sigma, w0, ctl, 0, 1.0 / double(P->g.N), skip));
-            else
-                HIP_TRY(launch_dct_pass(P->spec, gc, P->stream, 0, 0, oty + o, nullptr, 0.0, nullptr, 0.0, x + o, sigma,
-                                        w0, ctl, 0, 1.0 / double(P->g.N), skip));
-            P->tstop(h);
-            h = P->tstart(MVTV_K_DCT);
-            HIP_TRY(launch_dct_pass(P->spec, gc, P->stream, 0, 1, x + o, nullptr, 0.0, nullptr, 0.0, x + o, sigma, w0,
-                                    ctl, 0, 1.0 / double(P->g.N), skip));
-            P->tstop(h);
-        }
-        int h = P->tstart(MVTV_K_DCT);
-        HIP_TRY(launch_dct_pass(P->spec, P->g, P->stream, 2, 2, x, nullptr, 0.0, nullptr, 0.0, x, sigma, w0, ctl, 0, 0.0,
-                                skip));
-        P->tstop(h);
-        for (uint32_t c = 0; c < nch; ++c) {
-            const size_t o = size_t(c) * cw;
-            h = P->tstart(MVTV_K_DCT);
-            HIP_TRY(launch_dct_pass(P->spec, gc, P->stream, 1, 1, x + o, nullptr, 0.0, nullptr, 0.0, x + o, sigma, w0,
-                                    ctl, 0, 1.0 / double(P->g.N), skip));
-            P->tstop(h);
-            h = P->tstart(MVTV_K_DCT);
-            HIP_TRY(launch_dct_pass(P->spec, gc, P->stream, 1, 0, x + o, nullptr, 0.0, nullptr, 0.0, x + o, sigma, w0,
-                                    ctl, 0, 1.0 / double(P->g.N), skip));
-            P->tstop(h);
-        }
-        return MVTV_OK;
-    }
-    if (plane) {
-        const int h = P->tstart(ga ? (fold ? MVTV_K_DCT_FOLD : MVTV_K_DCT_FIRST) : MVTV_K_DCT);
-        if (ga && fold)
-            HIP_TRY(launch_plane_pass(P->spec, P->g, P->stream, 0, oty, ga, 1.0, gb, 0.0, x, ctl, skip, true));
-        else if (ga)
-            HIP_TRY(launch_plane_pass(P->spec, P->g, P->stream, 0, oty, ga, ca, gb, cb, x, ctl, skip));
-        else
-            HIP_TRY(launch_plane_pass(P->spec, P->g, P->stream, 0, oty, nullptr, 0.0, nullptr, 0.0, x, ctl, skip));
-        P->tstop(h);
-    }
     for (int t = plane ? 2 : 0; t < p; ++t) {
         const int d = order[t];
         const bool first = t == 0;

@@ -787,146 +787,6 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
 }
 
 // =============================================================================================
-// Streamed strided passes (d > 0, FWD or INV, 16-line tiles, every tile full): k_dct8's tile work with the
-// next tile's loads in flight during this tile's FFT. A grid of resident workgroups walks the tiles
-// (blockIdx.x, + gridDim.x, ...); a thread holds this tile's 8 inputs and the next tile's 8 (32 more VGPRs:
-// FWD 78 -> ~110, INV 94 -> ~126, still 4 waves per SIMD at 512 threads) and every barrier orders LDS only
-// (lds_barrier), so the prefetch is never waited for before its tile. In k_dct8 a workgroup's loads are all
-// in flight only before its first stage, and with two workgroups per CU (LDS) both may be computing.
-template <int L, int MODE, bool D0 = false>
-__global__ __launch_bounds__((spec8::ShapeK<L, 16>::NT), 4) void k_dct8s(const SpecArgs a) {
-    using S = spec8::ShapeK<L, 16>;
-    static_assert(MODE == SPEC_FWD || MODE == SPEC_INV, "forward or inverse passes");
-    static_assert(!D0 || MODE == SPEC_INV, "d = 0: the inverse pass (the forward one forms b)");
-    if (a.skip && *a.skip) return;
-    if (a.ctl && a.ctl->done) return;
-    constexpr int M = S::M, TPL = S::TPL, NCL = S::NCL, R0 = S::R0;
-    __shared__ double2 buf[NCL * S::LP];
-    int t = threadIdx.x;
-    int j = D0 ? t % TPL : t / NCL, c = D0 ? t / TPL : t % NCL;
-    double2* X = buf + c * S::LP;
-    int cx = c & 7;
-    const uint32_t ntiles = a.nlines / 16u;
-    // (line 2c of tile tt, position k) -> global offset; lines 2c, 2c + 1 are adjacent words
-    // (d = 0: line 2c's own offset; line 2c + 1 is M words further)
-    auto gaddr = [&](uint32_t tt, uint32_t k) -> uint32_t {
-        const uint32_t q = tt * 16u + uint32_t(2 * c);
-        if (D0) return (q << L) + k;
-        return (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (k << a.ls);
-    };
-    auto ld2 = [&](uint32_t g) -> double2 {
-        if (D0) return make_double2(__builtin_nontemporal_load(a.in + g), __builtin_nontemporal_load(a.in + g + M));
-        return ldnt2(a.in + g);
-    };
-    // FWD: the first stage's inputs (Makhoul positions); INV: the coefficient pairs (k, M - k)
-    auto load = [&](uint32_t tt, double2* v) {
-        if constexpr (MODE == SPEC_FWD) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int n = stage_in_pos<L, R0>(j, i);
-                const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
-                v[i] = ldnt2(a.in + gaddr(tt, k));
-            }
-        } else {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int k = j + s * TPL;
-                v[2 * s] = ld2(gaddr(tt, uint32_t(k)));
-                v[2 * s + 1] = ld2(gaddr(tt, uint32_t(k ? M - k : M / 2)));
-            }
-        }
-    };
-    double2 nx[8];
-    uint32_t tt = blockIdx.x;
-    if (tt < ntiles) load(tt, nx);
-    for (; tt < ntiles; tt += gridDim.x) {
-        // per-thread offsets re-derived from an opaque copy of the thread index every tile, and the twiddle
-        // tables through opaque pointers (hoisted out of the loop they stay live beside the prefetch and the
-        // kernel needs ~166 VGPRs: one workgroup per CU)
-        const double2* tw = a.tw;
-        asm volatile("" : "+s"(tw));
-        asm volatile("" : "+v"(t));
-        j = D0 ? t % TPL : t / NCL;
-        c = D0 ? t / TPL : t % NCL;
-        X = buf + c * S::LP;
-        cx = c & 7;
-        double2 z[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) z[i] = nx[i];
-        if (tt + gridDim.x < ntiles) load(tt + gridDim.x, nx);
-        if constexpr (MODE == SPEC_FWD) {
-            // its first barrier also ends the previous tile's reads of X
-            stages_from<L, R0, 1, false, false, true>(z, j, X, cx, tw);   // natural-order spectrum in X
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int k = j + s * TPL;
-                const int ka = k, kb = k ? M - k : M / 2;
-                const double2 Z1 = X[spec8::slot(ka, cx)], Z2 = X[spec8::slot(kb, cx)];
-                const double2 q1 = a.twq[ka], q2 = a.twq[kb];
-                double2 Xk, Xmk;
-                if (k == 0) {
-                    Xk = make_double2(q1.x * Z1.x, q1.x * Z1.y);
-                    Xmk = make_double2(q2.x * Z2.x, q2.x * Z2.y);
-                } else {
-                    const double2 Ap = make_double2(0.5 * (Z1.x + Z2.x), 0.5 * (Z1.y - Z2.y));
-                    const double2 Bp = make_double2(0.5 * (Z1.y + Z2.y), -0.5 * (Z1.x - Z2.x));
-                    Xk = make_double2(q1.x * Ap.x - q1.y * Ap.y, q1.x * Bp.x - q1.y * Bp.y);
-                    Xmk = make_double2(q2.x * Ap.x + q2.y * Ap.y, q2.x * Bp.x + q2.y * Bp.y);
-                }
-                stnt2(a.out + gaddr(tt, uint32_t(ka)), Xk);
-                stnt2(a.out + gaddr(tt, uint32_t(kb)), Xmk);
-            }
-        } else {
-            lds_barrier();   // the previous tile's reads of X are done
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int k = j + s * TPL;
-                const int ka = k, kb = k ? M - k : M / 2;
-                const double2 Xk = z[2 * s], Xmk = z[2 * s + 1];
-                const double2 q1 = cconj(a.twq[ka]), q2 = cconj(a.twq[kb]);
-                if (k == 0) {
-                    const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xmk.x));
-                    const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xmk.y));
-                    X[spec8::slot(0, cx)] = Xk;
-                    X[spec8::slot(M / 2, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
-                } else {
-                    const double2 va1 = cmul(q1, make_double2(Xk.x, -Xmk.x));
-                    const double2 vb1 = cmul(q1, make_double2(Xk.y, -Xmk.y));
-                    const double2 va2 = cmul(q2, make_double2(Xmk.x, -Xk.x));
-                    const double2 vb2 = cmul(q2, make_double2(Xmk.y, -Xk.y));
-                    X[spec8::slot(ka, cx)] = make_double2(va1.x - vb1.y, va1.y + vb1.x);
-                    X[spec8::slot(kb, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
-                }
-            }
-            lds_barrier();
-#pragma unroll
-            for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, R0>(j, i), cx)];
-            if constexpr (D0) {
-                // the output goes through X so (x[2n], x[2n+1]) of a line leave as one 16-B store
-                stages_from<L, R0, 1, true, false, true>(z, j, X, cx, tw);
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) {
-                    const int n = j + s4 * TPL;
-                    const double2 v0 = X[spec8::slot(n, cx)], v1 = X[spec8::slot(M - 1 - n, cx)];
-                    const uint32_t g = gaddr(tt, uint32_t(2 * n));
-                    stnt2(a.out + g, make_double2(v0.x, v1.x));
-                    stnt2(a.out + g + M, make_double2(v0.y, v1.y));
-                }
-            } else {
-                stages_from<L, R0, 1, true, true, true>(z, j, X, cx, tw);
-                using LS = LastStage<L>;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int n = stage_out_pos<L, LS::R, LS::NS>(j, i);
-                    const uint32_t k = n < M / 2 ? uint32_t(2 * n) : uint32_t(2 * (M - 1 - n) + 1);
-                    stnt2(a.out + gaddr(tt, k), z[i]);
-                }
-            }
-        }
-    }
-}
-
-// =============================================================================================
 // Two in-plane passes in one launch (m0 = m1 = 2^L, L <= 7): a workgroup owns one (dim 0, dim 1) plane,
 // 128 KB at L = 7, and keeps it on chip between the two 1-D transforms, so the spectral solve of a 4-D
 // 128^4 mesh makes 5 passes over HBM instead of 7 (3 instead of 5 at 128^3). NCL = M / 2 complex lines x
@@ -2661,167 +2521,6 @@ __global__ __launch_bounds__((tri::Shape<L, SEG, TQL>::NT)) void k_tri(const Spe
         __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + (uint32_t(i) << a.ls));
 }
 
-// k_tri_s: k_tri<L, 32, 64> over resident workgroups that walk the tiles (blockIdx.x, + gridDim.x, ...), the first
-// PF rows of the next tile's segments loaded during this tile's solve (PF VGPRs more: 106 -> ~122 at 1024
-// threads), every barrier ordering LDS only so the prefetch is not waited for. k_tri's one workgroup per CU
-// (99 KB of LDS) otherwise has no loads in flight while it computes the line constants and the interface system.
-namespace tri {
-// prefetched rows of a 32-row segment (1024-thread workgroups at L = 9 have 128 VGPRs: 8 fit without spills)
-template <int L>
-constexpr int pf_rows() { return L >= 9 ? 8 : 16; }
-}
-template <int L>
-__global__ __launch_bounds__((tri::Shape<L, 32, 64>::NT)) void k_tri_s(const SpecArgs a) {
-    constexpr int SEG = 32, TQ = 64, PF = tri::pf_rows<L>();
-    using S = tri::Shape<L, SEG, TQ>;
-    constexpr int NSEG = S::NSEG;
-    double sigma = a.sigma;
-    if (a.skip && *a.skip) return;
-    if (a.ctl) {
-        if (a.ctl->done) return;
-        sigma = a.ctl->sigma;
-    }
-    __shared__ double t_id[SEG][TQ], t_e[SEG][TQ], t_h[SEG][TQ], t_k[SEG][TQ];
-    __shared__ double s_a[TQ];
-    __shared__ double s_u[NSEG][TQ], s_v[NSEG][TQ], s_bu[NSEG][TQ], s_bv[NSEG][TQ];
-    int t = threadIdx.x, c = t % TQ, sj = t / TQ;
-    const uint32_t ntiles = a.nlines / uint32_t(TQ);
-    auto base_of = [&](uint32_t tt) -> uint32_t {
-        const uint32_t q = tt * uint32_t(TQ) + uint32_t(c);
-        return (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (uint32_t(sj * SEG) << a.ls);
-    };
-    double nx[PF];
-    uint32_t tt = blockIdx.x;
-    if (tt < ntiles) {
-        const uint32_t b = base_of(tt);
-#pragma unroll
-        for (int i = 0; i < PF; ++i) nx[i] = __builtin_nontemporal_load(a.in + b + (uint32_t(i) << a.ls));
-    }
-    for (; tt < ntiles; tt += gridDim.x) {
-        asm volatile("" : "+v"(t));   // per-thread offsets re-derived every tile (hoisted, they spill)
-        c = t % TQ;
-        sj = t / TQ;
-        const uint32_t base = base_of(tt);
-        // eigenvalue loads first (the constants wait for them alone), then this tile's remaining rows, then the
-        // next tile's first rows (loads complete in order)
-        double lamv[kMaxDims] = {0, 0, 0, 0};
-        if (t < TQ) {
-            uint32_t rest = a.q_off + tt * uint32_t(TQ) + uint32_t(c);
-            const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
-            for (int jj = 0; jj < a.p; ++jj) {
-                if (jj == a.d) continue;
-                const uint32_t qq = (jj < jlast) ? a.fd[jj].div(rest) : 0u;
-                lamv[jj] = a.lam[a.lam_off[jj] + (rest - qq * a.m[jj])];
-                rest = qq;
-            }
-        }
-        double g[SEG];
-#pragma unroll
-        for (int i = 0; i < PF; ++i) g[i] = nx[i];
-#pragma unroll
-        for (int i = PF; i < SEG; ++i) g[i] = __builtin_nontemporal_load(a.in + base + (uint32_t(i) << a.ls));
-        if (tt + gridDim.x < ntiles) {
-            const uint32_t bn = base_of(tt + gridDim.x);
-#pragma unroll
-            for (int i = 0; i < PF; ++i) nx[i] = __builtin_nontemporal_load(a.in + bn + (uint32_t(i) << a.ls));
-        }
-        if (t < TQ) {
-            double c0 = a.w0, c1 = 0.0;
-            for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
-                if (a.cS[Sm] == 0.0) continue;
-                double prod = sigma * a.cS[Sm];
-                for (int jj = 0; jj < a.p; ++jj)
-                    if (jj != a.d && ((Sm >> jj) & 1)) prod *= lamv[jj];
-                if ((Sm >> a.d) & 1) c1 += prod;
-                else c0 += prod;
-            }
-            const double A = -c1, B = c0 + 2.0 * c1;
-            double e = 0.0, h = 1.0;
-#pragma unroll 1
-            for (int i = 0; i < SEG; ++i) {
-                const double id = 1.0 / (B - A * e);
-                e = A * id;
-                h = -A * h * id;
-                t_id[i][c] = id;
-                t_e[i][c] = e;
-                t_h[i][c] = h;
-            }
-            double H = t_h[SEG - 1][c], K = -t_e[SEG - 1][c];
-            t_k[SEG - 1][c] = K;
-#pragma unroll 1
-            for (int i = SEG - 2; i >= 0; --i) {
-                const double ei = t_e[i][c];
-                H = t_h[i][c] - ei * H;
-                K = -ei * K;
-                t_h[i][c] = H;
-                t_k[i][c] = K;
-            }
-            s_a[c] = A;
-        }
-        lds_barrier();
-        {
-            const double A = s_a[c];
-            g[0] *= t_id[0][c];
-#pragma unroll
-            for (int i = 1; i < SEG; ++i) g[i] = (g[i] - A * g[i - 1]) * t_id[i][c];
-#pragma unroll
-            for (int i = SEG - 2; i >= 0; --i) g[i] -= t_e[i][c] * g[i + 1];
-            s_u[sj][c] = g[0];
-            s_v[sj][c] = g[SEG - 1];
-        }
-        lds_barrier();
-        if (t < TQ) {
-            const double H0 = t_h[0][c], K0 = t_k[0][c], H1 = t_h[SEG - 1][c], K1 = t_k[SEG - 1][c];
-            double av = 0.0, bv = 0.0;
-#pragma unroll 1
-            for (int jb = 0; jb < NSEG - 1; ++jb) {
-                const double g0 = s_u[jb][c], g1 = s_v[jb][c];
-                double au, bu;
-                if (jb == 0) {
-                    const double id = 1.0 / (1.0 - H0);
-                    au = g0 * id;
-                    bu = K0 * id;
-                    av = g1 + H1 * au;
-                    bv = K1 + H1 * bu;
-                } else {
-                    const double id = 1.0 / (1.0 - H0 * bv);
-                    au = (g0 + H0 * av) * id;
-                    bu = K0 * id;
-                    const double nav = g1 + H1 * av + H1 * bv * au;
-                    bv = K1 + H1 * bv * bu;
-                    av = nav;
-                }
-                s_u[jb][c] = au;
-                s_bu[jb][c] = bu;
-                s_v[jb][c] = av;
-                s_bv[jb][c] = bv;
-            }
-            constexpr int J = NSEG - 1;
-            const double a11 = 1.0 - H0 * bv, a12 = -K0, a21 = -H1 * bv, a22 = 1.0 - K1;
-            const double b1 = s_u[J][c] + H0 * av, b2 = s_v[J][c] + H1 * av;
-            const double idet = 1.0 / (a11 * a22 - a12 * a21);
-            double u = (b1 * a22 - a12 * b2) * idet;
-            s_u[J][c] = u;
-            s_v[J][c] = (a11 * b2 - a21 * b1) * idet;
-#pragma unroll 1
-            for (int jb = J - 1; jb >= 0; --jb) {
-                const double un = u;
-                u = s_u[jb][c] + s_bu[jb][c] * un;
-                s_v[jb][c] = s_v[jb][c] + s_bv[jb][c] * un;
-                s_u[jb][c] = u;
-            }
-        }
-        lds_barrier();
-        const double Lj = sj == 0 ? s_u[0][c] : s_v[sj - 1][c];
-        const double Rj = sj == NSEG - 1 ? s_v[NSEG - 1][c] : s_u[sj + 1][c];
-        const double sc = a.inv_n * double(S::M);
-#pragma unroll
-        for (int i = 0; i < SEG; ++i)
-            __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + (uint32_t(i) << a.ls));
-        lds_barrier();   // every read of this tile's constants and interface values before the next tile's writes
-    }
-}
-
 // k_trig: the same solve for any line length m = NSEG * s (segment length s <= 32 chosen at launch,
 // NSEG <= 64) and any line stride (FastDiv addressing): the last-dimension pass of the mixed-radix
 // meshes. Rows past s in the fixed-size register arrays are predicated off.
@@ -3340,21 +3039,6 @@ static void launch_tri(SpecArgs& a, hipStream_t s, int tq) {
             launch_tri_seg<16, 32>(a, s);
         } else if (tqw == 64 && seg == 16 && a.stride >= 64u && a.L >= 7 && a.L <= 9 && a.nlines / 64u >= 256u) {
             a.tq = 64;
-            static const bool tri_stream = probe_env("MVTV_TRI_STREAM") != nullptr;
-            if (tri_stream && a.nlines % 64u == 0u && a.nlines / 64u >= 1024u) {
-                static const uint32_t cus = [] {
-                    int dev = 0, n = 0;
-                    if (hipGetDevice(&dev) != hipSuccess ||
-                        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                        return 256u;
-                    return uint32_t(std::max(1, n));
-                }();
-                const dim3 grid(std::min(a.nlines / 64u, cus));   // one 99-KB workgroup per CU
-                if (a.L == 7) klaunch(k_tri_s<7>, grid, dim3(tri::Shape<7, 32, 64>::NT), 0, s, a);
-                else if (a.L == 8) klaunch(k_tri_s<8>, grid, dim3(tri::Shape<8, 32, 64>::NT), 0, s, a);
-                else klaunch(k_tri_s<9>, grid, dim3(tri::Shape<9, 32, 64>::NT), 0, s, a);
-                return;
-            }
             const dim3 grid((a.nlines + 63u) / 64u);
             if (a.L == 7) klaunch(k_tri<7, 32, 64>, grid, dim3(tri::Shape<7, 32, 64>::NT), 0, s, a);
             else if (a.L == 8) klaunch(k_tri<8, 32, 64>, grid, dim3(tri::Shape<8, 32, 64>::NT), 0, s, a);
@@ -3450,38 +3134,9 @@ static bool try_tile(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb, 
 // contiguous runs, so the 4 tiles of a 128-B row share one L2. 1024^2: 8355 -> 9650 ADMM it/s (d = 0
 // passes 17.5 -> 14.8 us, strided 18.7 -> 11.8 us); 2048^2: 4797 -> 4862 (profiles/r02/v17_dct_tiles).
 // Probe builds: MVTV_DCT_T0 / _T1 set the d = 0 / d > 0 tile, MVTV_DCT_XCD=0/1 the XCD runs.
-// k_dct8s (streamed strided passes): resident workgroups x CUs, at most one per tile
-template <int L, int MODE, bool D0 = false>
-static void launch_dct8s(SpecArgs& a, hipStream_t s) {
-    static const uint32_t resident = [] {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dct8s<L, MODE, D0>, spec8::ShapeK<L, 16>::NT, 0) !=
-                hipSuccess)
-            return 512u;
-        return uint32_t(std::max(1, cus) * std::max(1, per_cu));
-    }();
-    a.tq = 16;
-    const uint32_t ntiles = a.nlines / 16u;
-    klaunch(k_dct8s<L, MODE, D0>, dim3(std::min(ntiles, resident)), dim3(spec8::ShapeK<L, 16>::NT), 0, s, a);
-}
-
 template <int L>
 static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
     using S = spec8::Shape<L>;
-    // strided forward / inverse passes of full 16-line tiles over many tiles: the streamed form (probe builds:
-    // MVTV_DCT_STREAM=1)
-    if constexpr (L >= 6 && L <= 9) {
-        static const bool stream = probe_env("MVTV_DCT_STREAM") != nullptr;
-        if (stream && !formb && (mode == SPEC_FWD || mode == SPEC_INV) && (d0 || a.stride >= 16u) &&
-            !(d0 && mode == SPEC_FWD) && a.nlines % 16u == 0u && a.nlines / 16u >= 2048u && !a.pf.mode) {
-            if (d0) launch_dct8s<L, SPEC_INV, true>(a, s);
-            else if (mode == SPEC_FWD) launch_dct8s<L, SPEC_FWD>(a, s);
-            else launch_dct8s<L, SPEC_INV>(a, s);
-            return;
-        }
-    }
     constexpr int TMIN = tile_ok<L>(2) ? 2 : (tile_ok<L>(4) ? 4 : (tile_ok<L>(8) ? 8 : 16));
     int want = S::TQ;
     bool xcd_def = false;
