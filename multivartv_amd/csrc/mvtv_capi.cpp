@@ -502,6 +502,16 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
     order[n++] = mid;
     // m0 = m1 <= 128: dims 0 and 1 in one pass each way (k_plane8: the plane stays on chip between them)
     const bool plane = mid >= 2 && plane_pass_ok(P->g);
+    if (plane) {
+        const int h = P->tstart(ga ? (fold ? MVTV_K_DCT_FOLD : MVTV_K_DCT_FIRST) : MVTV_K_DCT);
+        if (ga && fold)
+            HIP_TRY(launch_plane_pass(P->spec, P->g, P->stream, 0, oty, ga, 1.0, gb, 0.0, x, ctl, skip, true));
+        else if (ga)
+            HIP_TRY(launch_plane_pass(P->spec, P->g, P->stream, 0, oty, ga, ca, gb, cb, x, ctl, skip));
+        else
+            HIP_TRY(launch_plane_pass(P->spec, P->g, P->stream, 0, oty, nullptr, 0.0, nullptr, 0.0, x, ctl, skip));
+        P->tstop(h);
+    }
     for (int t = plane ? 2 : 0; t < p; ++t) {
         const int d = order[t];
         const bool first = t == 0;

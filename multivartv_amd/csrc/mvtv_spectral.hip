@@ -800,7 +800,12 @@ __global__ __launch_bounds__((1 << L) / 2 * (1 << L) / 8) void k_plane8(const Sp
     using S = spec8::Shape<L>;
     constexpr int M = S::M, TPL = S::TPL, NCL = M / 2, R0 = S::R0;
     static_assert(L >= 4 && L <= 7, "the plane must fit the exchange buffer of one workgroup");
-    static_assert(size_t(NCL) * S::LP * 16 >= size_t(M) * M * 8, "plane image aliases the exchange buffer");
+    // plane image pitch PP = M + M / 16 doubles (18 at M = 16): a wave's row accesses (8-B words, TPL = M / 8
+    // lanes per row, 8 rows a wave at M = 64, 4 at 128) then start 16 PP bytes apart = M bytes mod 256, so the rows
+    // of one wave instruction fall on different LDS banks; with pitch M every row started on bank 0 (rows 2 KB
+    // apart at M = 128: 4-way conflicts on the transposes). Column accesses stay 16-B aligned (PP even).
+    constexpr int PP = M + (M / 16 > 2 ? M / 16 : 2);
+    static_assert(size_t(NCL) * S::LP * 16 >= size_t(M) * PP * 8, "plane image aliases the exchange buffer");
     static_assert(MODE == SPEC_FWD || !FORMB, "b is formed by the forward pass");
     double ca = a.ca, cb = a.cb;
     bool rd_gb = true;
@@ -816,7 +821,7 @@ __global__ __launch_bounds__((1 << L) / 2 * (1 << L) / 8) void k_plane8(const Sp
         }
     }
     __shared__ double2 buf[NCL * S::LP];
-    double* const PI = reinterpret_cast<double*>(buf);   // plane image [row x1][column x0], pitch M
+    double* const PI = reinterpret_cast<double*>(buf);   // plane image [row x1][column x0], pitch PP
     // rows mapping (dim-0 lines: lanes over j) and columns mapping (dim-1 lines: lanes over the line pair); the
     // loop below re-derives them from an opaque copy of the thread index each plane, so the many per-thread LDS
     // offsets are not hoisted out of it (kept live across the loop they spill)
@@ -931,10 +936,10 @@ __global__ __launch_bounds__((1 << L) / 2 * (1 << L) / 8) void k_plane8(const Sp
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int k = jr + s * TPL, ka = k, kb = k ? M - k : M / 2;
-                PI[(2 * cr) * M + ka] = z[2 * s].x;
-                PI[(2 * cr + 1) * M + ka] = z[2 * s].y;
-                PI[(2 * cr) * M + kb] = z[2 * s + 1].x;
-                PI[(2 * cr + 1) * M + kb] = z[2 * s + 1].y;
+                PI[(2 * cr) * PP + ka] = z[2 * s].x;
+                PI[(2 * cr + 1) * PP + ka] = z[2 * s].y;
+                PI[(2 * cr) * PP + kb] = z[2 * s + 1].x;
+                PI[(2 * cr + 1) * PP + kb] = z[2 * s + 1].y;
             }
             lds_barrier();
             // ---- dim 1: columns 2cc, 2cc + 1 as one complex line -------------------------------------------
@@ -942,7 +947,7 @@ __global__ __launch_bounds__((1 << L) / 2 * (1 << L) / 8) void k_plane8(const Sp
             for (int i = 0; i < 8; ++i) {
                 const int n = stage_in_pos<L, R0>(jc, i);
                 const int k = n < M / 2 ? 2 * n : 2 * (M - 1 - n) + 1;
-                z[i] = *reinterpret_cast<const double2*>(&PI[k * M + 2 * cc]);
+                z[i] = *reinterpret_cast<const double2*>(&PI[k * PP + 2 * cc]);
             }
             stages_from<L, R0, 1, false, false, true>(z, jc, Xc, cxc, tw);   // its first barrier ends the image reads
 #pragma unroll
@@ -969,15 +974,15 @@ __global__ __launch_bounds__((1 << L) / 2 * (1 << L) / 8) void k_plane8(const Sp
             for (int i = 0; i < 8; ++i) {
                 const int n = stage_out_pos<L, LS::R, LS::NS>(jc, i);
                 const int k = n < M / 2 ? 2 * n : 2 * (M - 1 - n) + 1;
-                *reinterpret_cast<double2*>(&PI[k * M + 2 * cc]) = z[i];
+                *reinterpret_cast<double2*>(&PI[k * PP + 2 * cc]) = z[i];
             }
             lds_barrier();
             // ---- dim 0 inverse: rows 2cr, 2cr + 1 -----------------------------------------------------------
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int k = jr + s * TPL, kb = k ? M - k : M / 2;
-                z[2 * s] = make_double2(PI[(2 * cr) * M + k], PI[(2 * cr + 1) * M + k]);
-                z[2 * s + 1] = make_double2(PI[(2 * cr) * M + kb], PI[(2 * cr + 1) * M + kb]);
+                z[2 * s] = make_double2(PI[(2 * cr) * PP + k], PI[(2 * cr + 1) * PP + k]);
+                z[2 * s + 1] = make_double2(PI[(2 * cr) * PP + kb], PI[(2 * cr + 1) * PP + kb]);
             }
             lds_barrier();   // every image read before the exchange buffer (same LDS) is written
 #pragma unroll
