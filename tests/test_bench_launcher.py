@@ -78,3 +78,18 @@ def test_bounded_agreement_after_a_slab_failure():
     assert out[0].startswith("none") and float(out[0].split()[-1]) < 7.0
     out = _two_ranks(stall=False)
     assert out[0].startswith("agreed") and "[2.0]" in out[0]
+
+
+def test_cpu_baseline_cores_follow_affinity_and_cgroup_quota(monkeypatch):
+    """cpu_baseline's threads: the affinity mask capped by cgroup v2 cpu.max (the GPU box grants 16 of 256)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(256)))
+    monkeypatch.setattr(bench, "_cgroup_cpu_max", lambda: "1600000 100000")
+    assert bench._usable_cores() == 16
+    monkeypatch.setattr(bench, "_cgroup_cpu_max", lambda: "max 100000")
+    assert bench._usable_cores() == 256
+    monkeypatch.setattr(bench, "_cgroup_cpu_max", lambda: None)
+    assert bench._usable_cores() == 256
+    monkeypatch.setattr(bench, "_cgroup_cpu_max", lambda: "50000 100000")   # half a CPU: at least one thread
+    assert bench._usable_cores() == 1
