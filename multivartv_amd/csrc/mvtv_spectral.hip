@@ -466,11 +466,28 @@ __device__ __forceinline__ int stage_out_pos(int j, int i) {
     return (b / NS) * NS * R + (b % NS) + r * NS;
 }
 
+// Barrier policies of the FFT exchanges: 0 __syncthreads, 1 LDS-only workgroup barrier (lds_barrier: global loads
+// issued before the stages stay in flight), 2 the wave alone — for tiles where every complex line's threads are one
+// wave's lanes (d = 0 passes with m / 8 <= 64 threads per line), whose exchange slots no other wave touches: a
+// wave's LDS accesses complete in issue order, so only the compiler must not move them across the point
+template <int BAR>
+__device__ __forceinline__ void xbar() {
+    if constexpr (BAR == 0) {
+        __syncthreads();
+    } else if constexpr (BAR == 1) {
+        lds_barrier();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
+}
+
 // Stages after the first (the first is peeled: its input comes from HBM or the caller's LDS).
 // STAGE counts radix-8 stages done after R0. Writes the outputs of stage NS_IN's butterflies
-// to LDS, then (if more stages remain) reads the next stage's inputs.
-// LDSB: LDS-only barriers (lds_barrier), so global loads issued before the stages stay in flight
-template <int L, int R, int NS, bool INV, bool LAST_TO_REGS, bool LDSB = false>
+// to LDS, then (if more stages remain) reads the next stage's inputs. BAR: the barrier policy (xbar); true (1):
+// LDS-only barriers (lds_barrier), so global loads issued before the stages stay in flight
+template <int L, int R, int NS, bool INV, bool LAST_TO_REGS, int BAR = 0>
 __device__ __forceinline__ void stages_from(double2* z, int j, double2* X, int cx, const double2* __restrict__ tw) {
     using S = spec8::Shape<L>;
     stage_compute<L, R, NS, INV>(z, j, tw);
@@ -478,16 +495,14 @@ __device__ __forceinline__ void stages_from(double2* z, int j, double2* X, int c
     if constexpr (NS_NEXT == S::M && LAST_TO_REGS) {
         return;   // caller stores z (output positions stage_out_pos<L, R, NS>)
     } else {
-        if constexpr (LDSB) lds_barrier();   // everyone has read this stage's inputs
-        else __syncthreads();
+        xbar<BAR>();   // everyone has read this stage's inputs
 #pragma unroll
         for (int i = 0; i < 8; ++i) X[spec8::slot(stage_out_pos<L, R, NS>(j, i), cx)] = z[i];
-        if constexpr (LDSB) lds_barrier();
-        else __syncthreads();
+        xbar<BAR>();
         if constexpr (NS_NEXT < S::M) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, 8>(j, i), cx)];
-            stages_from<L, 8, NS_NEXT, INV, LAST_TO_REGS, LDSB>(z, j, X, cx, tw);
+            stages_from<L, 8, NS_NEXT, INV, LAST_TO_REGS, BAR>(z, j, X, cx, tw);
         }
     }
 }
@@ -524,6 +539,9 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
         }
     }
     constexpr int M = S::M, TPL = S::TPL, NCL = S::NCL;
+    // d = 0 with <= 64 threads per complex line: each line's exchanges stay inside one wave (no workgroup barrier;
+    // MID keeps them: its line constants are shared)
+    constexpr int BAR = (D0 && TPL <= 64 && 64 % TPL == 0 && MODE != SPEC_MID) ? 2 : 0;
     __shared__ double2 buf[NCL * S::LP];
     __shared__ double lc0[2 * NCL], lc1[2 * NCL];
     const int t = threadIdx.x;
@@ -658,7 +676,7 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
                 X[spec8::slot(n, cx)] = make_double2(xa.x, xb.x);
                 X[spec8::slot(M - 1 - n, cx)] = make_double2(xa.y, xb.y);
             }
-            __syncthreads();
+            xbar<BAR>();
 #pragma unroll
             for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, R0>(j, i), cx)];
         } else {
@@ -669,7 +687,7 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
                 z[i] = ld2(k);
             }
         }
-        stages_from<L, R0, 1, false, false>(z, j, X, cx, tw);   // natural-order spectrum in LDS
+        stages_from<L, R0, 1, false, false, BAR>(z, j, X, cx, tw);   // natural-order spectrum in LDS
     }
 
     // ---- spectrum <-> DCT coefficients for the pairs (k, M-k); k = 0 also takes M/2 -------------
@@ -735,7 +753,7 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
         }
     }
     if (MODE == SPEC_FWD) return;
-    __syncthreads();
+    xbar<BAR>();
 
     // ---- inverse FFT, natural in; the last stage's outputs go straight to HBM, un-permuted ------
     {
@@ -744,7 +762,7 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
         for (int i = 0; i < 8; ++i) z[i] = X[spec8::slot(stage_in_pos<L, R0>(j, i), cx)];
         if (D0) {
             // contiguous lines: the output goes through LDS so (x[2n], x[2n+1]) leave as one 16-B store
-            stages_from<L, R0, 1, true, false>(z, j, X, cx, tw);
+            stages_from<L, R0, 1, true, false, BAR>(z, j, X, cx, tw);
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
                 const int n = j + s4 * TPL;
@@ -800,6 +818,7 @@ __global__ __launch_bounds__((1 << L) / 2 * (1 << L) / 8) void k_plane8(const Sp
     using S = spec8::Shape<L>;
     constexpr int M = S::M, TPL = S::TPL, NCL = M / 2, R0 = S::R0;
     static_assert(L >= 4 && L <= 7, "the plane must fit the exchange buffer of one workgroup");
+    static_assert(TPL <= 64 && 64 % TPL == 0, "a row pair's threads are lanes of one wave (xbar<2> on the rows)");
     // plane image pitch PP = M + M / 16 doubles (18 at M = 16): a wave's row accesses (8-B words, TPL = M / 8
     // lanes per row, 8 rows a wave at M = 64, 4 at 128) then start 16 PP bytes apart = M bytes mod 256, so the rows
     // of one wave instruction fall on different LDS banks; with pitch M every row started on bank 0 (rows 2 KB
@@ -926,10 +945,12 @@ __global__ __launch_bounds__((1 << L) / 2 * (1 << L) / 8) void k_plane8(const Sp
                 Xr[spec8::slot(M - 1 - n, cxr)] = make_double2(xv[0].y, xv[1].y);
             }
             if (en < nplanes) issue(en);
-            lds_barrier();
+            // a row pair's 16 threads are lanes of one wave and its exchange slots are that wave's alone: the row
+            // transforms sync the wave only (xbar<2>); the plane image and the columns need the workgroup
+            xbar<2>();
 #pragma unroll
             for (int i = 0; i < 8; ++i) z[i] = Xr[spec8::slot(stage_in_pos<L, R0>(jr, i), cxr)];
-            stages_from<L, R0, 1, false, false, true>(z, jr, Xr, cxr, tw);   // natural-order spectrum in X
+            stages_from<L, R0, 1, false, false, 2>(z, jr, Xr, cxr, tw);   // natural-order spectrum in X
 #pragma unroll
             for (int s = 0; s < 4; ++s) fwd_coeff(Xr, cxr, jr + s * TPL, z[2 * s], z[2 * s + 1]);
             lds_barrier();   // every spectrum read before the plane image (same LDS) is written
@@ -987,10 +1008,10 @@ __global__ __launch_bounds__((1 << L) / 2 * (1 << L) / 8) void k_plane8(const Sp
             lds_barrier();   // every image read before the exchange buffer (same LDS) is written
 #pragma unroll
             for (int s = 0; s < 4; ++s) inv_spectrum(Xr, cxr, jr + s * TPL, z[2 * s], z[2 * s + 1]);
-            lds_barrier();
+            xbar<2>();   // the row transforms: one wave's slots (as forward)
 #pragma unroll
             for (int i = 0; i < 8; ++i) z[i] = Xr[spec8::slot(stage_in_pos<L, R0>(jr, i), cxr)];
-            stages_from<L, R0, 1, true, false, true>(z, jr, Xr, cxr, tw);   // output through X
+            stages_from<L, R0, 1, true, false, 2>(z, jr, Xr, cxr, tw);   // output through X
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
                 const int n = jr + s4 * TPL;
