@@ -674,6 +674,9 @@ mvtv_status ensure_state(mvtv_problem* P) {
 
 }  // namespace
 
+// the slab loop's ranks pick their z ping-pong pair the same way (mvtv_slab.cpp)
+mvtv_status zpair_pick(mvtv_problem* P, bool track_theta, bool twin) { return pick_zpair(P, track_theta, twin); }
+
 // =================================================================================== C ABI
 extern "C" {
 

@@ -192,3 +192,6 @@ struct mvtv_problem {
         return MVTV_OK;
     }
 };
+
+// timed choice of the fused 3-D kernel's z ping-pong buffer pair, once per problem (mvtv_capi.cpp pick_zpair)
+mvtv_status zpair_pick(mvtv_problem* P, bool track_theta, bool twin);

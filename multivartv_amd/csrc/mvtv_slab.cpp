@@ -830,6 +830,11 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     const bool solo = G == 1 && !(force && std::atoi(force) != 0);
     if (!solo && !P->slab_iface) MVTV_TRY(alloc(&P->slab_iface, 16 * size_t(sg.lines)));
     if (pingpong && !P->edges2) MVTV_TRY(alloc(&P->edges2, size_t(P->g.nb) * P->g.N));
+    // the z ping-pong pair by timed probes, as one GPU's loop does (its first fused run, slabs of >= 2^24 nodes):
+    // the fused pass's time depends on which physical buffers z moves between (slab world 1 at 512^3: 3.41 ms
+    // on the allocation-order pair against 3.17 for the one-GPU loop in the same round-4 sweep); a rank-local
+    // choice, no collective. The state is zeroed below
+    if (fused && !P->zpicked) MVTV_TRY(zpair_pick(P, false, twin));
     const size_t nodes = P->g.N, ebytes = size_t(P->g.nb) * nodes * sizeof(double);
 
     // ---- initial state: theta0 everywhere (ghosts included), u0 = 0, g_alpha = D^T D theta0 -----------
