@@ -122,6 +122,9 @@ def parse():
                          "metric) with the independent fits per GPU (weak scaling) reported beside it. "
                          "independent / slab: only that one")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--mesh", type=str, default="",
+                    help="--mode slab: an explicit mesh 'm0,m1,...' instead of size^dims (e.g. 512,512,64: one rank's "
+                         "share of 512^3 at 8 GPUs, run at world 1 with MVTV_SLAB_DISTRIBUTED=1)")
     ap.add_argument("--slab-ranks", type=int, default=1,
                     help="--mode slab without torchrun: ranks of an in-process rehearsal on one GPU (1: RCCL, one rank)")
     ap.add_argument("--transport", choices=["auto", "rccl", "ipc"], default="auto",
@@ -346,7 +349,7 @@ def slab_main(a, D, comm=None):
     World size 1: --slab-ranks R > 1 rehearses an R-rank decomposition on the one GPU with the in-process
     loopback transport; R = 1 runs the slab loop over a one-rank RCCL communicator. Returns rank 0's line."""
     from multivartv_amd import slab
-    m = [a.size] * a.dims
+    m = [int(v) for v in a.mesh.split(",")] if a.mesh else [a.size] * a.dims
     lam = a.lam
     deltas = [(1.0 + 2e-4) / v for v in m]
     R = max(1, a.slab_ranks)
@@ -404,8 +407,8 @@ def slab_main(a, D, comm=None):
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(g_elapsed / a.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: towers + 0.5 N(0,1) (splitmix64/Box-Muller, seed 0x4D565456), O = I",
-        "config": {"workload": f"{a.dims}D {a.size}^{a.dims} fp64 mesh-TV ADMM, variant B, lambda={lam}, one mesh "
-                               f"slab-decomposed along dim {a.dims - 1} over {nranks} ranks", "mesh": m,
+        "config": {"workload": f"{len(m)}D {'x'.join(map(str, m))} fp64 mesh-TV ADMM, variant B, lambda={lam}, one mesh "
+                               f"slab-decomposed along dim {len(m) - 1} over {nranks} ranks", "mesh": m,
                    "theta_solver": "spectral (local transforms; the last dimension's line solves substructured "
                                    "over the ranks)" if distributed else "spectral (one rank: the whole lines local)",
                    "parallelism": f"slab x{nranks} ({transport}: halo planes, "
