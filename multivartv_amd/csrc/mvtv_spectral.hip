@@ -2712,18 +2712,20 @@ namespace tris {
 constexpr int NSMAX = 64, TQ = 16;
 }
 
-template <int PHASE, int SMAX>
+// TQ lines per workgroup (16: 128-B rows; 64: 512-B rows, one full run per wave load), NS >= nseg segments (the LDS
+// of the interface arrays is sized by it: with NS = 64 for every block, a 4-segment block of a G = 8 rank at 512^3
+// took 48 KB for one wave, 3 waves per CU, and moved 0.9-1.5 TB/s)
+template <int PHASE, int SMAX, int TQ = tris::TQ, int NS = tris::NSMAX>
 __global__ __launch_bounds__(1024) void k_tris(const SpecArgs a, int sl, int nseg, double* __restrict__ x,
                                                double* __restrict__ coef, const double* __restrict__ lr,
                                                uint32_t chunk, int lo_ext, int hi_ext, double scale) {
-    constexpr int TQ = tris::TQ, NS = tris::NSMAX;
     double sigma = a.sigma;
     if (a.skip && *a.skip) return;
     if (a.ctl) {
         if (a.ctl->done) return;
         sigma = a.ctl->sigma;
     }
-    __shared__ double t_id[SMAX][TQ], t_e[SMAX][TQ], t_h[SMAX][TQ], t_k[SMAX][TQ];
+    __shared__ double t_id[SMAX][TQ], t_h[SMAX][TQ], t_k[SMAX][TQ];   // e_i = A id_i: recomputed, not stored
     __shared__ double s_a[TQ];
     __shared__ double s_u[NS][TQ], s_v[NS][TQ], s_bu[NS][TQ];
     // phase 1: the forward-eliminated u of the L- and R-response tracks; phase 3: the slopes of v_j on u_{j+1}
@@ -2771,14 +2773,13 @@ __global__ __launch_bounds__(1024) void k_tris(const SpecArgs a, int sl, int nse
             e = A * id;
             h = -A * h * id;
             t_id[i][c] = id;
-            t_e[i][c] = e;
             t_h[i][c] = h;
         }
-        double H = t_h[sl - 1][c], K = -t_e[sl - 1][c];
+        double H = t_h[sl - 1][c], K = -(A * t_id[sl - 1][c]);
         t_k[sl - 1][c] = K;
 #pragma unroll 1
         for (int i = sl - 2; i >= 0; --i) {
-            const double ei = t_e[i][c];
+            const double ei = A * t_id[i][c];
             H = t_h[i][c] - ei * H;
             K = -ei * K;
             t_h[i][c] = H;
@@ -2798,7 +2799,7 @@ __global__ __launch_bounds__(1024) void k_tris(const SpecArgs a, int sl, int nse
 #pragma unroll
         for (int i = SMAX - 1; i >= 0; --i) {
             if (i == sl - 1) last = g[i];
-            if (i < sl - 1) g[i] -= t_e[i][c] * g[i + 1];
+            if (i < sl - 1) g[i] -= (A * t_id[i][c]) * g[i + 1];
         }
         s_u[sj][c] = g[0];
         s_v[sj][c] = last;
@@ -2979,19 +2980,36 @@ hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, in
     tris_seg(n, &sl, &nseg);
     if (!tri_slab_ok(n) || chunk == 0 || a.nlines % chunk != 0)
         return hipErrorInvalidValue;
-    const dim3 grid((a.nlines + uint32_t(tris::TQ) - 1) / uint32_t(tris::TQ)), block(uint32_t(tris::TQ * nseg));
-    // segments of <= 16 rows (blocks up to 1024 planes) keep the row registers at 16
-    if (phase == 1 && sl <= 16)
-        klaunch((k_tris<1, 16>), grid, block, 0, s, a, sl, nseg, x, coef, lr, chunk, lo_ext, hi_ext, scale);
-    else if (phase == 1)
-        klaunch((k_tris<1, 32>), grid, block, 0, s, a, sl, nseg, x, coef, lr, chunk, lo_ext, hi_ext, scale);
-    else if (phase == 3 && sl <= 16)
-        klaunch((k_tris<3, 16>), grid, block, 0, s, a, sl, nseg, x, coef, lr, chunk, lo_ext, hi_ext, scale);
-    else if (phase == 3)
-        klaunch((k_tris<3, 32>), grid, block, 0, s, a, sl, nseg, x, coef, lr, chunk, lo_ext, hi_ext, scale);
-    else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
+    if (phase != 1 && phase != 3) return hipErrorInvalidValue;
+    // 64-line tiles with the segment arrays sized to the block (<= 16 segments: <= 1024 threads) where the lines
+    // fill >= 128 such workgroups; otherwise 16-line tiles sized for any block (<= 64 segments)
+    static const bool wide_off = probe_env("MVTV_TRIS_NARROW") != nullptr;
+    auto go = [&](auto kern, uint32_t tq) {
+        klaunch(kern, dim3((a.nlines + tq - 1) / tq), dim3(tq * uint32_t(nseg)), 0, s, a, sl, nseg, x, coef, lr, chunk,
+                lo_ext, hi_ext, scale);
+        return hipGetLastError();
+    };
+    if (!wide_off && nseg <= 16 && a.nlines >= 64u * 128u) {
+        // segments of <= 16 rows keep the row registers at 16 (blocks up to 256 planes here); <= 4 rows (blocks of
+        // <= 16 planes: a 4-D rank at G = 8) size the line constants for 4
+        const int ns = nseg <= 4 ? 4 : (nseg <= 8 ? 8 : 16);
+        if (sl <= 4 && ns == 4) return phase == 1 ? go(k_tris<1, 4, 64, 4>, 64u) : go(k_tris<3, 4, 64, 4>, 64u);
+        if (sl <= 16) {
+            if (phase == 1) {
+                if (ns == 4) return go(k_tris<1, 16, 64, 4>, 64u);
+                if (ns == 8) return go(k_tris<1, 16, 64, 8>, 64u);
+                return go(k_tris<1, 16, 64, 16>, 64u);
+            }
+            if (ns == 4) return go(k_tris<3, 16, 64, 4>, 64u);
+            if (ns == 8) return go(k_tris<3, 16, 64, 8>, 64u);
+            return go(k_tris<3, 16, 64, 16>, 64u);
+        }
+    }
+    const uint32_t tq = uint32_t(tris::TQ);
+    if (phase == 1 && sl <= 16) return go(k_tris<1, 16>, tq);
+    if (phase == 1) return go(k_tris<1, 32>, tq);
+    if (sl <= 16) return go(k_tris<3, 16>, tq);
+    return go(k_tris<3, 32>, tq);
 }
 
 hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint32_t chunk, int G, const AdmmCtl* ctl,
