@@ -30,6 +30,12 @@ inline const char* probe_env(const char* name) {
 #endif
 }
 
+// a probe switch: set to a non-zero number (probe builds only)
+inline bool probe_flag(const char* name) {
+    const char* e = probe_env(name);
+    return e && std::atoi(e) != 0;
+}
+
 // Unsigned 32-bit division by an invariant divisor (Granlund-Montgomery):
 // q = (umulhi(n, mul) + n) >> shift, evaluated with a 64-bit add so it holds for every n < 2^32.
 struct FastDiv {

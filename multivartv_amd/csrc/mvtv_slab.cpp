@@ -63,8 +63,15 @@ struct mvtv_comm {
     // a rank whose loop failed tells its peers, so that they fail instead of waiting for it (loopback, ipc; an
     // RCCL peer of a failed process is ended by the launcher)
     virtual void abort() {}
-    // called at the start of every mvtv_slab_run (the ipc transport drops its buffer mappings there)
-    virtual void run_begin() {}
+    // called at the start of every mvtv_slab_run (the ipc transport drops its buffer mappings there; RCCL splits off
+    // its second communicator there, a collective call every rank makes at the same point); non-OK: no second lane
+    virtual mvtv_status run_begin() { return MVTV_OK; }
+    // lanes: independent orderings of collectives, so the critical-path collectives (lane 0, issued on the compute
+    // stream) and the halos (lane 1, on the collectives stream) may run concurrently. RCCL: one communicator per
+    // lane (two ops of one communicator must not run at once on different streams); the loopback and ipc groups match
+    // their transfers in host program order, which every rank shares, so both lanes are the same group there
+    virtual int lanes() const { return 2; }
+    virtual void set_lane(int) {}
 };
 
 namespace {
@@ -82,6 +89,7 @@ struct RcclApi {
     ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                               hipStream_t) = nullptr;
     const char* (*GetErrorString)(ncclResult_t) = nullptr;
+    ncclResult_t (*CommSplit)(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*) = nullptr;
     std::string path;   // the file the functions came from
 };
 
@@ -111,6 +119,7 @@ mvtv_status rccl_api(RcclApi** out) {
             sym(api.GroupEnd, "ncclGroupEnd");
             sym(api.AllReduce, "ncclAllReduce");
             sym(api.GetErrorString, "ncclGetErrorString");
+            sym(api.CommSplit, "ncclCommSplit");
             Dl_info info{};
             if (api.GetUniqueId && dladdr(reinterpret_cast<void*>(api.GetUniqueId), &info) && info.dli_fname)
                 api.path = info.dli_fname;
@@ -148,7 +157,28 @@ struct SelfCopy {
 struct RcclComm final : mvtv_comm {
     RcclApi* api_ = nullptr;
     ncclComm_t comm = nullptr;
+    ncclComm_t comm2 = nullptr;   // lane 1 (the halos), split off comm at the first run
+    bool split_tried = false;
+    int lane_ = 0;
+    ncclComm_t cur() const { return lane_ == 1 && comm2 ? comm2 : comm; }
+    mvtv_status run_begin() override {
+        lane_ = 0;
+        if (!split_tried) {   // every rank reaches this at its first run: a collective call in the same order
+            split_tried = true;
+            const char* e = std::getenv("MVTV_RCCL_ONE_COMM");
+            const bool off = e && std::atoi(e) != 0;
+            if (!off && api_->CommSplit) {
+                DeviceGuard dg(device);
+                if (api_->CommSplit(comm, 0, rank, &comm2, nullptr) != ncclSuccess) comm2 = nullptr;
+            }
+            if (!comm2 && !off) return fail(MVTV_HIP_ERROR, "RCCL: ncclCommSplit failed (one lane)");
+        }
+        return MVTV_OK;
+    }
+    int lanes() const override { return comm2 ? 2 : 1; }
+    void set_lane(int l) override { lane_ = l; }
     ~RcclComm() override {
+        if (comm2 && api_->CommDestroy) api_->CommDestroy(comm2);
         if (comm && api_->CommDestroy) api_->CommDestroy(comm);
         if (scratch) (void)hipFree(scratch);
         if (stream) (void)hipStreamDestroy(stream);
@@ -158,11 +188,11 @@ struct RcclComm final : mvtv_comm {
         return MVTV_OK;
     }
     mvtv_status send(const double* buf, size_t n, int peer, hipStream_t s) override {
-        NCCL_TRY(api_->Send(buf, n, ncclFloat64, peer, comm, s));
+        NCCL_TRY(api_->Send(buf, n, ncclFloat64, peer, cur(), s));
         return MVTV_OK;
     }
     mvtv_status recv(double* buf, size_t n, int peer, hipStream_t s) override {
-        NCCL_TRY(api_->Recv(buf, n, ncclFloat64, peer, comm, s));
+        NCCL_TRY(api_->Recv(buf, n, ncclFloat64, peer, cur(), s));
         return MVTV_OK;
     }
     mvtv_status end(hipStream_t) override {
@@ -170,7 +200,7 @@ struct RcclComm final : mvtv_comm {
         return MVTV_OK;
     }
     mvtv_status allreduce_sum(double* buf, size_t n, hipStream_t s) override {
-        NCCL_TRY(api_->AllReduce(buf, buf, n, ncclFloat64, ncclSum, comm, s));
+        NCCL_TRY(api_->AllReduce(buf, buf, n, ncclFloat64, ncclSum, cur(), s));
         return MVTV_OK;
     }
 };
@@ -440,7 +470,10 @@ struct IpcComm final : mvtv_comm {
     void abort() override {
         if (shm) shm->aborted.store(1);
     }
-    void run_begin() override { close_mappings(); }
+    mvtv_status run_begin() override {
+        close_mappings();
+        return MVTV_OK;
+    }
     // poll until pred() holds; false on abort or timeout
     template <class F>
     bool wait(F pred, const char* what, mvtv_status* st) {
@@ -716,6 +749,7 @@ mvtv_status mvtv_comm_allreduce_host(mvtv_comm* c, double* vals, int32_t n) {
     if (n == 0) return MVTV_OK;
     if (auto* ic = dynamic_cast<IpcComm*>(c)) return ic->size == 1 ? MVTV_OK : ic->allreduce_host_vals(vals, size_t(n));
     if (!dynamic_cast<RcclComm*>(c)) return fail(MVTV_BAD_ARG, "host all-reduce: RCCL or ipc communicators only");
+    c->set_lane(0);
     DeviceGuard dg(c->device);
     if (!c->stream) HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     if (!c->scratch) MVTV_TRY(alloc(&c->scratch, 64));
@@ -786,6 +820,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         double flags[9] = {P->f3d ? 1.0 : 0.0, P->g.eaos ? 1.0 : 0.0, P->e3d ? 1.0 : 0.0, double(sg.plane),
                            wd ? 1.0 : 0.0, P->wsum_own, P->wsum2_own, lines_ok ? 1.0 : 0.0, P->f4d ? 1.0 : 0.0};
         HIP_TRY(hipMemcpyAsync(P->red, flags, sizeof(flags), hipMemcpyHostToDevice, s));
+        C->set_lane(0);
         MVTV_TRY(C->allreduce_sum(P->red, 9, s));
         double sum[9];
         HIP_TRY(hipMemcpyAsync(sum, P->red, sizeof(sum), hipMemcpyDeviceToHost, s));
@@ -920,6 +955,14 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         return MVTV_OK;
     };
     bool zh_pending = false;   // a z halo was enqueued on sc that the next edge pass must wait for
+    // Collectives on the critical path (the line solves' two all-to-alls, every all-reduce) go on the compute
+    // stream itself, lane 0 of the transport, so no event hand-off between streams sits between a kernel and the
+    // collective that consumes its output (a rank's share at G = 8 showed ~20 us of idle GPU per hand-off, eight per
+    // iteration); the halos stay on sc, lane 1 (RCCL: a second communicator split off the first, so the two lanes may
+    // run at once), the z halo overlapping the next theta-solve. One lane (lanes() == 1, or MVTV_SLAB_CRIT_SC=1 in
+    // probe builds): every collective on sc with hand-offs, the round-4 schedule
+    const bool crit_s = !solo && C->lanes() >= 2 && !probe_flag("MVTV_SLAB_CRIT_SC");
+    auto lane = [&](int l) { C->set_lane(crit_s ? l : 0); };
 
     // edge plane e of buffer z (eaos: one contiguous run of nb * plane words; block-major: nb runs)
     auto edge_plane_xfer = [&](double* z, size_t e, int peer, bool is_send) -> mvtv_status {
@@ -934,17 +977,33 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         return MVTV_OK;
     };
     // all-to-all of k numbers per line: block r of `send` (k x chunk) -> rank r, rank r's -> block r of `recv`
-    auto a2a = [&](const double* send, double* recv, size_t k) -> mvtv_status {
+    auto a2a = [&](const double* send, double* recv, size_t k, hipStream_t st) -> mvtv_status {
         MVTV_TRY(C->begin());
-        for (int r = 0; r < G; ++r) MVTV_TRY(C->send(send + size_t(r) * k * ch, k * ch, r, sc));
-        for (int r = 0; r < G; ++r) MVTV_TRY(C->recv(recv + size_t(r) * k * ch, k * ch, r, sc));
-        return C->end(sc);
+        for (int r = 0; r < G; ++r) MVTV_TRY(C->send(send + size_t(r) * k * ch, k * ch, r, st));
+        for (int r = 0; r < G; ++r) MVTV_TRY(C->recv(recv + size_t(r) * k * ch, k * ch, r, st));
+        return C->end(st);
+    };
+    // a critical-path all-to-all / all-reduce: on s (lane 0), or on sc between hand-offs (one lane)
+    auto crit_a2a = [&](const double* send, double* recv, size_t k, int e_in, int e_out) -> mvtv_status {
+        lane(0);
+        if (crit_s) return a2a(send, recv, k, s);
+        MVTV_TRY(handoff(ev[e_in], s, sc));
+        MVTV_TRY(a2a(send, recv, k, sc));
+        return handoff(ev[e_out], sc, s);
+    };
+    auto crit_allreduce = [&](double* buf, size_t n) -> mvtv_status {
+        lane(0);
+        if (crit_s) return C->allreduce_sum(buf, n, s);
+        MVTV_TRY(handoff(ev[EV_RED], s, sc));
+        MVTV_TRY(C->allreduce_sum(buf, n, sc));
+        return handoff(ev[EV_AR], sc, s);
     };
 
     // ghost planes of a node vector v (theta, or PCG's search direction): the first and last owned planes to
     // the neighbours, on sc, handed the data by event e and recording EV_THD when done
     auto halo = [&](double* v, hipEvent_t e) -> mvtv_status {
         MVTV_TRY(handoff(e, s, sc));
+        lane(1);
         MVTV_TRY(C->begin());
         if (rk > 0) MVTV_TRY(C->send(v + first_owned, pl, rk - 1, sc));
         if (rk < G - 1) MVTV_TRY(C->send(v + last_owned, pl, rk + 1, sc));
@@ -992,13 +1051,9 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         } else {
             HIP_TRY(launch_tri_slab(P->spec, og, s, 1, z, co_send, nullptr, uint32_t(ch), rk > 0, rk < G - 1, scale,
                                     nullptr, sigma, w0, skip));
-            MVTV_TRY(handoff(ev[EV_CO], s, sc));
-            MVTV_TRY(a2a(co_send, co_recv, 6));
-            MVTV_TRY(handoff(ev[EV_COD], sc, s));
+            MVTV_TRY(crit_a2a(co_send, co_recv, 6, EV_CO, EV_COD));
             HIP_TRY(launch_tri_iface(s, co_recv, lr_send, uint32_t(ch), G, nullptr, skip));
-            MVTV_TRY(handoff(ev[EV_LR], s, sc));
-            MVTV_TRY(a2a(lr_send, lr_recv, 2));
-            MVTV_TRY(handoff(ev[EV_LRD], sc, s));
+            MVTV_TRY(crit_a2a(lr_send, lr_recv, 2, EV_LR, EV_LRD));
             HIP_TRY(launch_tri_slab(P->spec, og, s, 3, z, nullptr, lr_recv, uint32_t(ch), rk > 0, rk < G - 1, scale,
                                     nullptr, sigma, w0, skip));
         }
@@ -1011,11 +1066,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     double* pred = P->red + 8;
     auto global_step = [&](int nparts, int nr, int op, double rtol2, int maxit) -> mvtv_status {
         HIP_TRY(launch_finalize(s, P->partials, nparts, nr, 0, 0, pred, P->st));
-        if (!solo) {
-            MVTV_TRY(handoff(ev[EV_RED], s, sc));
-            MVTV_TRY(C->allreduce_sum(pred, size_t(nr), sc));
-            MVTV_TRY(handoff(ev[EV_AR], sc, s));
-        }
+        if (!solo) MVTV_TRY(crit_allreduce(pred, size_t(nr)));
         HIP_TRY(launch_finalize(s, pred, 1, nr, 0, op, nullptr, P->st, rtol2, maxit));
         return MVTV_OK;
     };
@@ -1118,13 +1169,9 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
                 HIP_TRY(launch_tri_slab(P->spec, og, s, 1, th, co_send, nullptr, uint32_t(ch), rk > 0, rk < G - 1, scale,
                                         P->ctl));
                 P->tstop(h);
-                MVTV_TRY(handoff(ev[EV_CO], s, sc));
-                MVTV_TRY(a2a(co_send, co_recv, 6));
-                MVTV_TRY(handoff(ev[EV_COD], sc, s));
+                MVTV_TRY(crit_a2a(co_send, co_recv, 6, EV_CO, EV_COD));
                 HIP_TRY(launch_tri_iface(s, co_recv, lr_send, uint32_t(ch), G, P->ctl));
-                MVTV_TRY(handoff(ev[EV_LR], s, sc));
-                MVTV_TRY(a2a(lr_send, lr_recv, 2));
-                MVTV_TRY(handoff(ev[EV_LRD], sc, s));
+                MVTV_TRY(crit_a2a(lr_send, lr_recv, 2, EV_LR, EV_LRD));
                 h = P->tstart(MVTV_K_DCT);
                 HIP_TRY(launch_tri_slab(P->spec, og, s, 3, th, nullptr, lr_recv, uint32_t(ch), rk > 0, rk < G - 1, scale,
                                         P->ctl));
@@ -1183,6 +1230,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
                 HIP_TRY(fill_twins(P->g, P->order, s, zn, uint32_t(last_owned), uint32_t(last_owned + pl)));
             if (!solo) {
                 MVTV_TRY(handoff(ev[EV_EDGE], s, sc));
+                lane(1);
                 MVTV_TRY(C->begin());
                 if (rk < G - 1) MVTV_TRY(edge_plane_xfer(zn, last_owned / pl, rk + 1, true));
                 if (rk > 0) MVTV_TRY(edge_plane_xfer(zn, 0, rk - 1, false));
@@ -1209,6 +1257,7 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
             // D^T at the first owned plane reads the new z of plane zb-1 (rank-1's last plane)
             if (!solo) {
                 MVTV_TRY(handoff(ev[EV_EDGE], s, sc));
+                lane(1);
                 MVTV_TRY(C->begin());
                 if (rk < G - 1) MVTV_TRY(edge_plane_xfer(P->edges, last_owned / pl, rk + 1, true));
                 if (rk > 0) MVTV_TRY(edge_plane_xfer(P->edges, 0, rk - 1, false));
@@ -1229,15 +1278,15 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
             HIP_TRY(launch_finalize(s, P->partials, npg, GR_N, 0, 0, P->red + ER_N, P->st, 0.0, 0, P->ctl));
         }
         // -- global sums, then every rank's identical decision
-        if (!solo) {
-            MVTV_TRY(handoff(ev[EV_RED], s, sc));
-            MVTV_TRY(C->allreduce_sum(P->red, ER_N + GR_N, sc));
-            MVTV_TRY(handoff(ev[EV_AR], sc, s));
-        }
+        if (!solo) MVTV_TRY(crit_allreduce(P->red, ER_N + GR_N));
         HIP_TRY(launch_admm_control(s, P->ctl, P->red));
         // -- z halo for the next iteration's chunk-start recompute (fused): rank-1's last plane of z_new, on sc
         //    (z_new is complete: EV_RED was recorded after the fused pass) while s starts the next solve
         if (fused && !solo) {
+            // z_new is complete on s (the fused pass and its sums precede this point); with the all-reduce on sc
+            // its hand-off carried that, on s (crit_s) this one does
+            if (crit_s) MVTV_TRY(handoff(ev[EV_EDGE], s, sc));
+            lane(1);
             MVTV_TRY(C->begin());
             if (rk < G - 1) MVTV_TRY(edge_plane_xfer(zn, last_owned / pl, rk + 1, true));
             if (rk > 0) MVTV_TRY(edge_plane_xfer(zn, 0, rk - 1, false));
@@ -1311,7 +1360,8 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
 extern "C" mvtv_status mvtv_slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, double lambda,
                                      double theta0, double rho0, mvtv_admm_stats* stats) {
     if (!C) return fail(MVTV_BAD_ARG, "null communicator");
-    C->run_begin();
+    (void)C->run_begin();   // a failed split leaves one lane (lanes() == 1): the loop then keeps every collective
+                            // on the collectives stream, the round-4 schedule
     const mvtv_status st =
         (!P || !opts) ? fail(MVTV_BAD_ARG, "null argument") : slab_run(P, C, opts, lambda, theta0, rho0, stats);
     if (st != MVTV_OK && st != MVTV_MAXITER) C->abort();
