@@ -217,7 +217,9 @@ typedef struct mvtv_slab_desc {
 } mvtv_slab_desc;
 typedef struct mvtv_comm mvtv_comm;
 mvtv_status mvtv_problem_create_slab(const mvtv_problem_desc* desc, const mvtv_slab_desc* slab, mvtv_problem** out);
-/* RCCL transport (one process per GPU): rank 0 makes the id, every rank passes the same 128 bytes */
+/* RCCL transport (one process per GPU): rank 0 makes the id, every rank passes the same 128 bytes. The first
+ * mvtv_slab_run on a communicator splits off a second RCCL communicator (ncclCommSplit, collective) for the halos, so
+ * they can run beside the critical-path collectives issued on the problem's stream; MVTV_RCCL_ONE_COMM=1 keeps one */
 mvtv_status mvtv_comm_unique_id(uint8_t* id128);
 mvtv_status mvtv_comm_create_rccl(const uint8_t* id128, int32_t nranks, int32_t rank, int32_t device, mvtv_comm** out);
 /* in-process loopback group of nranks handles (comms[0..nranks-1]): each rank's mvtv_slab_run on its own
