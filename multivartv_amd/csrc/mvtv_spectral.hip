@@ -76,6 +76,7 @@ struct SpecArgs {
     FastDiv fper[8], fL[8];   // stage s: butterflies per line (m / rad[s]) and the span before it
     const uint32_t* perm;     // position of sample k in the digit-reversed Makhoul order (this dim)
     int32_t xcd;              // k_dct8: tiles dealt to the XCDs in contiguous runs (grid a multiple of 8)
+    int32_t xrun;             // k_dctg / k_dctm / k_dctb / k_dctb8 / k_trig: the same for any grid (xcd_run)
     PcgFuse pf;               // k_dct8 PC = 1 / 2: the PCG vector work of the preconditioner's d = 0 passes
     int32_t fold;             // FORMB from the folded s (k_dct8, ctl): b = in + fold_ka ga [+ fold_kb gb if ctl->fix]
     // Bluestein lengths (k_dctb; L = log2 M then, tw = the length-M FFT twiddles): the chirp c[n] = e^{-i pi n^2/m}
@@ -84,6 +85,15 @@ struct SpecArgs {
     const double2* bvf;
     const double2* bvi;
 };
+
+// Workgroup b of G runs on XCD b % 8. The tile it takes when the tiles are dealt to the XCDs in contiguous runs, for
+// any G (XCD x takes G / 8 tiles, one more when x < G % 8): the tiles that share the 128-B lines of a strided row —
+// a line pitch that is not a multiple of 128 B (500, 251, 100 points ...) — are then read through one L2 instead of
+// two, where round-robin dealing put neighbouring tiles on different XCDs and each straddled line came from HBM twice
+__device__ __forceinline__ uint32_t xcd_run(uint32_t b, uint32_t G) {
+    const uint32_t x = b & 7u, i = b >> 3, q = G >> 3, r = G & 7u;
+    return x * q + (x < r ? x : r) + i;
+}
 
 enum SpecMode { SPEC_FWD = 0, SPEC_INV = 1, SPEC_MID = 2 };
 
@@ -1406,7 +1416,7 @@ __global__ __launch_bounds__(dctg::NT) __attribute__((amdgpu_waves_per_eu(4))) v
     const int m = int(a.m[a.d]);
     const int tq = a.tq, ncl = tq >> 1;
     const int LP = m + spec::PAD;
-    const uint32_t q0 = blockIdx.x * uint32_t(tq);
+    const uint32_t q0 = (a.xrun ? xcd_run(blockIdx.x, gridDim.x) : blockIdx.x) * uint32_t(tq);
 
     if (MODE == SPEC_MID && threadIdx.x < uint32_t(tq)) {
         const uint32_t q = a.q_off + q0 + threadIdx.x;
@@ -1643,7 +1653,7 @@ __global__ __launch_bounds__(dctm::Shape<M>::NT) void k_dctm(const SpecArgs a) {
     const int t = threadIdx.x;
     const int j = D0 ? (t % T) : (t / NCL);
     const int c = D0 ? (t / T) : (t % NCL);
-    const uint32_t q0 = blockIdx.x * uint32_t(dctm::TQ);
+    const uint32_t q0 = (a.xrun ? xcd_run(blockIdx.x, gridDim.x) : blockIdx.x) * uint32_t(dctm::TQ);
     const int la = 2 * c;
     const bool va = q0 + uint32_t(la) < a.nlines;   // lines come in pairs: nlines is even (launcher)
     double2* X = buf + c * S::LP;
@@ -1921,7 +1931,7 @@ __global__ __launch_bounds__(dctb::NT) void k_dctb(const SpecArgs a) {
     const int L = a.L, M = 1 << L;     // a.L = log2 M here
     const int tq = a.tq, ncl = tq >> 1, lncl = __ffs(ncl) - 1;
     const int LP = M + spec::PAD;
-    const uint32_t q0 = blockIdx.x * uint32_t(tq);
+    const uint32_t q0 = (a.xrun ? xcd_run(blockIdx.x, gridDim.x) : blockIdx.x) * uint32_t(tq);
     const double2* __restrict__ chirp = a.bchirp;   // c[n] = e^{-i pi n^2 / m} (s = -1), n < m
 
     if (MODE == SPEC_MID && threadIdx.x < uint32_t(tq)) {   // c0 + c1 lam_d(k) per line, as k_dctg
@@ -2129,7 +2139,7 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dctb8(const Spe
     const int t = threadIdx.x;
     const int j = D0 ? (t % TPL) : (t / NCL);
     const int c = D0 ? (t / TPL) : (t % NCL);
-    const uint32_t q0 = blockIdx.x * uint32_t(TQW);
+    const uint32_t q0 = (a.xrun ? xcd_run(blockIdx.x, gridDim.x) : blockIdx.x) * uint32_t(TQW);
     const int la = 2 * c, lb = 2 * c + 1;
     const bool va = q0 + uint32_t(la) < a.nlines, vb = q0 + uint32_t(lb) < a.nlines;
     double2* const X = buf + c * S::LP;
@@ -2547,27 +2557,34 @@ __global__ __launch_bounds__((tri::Shape<L, SEG, TQL>::NT)) void k_tri(const Spe
         __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + (uint32_t(i) << a.ls));
 }
 
-// k_trig: the same solve for any line length m = NSEG * s (segment length s <= 32 chosen at launch,
-// NSEG <= 64) and any line stride (FastDiv addressing): the last-dimension pass of the mixed-radix
-// meshes. Rows past s in the fixed-size register arrays are predicated off.
+// k_trig: the same solve for any line length m = (NSEG - 1) * s + sr (segment length s <= SMAX chosen at launch,
+// NSEG <= NS, the last segment sr <= s rows) and any line stride (FastDiv addressing): the last-dimension pass of
+// the mixed-radix and prime-length meshes. Rows past a segment's length in the fixed-size register arrays are
+// predicated off. A shorter last segment (RG: m has no divisor in the segment range, e.g. a prime length) shares
+// the forward-elimination constants id_i, h_i (they depend on the row's distance from the segment's top only) and
+// has its own backward responses H, K (from its own last row). TQ lines per workgroup: 16 (128-B rows,
+// any block of <= 64 segments) or, where the block fits 1024 threads, 32 / 64 (256- / 512-B rows) with the segment
+// arrays sized to the block (k_tris's tiles; e_i = A id_i recomputed, not stored: the same double)
 namespace trig {
 constexpr int SMAX = 32, NSMAX = 64, TQ = 16;
 }
 
-__global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nseg) {
-    constexpr int TQ = trig::TQ, SMAX = trig::SMAX;
+template <int SMAX, int TQ, int NS, bool RG = false>
+__global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nseg, int sr) {
     double sigma = a.sigma;
     if (a.skip && *a.skip) return;
     if (a.ctl) {
         if (a.ctl->done) return;
         sigma = a.ctl->sigma;
     }
-    __shared__ double t_id[SMAX][TQ], t_e[SMAX][TQ], t_h[SMAX][TQ], t_k[SMAX][TQ];
+    __shared__ double t_id[SMAX][TQ], t_h[SMAX][TQ], t_k[SMAX][TQ];
     __shared__ double s_a[TQ];
-    __shared__ double s_u[trig::NSMAX][TQ], s_v[trig::NSMAX][TQ], s_bu[trig::NSMAX][TQ], s_bv[trig::NSMAX][TQ];
+    __shared__ double s_u[NS][TQ], s_v[NS][TQ], s_bu[NS][TQ], s_bv[NS][TQ];
+    __shared__ double t_h2[RG ? SMAX : 1][TQ], t_k2[RG ? SMAX : 1][TQ];   // the last segment's H, K
     const int t = threadIdx.x, c = t % TQ, sj = t / TQ;
+    const int ln = (RG && sj == nseg - 1) ? sr : sl;   // this thread's segment length
     const uint32_t m = a.m[a.d];
-    const uint32_t q0 = blockIdx.x * uint32_t(TQ);
+    const uint32_t q0 = (a.xrun ? xcd_run(blockIdx.x, gridDim.x) : blockIdx.x) * uint32_t(TQ);
     const uint32_t q = q0 + uint32_t(c);
     const bool valid = q < a.nlines;
     const uint32_t qq = valid ? q : q0;
@@ -2577,7 +2594,7 @@ __global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nse
     double g[SMAX];
 #pragma unroll
     for (int i = 0; i < SMAX; ++i)
-        g[i] = (valid && i < sl) ? __builtin_nontemporal_load(a.in + base + uint32_t(i) * a.stride) : 0.0;
+        g[i] = (valid && i < ln) ? __builtin_nontemporal_load(a.in + base + uint32_t(i) * a.stride) : 0.0;
 
     if (t < TQ) {
         const uint32_t ql = a.q_off + qq;
@@ -2607,14 +2624,26 @@ __global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nse
             e = A * id;
             h = -A * h * id;
             t_id[i][c] = id;
-            t_e[i][c] = e;
             t_h[i][c] = h;
         }
-        double H = t_h[sl - 1][c], K = -t_e[sl - 1][c];
+        if constexpr (RG) {   // the last segment's sweep first: it reads the forward h_i that the next one replaces
+            double H2 = t_h[sr - 1][c], K2 = -(A * t_id[sr - 1][c]);
+            t_h2[sr - 1][c] = H2;
+            t_k2[sr - 1][c] = K2;
+#pragma unroll 1
+            for (int i = sr - 2; i >= 0; --i) {
+                const double ei = A * t_id[i][c];
+                H2 = t_h[i][c] - ei * H2;
+                K2 = -ei * K2;
+                t_h2[i][c] = H2;
+                t_k2[i][c] = K2;
+            }
+        }
+        double H = t_h[sl - 1][c], K = -(A * t_id[sl - 1][c]);
         t_k[sl - 1][c] = K;
 #pragma unroll 1
         for (int i = sl - 2; i >= 0; --i) {
-            const double ei = t_e[i][c];
+            const double ei = A * t_id[i][c];
             H = t_h[i][c] - ei * H;
             K = -ei * K;
             t_h[i][c] = H;
@@ -2629,12 +2658,12 @@ __global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nse
         g[0] *= t_id[0][c];
 #pragma unroll
         for (int i = 1; i < SMAX; ++i)
-            if (i < sl) g[i] = (g[i] - A * g[i - 1]) * t_id[i][c];
+            if (i < ln) g[i] = (g[i] - A * g[i - 1]) * t_id[i][c];
         double last = 0.0;
 #pragma unroll
         for (int i = SMAX - 1; i >= 0; --i) {
-            if (i == sl - 1) last = g[i];
-            if (i < sl - 1) g[i] -= t_e[i][c] * g[i + 1];
+            if (i == ln - 1) last = g[i];
+            if (i < ln - 1) g[i] -= (A * t_id[i][c]) * g[i + 1];
         }
         s_u[sj][c] = g[0];
         s_v[sj][c] = last;
@@ -2668,8 +2697,10 @@ __global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nse
             s_bv[j][c] = bv;
         }
         const int J = nseg - 1;
-        const double a11 = 1.0 - H0 * bv, a12 = -K0, a21 = -H1 * bv, a22 = 1.0 - K1;
-        const double b1 = s_u[J][c] + H0 * av, b2 = s_v[J][c] + H1 * av;
+        const double H0J = RG ? t_h2[0][c] : H0, K0J = RG ? t_k2[0][c] : K0;
+        const double H1J = RG ? t_h2[sr - 1][c] : H1, K1J = RG ? t_k2[sr - 1][c] : K1;
+        const double a11 = 1.0 - H0J * bv, a12 = -K0J, a21 = -H1J * bv, a22 = 1.0 - K1J;
+        const double b1 = s_u[J][c] + H0J * av, b2 = s_v[J][c] + H1J * av;
         const double idet = 1.0 / (a11 * a22 - a12 * a21);
         double u = (b1 * a22 - a12 * b2) * idet;
         s_u[J][c] = u;
@@ -2688,10 +2719,13 @@ __global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nse
     const double Rj = sj == nseg - 1 ? s_v[nseg - 1][c] : s_u[sj + 1][c];
     const double sc = a.inv_n * double(m);
     if (!valid) return;
+    const bool lastseg = RG && sj == nseg - 1;
 #pragma unroll
     for (int i = 0; i < SMAX; ++i)
-        if (i < sl)
-            __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + uint32_t(i) * a.stride);
+        if (i < ln) {
+            const double h = lastseg ? t_h2[i][c] : t_h[i][c], kk = lastseg ? t_k2[i][c] : t_k[i][c];
+            __builtin_nontemporal_store(sc * (g[i] + h * Lj + kk * Rj), a.out + base + uint32_t(i) * a.stride);
+        }
 }
 
 // =============================================================================================
@@ -3020,13 +3054,50 @@ hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint
 }
 
 // segment length for k_trig: the smallest divisor of m in [16, 32], else the largest in [4, 16),
-// with at most 64 segments; 0 when there is none
+// with at most 64 segments; else (no such divisor: a prime length, 2 x a prime ...; probe builds keep the
+// Bluestein MID pass with MVTV_TRIG_EXACT=1) 16 rows (32 past 1024 points; m / 4 rounded up below 64 points) with a
+// shorter last segment; 0 when there is none (m < 8, m > 2048)
 static int trig_seg(uint32_t m) {
     for (uint32_t sl = 16; sl <= uint32_t(trig::SMAX); ++sl)
         if (m % sl == 0 && m / sl <= uint32_t(trig::NSMAX) && m / sl >= 2) return int(sl);
     for (uint32_t sl = 15; sl >= 4; --sl)
         if (m % sl == 0 && m / sl <= uint32_t(trig::NSMAX) && m / sl >= 2) return int(sl);
-    return 0;
+    static const bool exact = probe_flag("MVTV_TRIG_EXACT");
+    if (exact || m < 8 || m > 2048) return 0;
+    if (m < 64) return int((m + 3) / 4);
+    return m > 1024 ? 32 : 16;
+}
+
+// k_trig's tile: 64 / 32 lines (512- / 256-B rows) with the segment arrays sized to the block where it fits 1024
+// threads and the lines fill >= 256 such workgroups, else 16 lines for any block (round 4's form; probe builds:
+// MVTV_TRIG_NARROW=1). sr < sl: a shorter last segment (RG)
+static void launch_trig(const SpecArgs& a, hipStream_t s, int sl, int nseg, int sr) {
+    static const bool narrow = probe_flag("MVTV_TRIG_NARROW");
+    auto go = [&](auto kern, uint32_t tq) {
+        klaunch(kern, dim3((a.nlines + tq - 1) / tq), dim3(tq * uint32_t(nseg)), 0, s, a, sl, nseg, sr);
+    };
+#define MVTV_TRIG(SM, TQ, NS)                                                                                   \
+    do {                                                                                                        \
+        if (sr != sl) go(k_trig<SM, TQ, NS, true>, uint32_t(TQ));                                               \
+        else go(k_trig<SM, TQ, NS, false>, uint32_t(TQ));                                                       \
+        return;                                                                                                 \
+    } while (0)
+    if (!narrow) {
+        if (nseg <= 16 && a.nlines / 64u >= 256u) {
+            if (sl <= 16) {
+                if (nseg <= 8) MVTV_TRIG(16, 64, 8);
+                MVTV_TRIG(16, 64, 16);
+            }
+            if (nseg <= 8) MVTV_TRIG(32, 64, 8);
+            MVTV_TRIG(32, 64, 16);
+        }
+        if (nseg <= 32 && a.nlines / 32u >= 256u) {
+            if (sl <= 16) MVTV_TRIG(16, 32, 32);
+            MVTV_TRIG(32, 32, 32);
+        }
+    }
+    MVTV_TRIG(trig::SMAX, trig::TQ, trig::NSMAX);
+#undef MVTV_TRIG
 }
 
 // k_tri serves the last-dimension pass when the lines are long enough for >= 4 segments and short enough
@@ -3397,12 +3468,14 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
             }
             a.perm = sp.perm + sp.lam_off[d];
         }
+        // strided passes: tiles in XCD runs (probe builds: MVTV_XRUN_OFF=1 deals them round-robin)
+        static const bool xrun_off = probe_flag("MVTV_XRUN_OFF");
+        a.xrun = (d > 0 && !xrun_off) ? 1 : 0;
         if (mode == SPEC_MID && d > 0 && !formb && a.nlines / uint32_t(trig::TQ) >= 256u && !probe_env("MVTV_DCT_TRI0")) {
             const int sl = trig_seg(m);
             if (sl > 0) {
-                const int nseg = int(m) / sl;
-                const dim3 grid((a.nlines + uint32_t(trig::TQ) - 1) / uint32_t(trig::TQ));
-                klaunch(k_trig, grid, dim3(trig::TQ * nseg), 0, s, a, sl, nseg);
+                const int nseg = int((m + uint32_t(sl) - 1) / uint32_t(sl));
+                launch_trig(a, s, sl, nseg, int(m) - (nseg - 1) * sl);
                 return hipGetLastError();
             }
         }

@@ -53,7 +53,8 @@ CASES = [([2], None, "cpp", False), ([8], None, "cpp", False), ([1024], None, "p
          # an odd number of lines: k_dctm pairs lines, so these fall back to k_dctg
          ([500, 7], [0.3, 0.7], "cpp", False), ([1000, 3], None, "py", False),
          # lengths with a prime factor >= 11 (Bluestein, k_dctb): FWD / INV along dim 0, MID along a 1-D mesh, a
-         # strided MID along the last dimension (few lines, and 4096 lines of a prime length k_trig cannot split),
+         # strided MID along the last dimension (few lines; >= 4096 lines of a prime length take k_trig with a
+         # shorter last segment: 67 = 4 x 16 + 3),
          # M = 8192 (one line pair in 128 KB of LDS), the R API's default m = floor(sqrt(n)) (31 at n = 1000)
          ([31], None, "cpp", False), ([1009], None, "py", False), ([4093], None, "cpp", False),
          ([37, 37], [0.3, 0.7], "cpp", False), ([22, 13], None, "py", False), ([4096, 67], [0.5, 0.5], "cpp", False),
@@ -104,11 +105,15 @@ def test_spectral_residual_baseline_sizes(m):
             assert np.linalg.norm(r) / np.linalg.norm(b) <= RTOL_DIRECT, (p, sigma)
 
 
-@pytest.mark.parametrize("m", [[256, 256, 128], [512, 512, 128], [1024, 1024, 128], [256, 256, 300], [512, 512, 135]])
+@pytest.mark.parametrize("m", [[256, 256, 128], [512, 512, 128], [1024, 1024, 128], [256, 256, 300], [512, 512, 135],
+                               [256, 256, 48], [96, 96, 400], [128, 128, 37], [256, 256, 101], [64, 64, 1009]])
 def test_3d_solve_residual_extreme_sigma(m):
     """3-D spectral solves (k_dct8 / k_dctg passes, k_tri along the last dimension) from sigma = 0 (the identity) to a
     dominant coupling (cond ~ 1e7): residual through the stencil operator within the backward-stable bound;
-    256 / 512 / 1024-point rows, last-dimension lengths a power of two, 300 = 4 3 5^2 and 135 = 27 5 (k_trig)."""
+    256 / 512 / 1024-point rows, last-dimension lengths a power of two, 300 = 4 3 5^2 and 135 = 27 5 (k_trig on
+    64-line tiles, 20- and 27-row segments), 48 (16-row segments), 400 (25 segments of 16: 32-line tiles), and
+    lengths k_trig splits with a shorter last segment: 37 = 3 x 10 + 7, 101 = 6 x 16 + 5 (64-line tiles), the prime
+    1009 = 63 x 16 + 1 (a one-row last segment; 16-line tiles, 4096 lines)."""
     p = len(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     N = int(np.prod(m))
