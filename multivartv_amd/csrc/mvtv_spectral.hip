@@ -1631,10 +1631,12 @@ __device__ __forceinline__ int dctm_in_pos(int j, int i) {
     return j + (i / R) * T + (i % R) * (M / R);
 }
 
-template <int M, int MODE, bool D0, bool FORMB>
-__global__ __launch_bounds__(dctm::Shape<M>::NT) void k_dctm(const SpecArgs a) {
+// NCLW complex lines (2 NCLW real lines) per workgroup: 8 (128-B rows) or 4 (64-B rows, half the LDS: more workgroups
+// a CU)
+template <int M, int MODE, bool D0, bool FORMB, int NCLW = dctm::NCL>
+__global__ __launch_bounds__(NCLW * dctm::Shape<M>::T) void k_dctm(const SpecArgs a) {
     using S = dctm::Shape<M>;
-    constexpr int T = S::T, NCL = dctm::NCL, V = S::V;
+    constexpr int T = S::T, NCL = NCLW, V = S::V, TQ = 2 * NCLW;
     static_assert(MODE == SPEC_FWD || MODE == SPEC_INV, "FWD / INV passes");
     double ca = a.ca, cb = a.cb;
     bool rd_gb = true;
@@ -1653,7 +1655,7 @@ __global__ __launch_bounds__(dctm::Shape<M>::NT) void k_dctm(const SpecArgs a) {
     const int t = threadIdx.x;
     const int j = D0 ? (t % T) : (t / NCL);
     const int c = D0 ? (t / T) : (t % NCL);
-    const uint32_t q0 = (a.xrun ? xcd_run(blockIdx.x, gridDim.x) : blockIdx.x) * uint32_t(dctm::TQ);
+    const uint32_t q0 = (a.xrun ? xcd_run(blockIdx.x, gridDim.x) : blockIdx.x) * uint32_t(TQ);
     const int la = 2 * c;
     const bool va = q0 + uint32_t(la) < a.nlines;   // lines come in pairs: nlines is even (launcher)
     double2* X = buf + c * S::LP;
@@ -1820,6 +1822,12 @@ __global__ __launch_bounds__(dctm::Shape<M>::NT) void k_dctm(const SpecArgs a) {
     }
 }
 
+// few lines (2-D meshes): halve a tile of tq lines, down to lo, while the grid has < 512 workgroups
+static int few_lines_tq(uint32_t nlines, int tq, int lo) {
+    while (tq > lo && (nlines + uint32_t(tq) - 1) / uint32_t(tq) < 512u) tq /= 2;
+    return tq;
+}
+
 // k_dctm serves FWD / INV passes of m = 500 / 1000 lines; false: the caller takes k_dctg
 static bool launch_dctm(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
     const uint32_t m = a.m[a.d];
@@ -1829,23 +1837,42 @@ static bool launch_dctm(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
         probe_env("MVTV_DCTM_OFF"))
         return false;
     if (!d0 && (a.stride & 1u)) return false;   // line pairs must be adjacent words
-    const dim3 grid((a.nlines + uint32_t(dctm::TQ) - 1) / uint32_t(dctm::TQ));
-#define MVTV_DCTM(MM)                                                                                           \
+    // 8-line tiles (500: 32 KB of LDS, up to five workgroups a CU against two with 16 lines; 1000: two against one):
+    // 500^3 137.5 / 138.3 -> 141.6 / 142.4 ADMM it/s on one box, the first pass 0.93 -> 0.86 ms
+    // (profiles/r05/v11_dctm_ncl4); few lines (1000 x 1000: 125 such tiles) one line pair per workgroup. Probe builds:
+    // MVTV_DCTM_NCL=8 / 4 / 1 forces the tile
+    static const int ncl_env = [] {
+        const char* e = probe_env("MVTV_DCTM_NCL");
+        return e ? std::atoi(e) : 0;
+    }();
+    static const bool few_off = probe_flag("MVTV_FEW_LINES_OFF");
+    const int ncl = (ncl_env == 8 || ncl_env == 4 || ncl_env == 1)
+                        ? ncl_env
+                        : (few_off ? 4 : few_lines_tq(a.nlines, 8, 2) / 2);
+#define MVTV_DCTM(MM, NC)                                                                                       \
     do {                                                                                                        \
-        const dim3 block(dctm::Shape<MM>::NT);                                                                  \
+        const dim3 grid((a.nlines + uint32_t(2 * NC) - 1) / uint32_t(2 * NC));                                 \
+        const dim3 block(NC * dctm::Shape<MM>::T);                                                              \
         if (mode == SPEC_INV) {                                                                                 \
-            if (d0) klaunch(k_dctm<MM, SPEC_INV, true, false>, grid, block, 0, s, a);                           \
-            else klaunch(k_dctm<MM, SPEC_INV, false, false>, grid, block, 0, s, a);                             \
+            if (d0) klaunch(k_dctm<MM, SPEC_INV, true, false, NC>, grid, block, 0, s, a);                       \
+            else klaunch(k_dctm<MM, SPEC_INV, false, false, NC>, grid, block, 0, s, a);                         \
         } else if (d0) {                                                                                        \
-            if (formb) klaunch(k_dctm<MM, SPEC_FWD, true, true>, grid, block, 0, s, a);                         \
-            else klaunch(k_dctm<MM, SPEC_FWD, true, false>, grid, block, 0, s, a);                              \
+            if (formb) klaunch(k_dctm<MM, SPEC_FWD, true, true, NC>, grid, block, 0, s, a);                     \
+            else klaunch(k_dctm<MM, SPEC_FWD, true, false, NC>, grid, block, 0, s, a);                          \
         } else {                                                                                                \
-            if (formb) klaunch(k_dctm<MM, SPEC_FWD, false, true>, grid, block, 0, s, a);                        \
-            else klaunch(k_dctm<MM, SPEC_FWD, false, false>, grid, block, 0, s, a);                             \
+            if (formb) klaunch(k_dctm<MM, SPEC_FWD, false, true, NC>, grid, block, 0, s, a);                    \
+            else klaunch(k_dctm<MM, SPEC_FWD, false, false, NC>, grid, block, 0, s, a);                         \
         }                                                                                                       \
     } while (0)
-    if (m == 500) MVTV_DCTM(500);
-    else MVTV_DCTM(1000);
+    if (m == 500) {
+        if (ncl == 8) MVTV_DCTM(500, 8);
+        else if (ncl == 4) MVTV_DCTM(500, 4);
+        else MVTV_DCTM(500, 1);
+    } else {
+        if (ncl == 8) MVTV_DCTM(1000, 8);
+        else if (ncl == 4) MVTV_DCTM(1000, 4);
+        else MVTV_DCTM(1000, 1);
+    }
 #undef MVTV_DCTM
     return true;
 }
@@ -3058,6 +3085,13 @@ hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint
 // Bluestein MID pass with MVTV_TRIG_EXACT=1) 16 rows (32 past 1024 points; m / 4 rounded up below 64 points) with a
 // shorter last segment; 0 when there is none (m < 8, m > 2048)
 static int trig_seg(uint32_t m) {
+    static const int force = [] {   // probe builds: MVTV_TRIG_SL=s forces the segment length (a shorter last one
+        const char* e = probe_env("MVTV_TRIG_SL");   // when s does not divide m)
+        return e ? std::atoi(e) : 0;
+    }();
+    if (force >= 4 && force <= trig::SMAX && m / uint32_t(force) >= 2 &&
+        (m + uint32_t(force) - 1) / uint32_t(force) <= uint32_t(trig::NSMAX))
+        return force;
     for (uint32_t sl = 16; sl <= uint32_t(trig::SMAX); ++sl)
         if (m % sl == 0 && m / sl <= uint32_t(trig::NSMAX) && m / sl >= 2) return int(sl);
     for (uint32_t sl = 15; sl >= 4; --sl)
@@ -3468,6 +3502,7 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
             }
             a.perm = sp.perm + sp.lam_off[d];
         }
+        static const bool few_off = probe_flag("MVTV_FEW_LINES_OFF");
         // strided passes: tiles in XCD runs (probe builds: MVTV_XRUN_OFF=1 deals them round-robin)
         static const bool xrun_off = probe_flag("MVTV_XRUN_OFF");
         a.xrun = (d > 0 && !xrun_off) ? 1 : 0;
@@ -3490,9 +3525,12 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
             return launch_dctb(a, s, mode, d == 0, formb);
         }
         if (launch_dctm(a, s, mode, d == 0, formb)) return hipGetLastError();
-        // <= 16 lines (128-B rows for d > 0) in <= 64 KB of LDS
+        // <= 16 lines (128-B rows for d > 0) in <= 64 KB of LDS; few lines (a 2-D mesh: 1000 lines of 1000) take
+        // smaller tiles until the grid has >= 512 workgroups (two a CU) or the tile two lines (probe builds:
+        // MVTV_FEW_LINES_OFF=1 keeps the LDS-sized tile)
         int tq = 16;
         while (tq > 2 && (tq / 2) * int(m + spec::PAD) > spec::LDS_WORDS / 2 + 8 * spec::PAD) tq /= 2;
+        if (!few_off) tq = few_lines_tq(a.nlines, tq, 2);
         a.tq = tq;
         launch_dctg(a, s, mode, d == 0, formb);
         return hipGetLastError();
