@@ -1559,7 +1559,7 @@ __global__ __launch_bounds__(dctg::NT) __attribute__((amdgpu_waves_per_eu(4))) v
 // k_dctg's MID pass); TQ = 16 real lines per workgroup, lanes over the lines for a strided pass (16-B accesses
 // of a line pair, 128-B rows when the tile does not straddle a stride boundary), over j for d = 0.
 namespace dctm {
-constexpr int NCL = 8, TQ = 2 * NCL;
+constexpr int NCL = 8;   // complex lines per workgroup (default tile)
 // radix plan and values per thread (every radix divides V): 500 = 2 2 5^3 with V = 10 (400 threads, two
 // workgroups per CU), 1000 = 2 4 5^3 with V = 20 (400 threads)
 template <int M> struct Plan;
@@ -2325,9 +2325,8 @@ constexpr int dctb8_tq() {
     return TQ < 2 ? 2 : ((TQ / 2) * TPL >= 64 ? TQ : 2 * (64 / TPL));
 }
 
-template <int L>
-static void launch_dctb8_l(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
-    constexpr int TQW = dctb8_tq<L>();
+template <int L, int TQW>
+static void launch_dctb8_t(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
     const dim3 grid((a.nlines + uint32_t(TQW) - 1) / uint32_t(TQW)), block(spec8::ShapeK<L, TQW>::NT);
 #define MVTV_DCTB8(MODE, D0, FB) klaunch(k_dctb8<L, MODE, D0, FB, TQW>, grid, block, 0, s, a)
     if (mode == SPEC_FWD) {
@@ -2353,6 +2352,21 @@ static void launch_dctb8_l(SpecArgs& a, hipStream_t s, int mode, bool d0, bool f
         }
     }
 #undef MVTV_DCTB8
+}
+
+// few lines (a 2-D mesh: 251 lines of 251): one line pair per workgroup where that is >= one wave of threads
+// (M >= 512), the default tile is >= 8 lines (M <= 1024) and leaves < 512 workgroups: 251^2 12851 / 12874 -> 16902 /
+// 16751 ADMM it/s; at M = 2048 (1009^2: 253 workgroups of 4 lines) one pair was slower, 8356 -> 8061
+// (profiles/r05/v14_few_lines_bluestein; probe builds: MVTV_FEW_LINES_OFF=1)
+template <int L>
+static void launch_dctb8_l(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
+    constexpr int TQW = dctb8_tq<L>();
+    static const bool few_off = probe_flag("MVTV_FEW_LINES_OFF");
+    if constexpr (L >= 9 && L <= 10 && TQW > 2) {
+        if (!few_off && (a.nlines + uint32_t(TQW) - 1) / uint32_t(TQW) < 512u)
+            return launch_dctb8_t<L, 2>(a, s, mode, d0, formb);
+    }
+    launch_dctb8_t<L, TQW>(a, s, mode, d0, formb);
 }
 
 static hipError_t launch_dctb(SpecArgs& a, hipStream_t s, int mode, bool d0, bool formb) {
@@ -3507,7 +3521,14 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
         static const bool xrun_off = probe_flag("MVTV_XRUN_OFF");
         a.xrun = (d > 0 && !xrun_off) ? 1 : 0;
         if (mode == SPEC_MID && d > 0 && !formb && a.nlines / uint32_t(trig::TQ) >= 256u && !probe_env("MVTV_DCT_TRI0")) {
-            const int sl = trig_seg(m);
+            int sl = trig_seg(m);
+            // more than 16 segments keep k_trig on 32-line tiles; where 64-line tiles fill the chip, <= 32-row
+            // segments with a shorter last one bring it to 16 (500: 25 x 20 -> 15 x 32 + 20 rows, 0.69 -> 0.48 ms
+            // at 500^3, profiles/r05/v13_trig_sl32; probe builds: MVTV_TRIG_SL forces, MVTV_TRIG_NARROW keeps)
+            static const bool sl_forced = probe_env("MVTV_TRIG_SL") != nullptr;
+            if (sl > 0 && !sl_forced && (m + uint32_t(sl) - 1) / uint32_t(sl) > 16u && a.nlines / 64u >= 256u &&
+                (m + 15u) / 16u <= uint32_t(trig::SMAX))
+                sl = int((m + 15u) / 16u);
             if (sl > 0) {
                 const int nseg = int((m + uint32_t(sl) - 1) / uint32_t(sl));
                 launch_trig(a, s, sl, nseg, int(m) - (nseg - 1) * sl);
