@@ -3143,6 +3143,12 @@ static void launch_trig(const SpecArgs& a, hipStream_t s, int sl, int nseg, int 
             if (sl <= 16) MVTV_TRIG(16, 32, 32);
             MVTV_TRIG(32, 32, 32);
         }
+        // few lines (the last dimension of a 2-D mesh: 1009 lines): 8- / 4-line tiles, >= 128 / 256 workgroups
+        if (a.nlines / uint32_t(trig::TQ) < 256u) {
+            const int tq = few_lines_tq(a.nlines, trig::TQ, 4);
+            if (tq == 4) MVTV_TRIG(trig::SMAX, 4, trig::NSMAX);
+            if (tq == 8) MVTV_TRIG(trig::SMAX, 8, trig::NSMAX);
+        }
     }
     MVTV_TRIG(trig::SMAX, trig::TQ, trig::NSMAX);
 #undef MVTV_TRIG
@@ -3520,7 +3526,13 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
         // strided passes: tiles in XCD runs (probe builds: MVTV_XRUN_OFF=1 deals them round-robin)
         static const bool xrun_off = probe_flag("MVTV_XRUN_OFF");
         a.xrun = (d > 0 && !xrun_off) ? 1 : 0;
-        if (mode == SPEC_MID && d > 0 && !formb && a.nlines / uint32_t(trig::TQ) >= 256u && !probe_env("MVTV_DCT_TRI0")) {
+        // the line solve along the last dimension also for the few lines of a 2-D mesh, on 4-line tiles where that
+        // makes >= 250 workgroups (a Bluestein MID pass is four FFTs of twice the length per line pair): 2039^2 2070 ->
+        // 3310 ADMM it/s, 1009^2 8431 -> 9086, 1000^2 10682 -> 11017; 500^2 (125 such tiles) 16059 -> 15855 keeps the
+        // MID pass (profiles/r05/v15_trig_2d; probe builds: MVTV_TRIG_FEW_OFF=1)
+        static const bool trig_few_off = probe_flag("MVTV_TRIG_FEW_OFF");
+        const bool trig_lines = a.nlines / uint32_t(trig::TQ) >= 256u || (!trig_few_off && a.nlines >= 1000u);
+        if (mode == SPEC_MID && d > 0 && !formb && trig_lines && !probe_env("MVTV_DCT_TRI0")) {
             int sl = trig_seg(m);
             // more than 16 segments keep k_trig on 32-line tiles; where 64-line tiles fill the chip, <= 32-row
             // segments with a shorter last one bring it to 16 (500: 25 x 20 -> 15 x 32 + 20 rows, 0.69 -> 0.48 ms

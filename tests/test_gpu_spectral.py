@@ -47,6 +47,9 @@ CASES = [([2], None, "cpp", False), ([8], None, "cpp", False), ([1024], None, "p
          ([7, 7, 7], [0.2, 0.3, 0.4], "cpp", True), ([3, 4096], [0.5, 0.5], "cpp", False),
          # mixed-radix mesh whose last dimension takes the general-length tridiagonal pass (k_trig)
          ([4096, 100], [0.5, 0.5], "cpp", False),
+         # ... and on 4-line tiles for the >= 1000 lines of a 2-D mesh (a prime length with a shorter last segment; a
+         # mixed-radix one)
+         ([1024, 67], [0.5, 0.5], "cpp", False), ([1200, 100], None, "py", False),
          # register-resident mixed-radix passes along dim 0 (k_dctm, m = 500 / 1000; the strided form is checked
          # at 500^3 below: unequal dims are refused at p >= 3, the reference's mixed-partial rule)
          ([500, 6], [0.3, 0.7], "cpp", False), ([1000, 4], None, "py", False),
