@@ -3311,11 +3311,13 @@ static void launch_dct8(SpecArgs& a, hipStream_t s, int mode, bool d0, bool form
     bool xcd_def = false;
     if (d0) {
         if (a.nlines / uint32_t(S::TQ) < 1024u) want = std::min(TMIN, S::TQ);
-    } else if (L >= 10 && L <= 12 && 2 * S::TQ <= int(a.stride)) {
-        want = 2 * S::TQ;
-        if (a.nlines / uint32_t(want) < 128u && tile_ok<L>(4) && int(a.stride) >= 4) {
-            want = 4;
-            xcd_def = true;
+    } else {
+        // strided passes: tiles in XCD runs (512^3: the dim-1 passes' bucket 0.436 -> 0.405 ms, 174.7 / 174.6 ->
+        // 178.3 / 178.3 ADMM it/s on one box, profiles/r05/v16_dct8_xcd; the d = 0 passes stay round-robin there)
+        xcd_def = true;
+        if (L >= 10 && L <= 12 && 2 * S::TQ <= int(a.stride)) {
+            want = 2 * S::TQ;
+            if (a.nlines / uint32_t(want) < 128u && tile_ok<L>(4) && int(a.stride) >= 4) want = 4;
         }
     }
     // (probe builds read these per launch, so a probe can vary them within one process)
