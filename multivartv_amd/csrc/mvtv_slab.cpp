@@ -165,13 +165,31 @@ struct RcclComm final : mvtv_comm {
         lane_ = 0;
         if (!split_tried) {   // every rank reaches this at its first run: a collective call in the same order
             split_tried = true;
-            const char* e = std::getenv("MVTV_RCCL_ONE_COMM");
-            const bool off = e && std::atoi(e) != 0;
-            if (!off && api_->CommSplit) {
+            // The second lane is opt-in (MVTV_RCCL_SPLIT=1) until a multi-GPU RCCL run has exercised it; with it on,
+            // the ranks agree on the outcome before any rank uses it: one rank on comm2 while its peers stay on comm
+            // would post mismatched operations and hang inside the loop
+            const char* e = std::getenv("MVTV_RCCL_SPLIT");
+            if (e && std::atoi(e) != 0) {
                 DeviceGuard dg(device);
-                if (api_->CommSplit(comm, 0, rank, &comm2, nullptr) != ncclSuccess) comm2 = nullptr;
+                bool ok = api_->CommSplit && api_->CommSplit(comm, 0, rank, &comm2, nullptr) == ncclSuccess;
+                if (!ok) comm2 = nullptr;
+                double host[1] = {ok ? 0.0 : 1.0};
+                bool agreed = false;
+                if (stream || hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) == hipSuccess) {
+                    if (scratch || alloc(&scratch, 64) == MVTV_OK) {
+                        agreed = hipMemcpyAsync(scratch, host, sizeof(double), hipMemcpyHostToDevice, stream) == hipSuccess &&
+                                 api_->AllReduce(scratch, scratch, 1, ncclFloat64, ncclSum, comm, stream) == ncclSuccess &&
+                                 hipMemcpyAsync(host, scratch, sizeof(double), hipMemcpyDeviceToHost, stream) == hipSuccess &&
+                                 hipStreamSynchronize(stream) == hipSuccess;
+                    }
+                }
+                if (!agreed || host[0] != 0.0) {   // some rank has no second communicator: every rank keeps one lane
+                    if (comm2 && api_->CommDestroy) api_->CommDestroy(comm2);
+                    comm2 = nullptr;
+                    (void)hipGetLastError();
+                    std::fprintf(stderr, "mvtv: RCCL second lane not on every rank (%g failed); one lane\n", host[0]);
+                }
             }
-            if (!comm2 && !off) return fail(MVTV_HIP_ERROR, "RCCL: ncclCommSplit failed (one lane)");
         }
         return MVTV_OK;
     }
@@ -462,9 +480,13 @@ struct IpcComm final : mvtv_comm {
         if (shm) munmap(shm, sizeof(IpcShm));
     }
     void close_mappings() {
-        DeviceGuard dg(device);
-        for (auto& mp : mapped)
-            if (mp.ptr) (void)hipIpcCloseMemHandle(mp.ptr);
+        // no HIP call (and no runtime initialisation) when nothing is mapped: the host-only transport tests
+        const bool any = std::any_of(mapped.begin(), mapped.end(), [](const Mapped& mp) { return mp.ptr != nullptr; });
+        if (any) {
+            DeviceGuard dg(device);
+            for (auto& mp : mapped)
+                if (mp.ptr) (void)hipIpcCloseMemHandle(mp.ptr);
+        }
         mapped.assign(size_t(size), Mapped{});
     }
     void abort() override {
@@ -868,8 +890,12 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     // the z ping-pong pair by timed probes, as one GPU's loop does (its first fused run, slabs of >= 2^24 nodes):
     // the fused pass's time depends on which physical buffers z moves between (slab world 1 at 512^3: 3.41 ms
     // on the allocation-order pair against 3.17 for the one-GPU loop in the same round-4 sweep); a rank-local
-    // choice, no collective. The state is zeroed below
-    if (fused && !P->zpicked) MVTV_TRY(zpair_pick(P, false, twin));
+    // choice, no collective. Skipped where ranks share a device (more ranks than devices: the IPC rehearsals), whose
+    // probes would time each other and race for the free memory the candidates need. The state is zeroed below
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+    const bool shared_device = G > 1 && ndev > 0 && G > ndev;
+    if (fused && !P->zpicked && !shared_device) MVTV_TRY(zpair_pick(P, false, twin));
     const size_t nodes = P->g.N, ebytes = size_t(P->g.nb) * nodes * sizeof(double);
 
     // ---- initial state: theta0 everywhere (ghosts included), u0 = 0, g_alpha = D^T D theta0 -----------
@@ -1360,8 +1386,8 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
 extern "C" mvtv_status mvtv_slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, double lambda,
                                      double theta0, double rho0, mvtv_admm_stats* stats) {
     if (!C) return fail(MVTV_BAD_ARG, "null communicator");
-    (void)C->run_begin();   // a failed split leaves one lane (lanes() == 1): the loop then keeps every collective
-                            // on the collectives stream, the round-4 schedule
+    (void)C->run_begin();   // without a second lane on every rank (lanes() == 1) the loop keeps every collective on
+                            // the collectives stream, the round-4 schedule; run_begin records no error
     const mvtv_status st =
         (!P || !opts) ? fail(MVTV_BAD_ARG, "null argument") : slab_run(P, C, opts, lambda, theta0, rho0, stats);
     if (st != MVTV_OK && st != MVTV_MAXITER) C->abort();

@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 
 #include "mvtv_device.h"
@@ -2598,6 +2599,156 @@ __global__ __launch_bounds__((tri::Shape<L, SEG, TQL>::NT)) void k_tri(const Spe
         __builtin_nontemporal_store(sc * (g[i] + t_h[i][c] * Lj + t_k[i][c] * Rj), a.out + base + (uint32_t(i) << a.ls));
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_trir: the same line solves by the factorised operator (round 6). c0 I + c1 T is, away from the ends,
+// -c1 x[i-1] + (c0 + 2 c1) x[i] - c1 x[i+1] = kappa (1 - r S+)(1 - r S-) with r the root in (0, 1) of
+// c1 r^2 - (c0 + 2 c1) r + c1 = 0; its Green's function is r^|k| / D with D = sqrt(c0 (c0 + 4 c1)). The
+// Neumann ends are the mirror conditions, so the line's solve is the bi-infinite one on the even extension of
+// the data: x_i = (F_i + B_i - f_i) / D with the two first-order recursions
+//     F_i = f_i + r F_{i-1} (forward),      B_i = f_i + r B_{i+1} (backward),
+// closed by the mirror: F_{-1} = B_0 and B_m = F_{m-1} (a 2 x 2 system with determinant 1 - r^2m).
+// Segment-parallel: a thread runs both recursions over its SEG rows from zero (two independent chains),
+// one thread per line combines the segments' sums into every segment's carries (F into its first row, B into
+// its last) and closes the mirror, and every thread reruns the recursions with its carries. No divide per row,
+// no per-row line constants (k_tri keeps four [SEG][TQ] tables in ~97 KB of LDS, so one workgroup fits a CU,
+// and eliminates the interface on one wave with a divide per step); LDS here is 2 sums per segment and five
+// constants per line. r = 2 c1 / (c0 + 2 c1 + D) and 1 - r = (c0 + D) / (c0 + 2 c1 + D) are cancellation-free;
+// 1 - r^k by t_2k = t_k (2 - t_k). Against a long-double Thomas solve (numpy transcription): 1e-15 at
+// c1 / c0 = 1e2, 3e-14 at 1e7 relative (an LU solve of the same system: 2e-11 at 1e7).
+namespace trir {
+template <int L, int SEG, int TQL>
+struct Shape {
+    static constexpr int M = 1 << L;
+    static constexpr int NSEG = M / SEG;
+    static constexpr int NT = TQL * NSEG;
+};
+}  // namespace trir
+
+template <int L, int SEG, int TQL>
+__global__ __launch_bounds__((trir::Shape<L, SEG, TQL>::NT), (SEG <= 16 ? 8 : 4)) void k_trir(const SpecArgs a) {
+    using S = trir::Shape<L, SEG, TQL>;
+    constexpr int TQ = TQL, NSEG = S::NSEG;
+    double sigma = a.sigma;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+    }
+    __shared__ double s_f[NSEG][TQ], s_b[NSEG][TQ];   // segment sums from zero, then the segments' carries
+    __shared__ double s_r[TQ], s_sd[TQ];               // r, scale / D per line
+    const int t = threadIdx.x, c = t % TQ, sj = t / TQ;
+    const uint32_t bx = a.xcd ? (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    const uint32_t q0 = bx * uint32_t(TQ);
+    const uint32_t q = q0 + uint32_t(c);
+    const bool valid = q < a.nlines;
+    const uint32_t base = (q & (a.stride - 1)) + ((q >> a.ls) << (a.ls + L)) + (uint32_t(sj * SEG) << a.ls);
+
+    double lamv[kMaxDims] = {0, 0, 0, 0};
+    if (t < TQ) {
+        const uint32_t ql = a.q_off + (valid ? q : q0);
+        uint32_t rest = ql;
+        const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
+        for (int jj = 0; jj < a.p; ++jj) {
+            if (jj == a.d) continue;
+            const uint32_t qq = (jj < jlast) ? a.fd[jj].div(rest) : 0u;
+            lamv[jj] = a.lam[a.lam_off[jj] + (rest - qq * a.m[jj])];
+            rest = qq;
+        }
+    }
+    double g[SEG];
+#pragma unroll
+    for (int i = 0; i < SEG; ++i) g[i] = valid ? __builtin_nontemporal_load(a.in + base + (uint32_t(i) << a.ls)) : 0.0;
+
+    double rm = 0.0, idet = 1.0, rseg = 0.0;   // t < TQ: r^m, 1 / (1 - r^2m), r^SEG
+    if (t < TQ) {
+        double c0 = a.w0, c1 = 0.0;
+        for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
+            if (a.cS[Sm] == 0.0) continue;
+            double prod = sigma * a.cS[Sm];
+            for (int jj = 0; jj < a.p; ++jj)
+                if (jj != a.d && ((Sm >> jj) & 1)) prod *= lamv[jj];
+            if ((Sm >> a.d) & 1) c1 += prod;
+            else c0 += prod;
+        }
+        const double D = sqrt(c0 * (c0 + 4.0 * c1));
+        const double den = 1.0 / (c0 + 2.0 * c1 + D);
+        const double r = 2.0 * c1 * den;
+        double pk = r, tk = (c0 + D) * den;   // r^k, 1 - r^k at k = 1
+#pragma unroll
+        for (int k = 1; k < SEG; k <<= 1) {
+            pk *= pk;
+            tk *= 2.0 - tk;
+        }
+        rseg = pk;
+#pragma unroll
+        for (int k = SEG; k < S::M; k <<= 1) {
+            pk *= pk;
+            tk *= 2.0 - tk;
+        }
+        rm = pk;
+        idet = 1.0 / (tk * (2.0 - tk));   // 1 / (1 - r^2m)
+        s_r[c] = r;
+        s_sd[c] = a.inv_n * double(S::M) / D;
+    }
+    __syncthreads();
+
+    const double r = s_r[c];
+    {
+        // both recursions over this segment from zero: two independent chains
+        double fl = 0.0, bl = 0.0;
+#pragma unroll
+        for (int i = 0; i < SEG; ++i) {
+            fl = fma(r, fl, g[i]);
+            bl = fma(r, bl, g[SEG - 1 - i]);
+        }
+        s_f[sj][c] = fl;
+        s_b[sj][c] = bl;
+    }
+    __syncthreads();
+
+    if (t < TQ) {
+        // carries: F into segment j's first row = sum_{k<j} r^{SEG(j-1-k)} fl_k + r^{SEG j} F_{-1}, B likewise from
+        // the right; F_{-1} = B_0 and B_m = F_{m-1} close the mirror
+        double acc = 0.0, bcc = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < NSEG; ++k) {
+            const double fk = s_f[k][c], bk = s_b[NSEG - 1 - k][c];
+            s_f[k][c] = acc;
+            s_b[NSEG - 1 - k][c] = bcc;
+            acc = fma(acc, rseg, fk);
+            bcc = fma(bcc, rseg, bk);
+        }
+        const double fm1 = (bcc + rm * acc) * idet, bm = (acc + rm * bcc) * idet;
+        double pw = 1.0;
+#pragma unroll 8
+        for (int k = 0; k < NSEG; ++k) {
+            s_f[k][c] = fma(pw, fm1, s_f[k][c]);
+            s_b[NSEG - 1 - k][c] = fma(pw, bm, s_b[NSEG - 1 - k][c]);
+            pw *= rseg;
+        }
+    }
+    __syncthreads();
+
+    if (!valid) return;
+    const double sd = s_sd[c], bin = s_b[sj][c];
+    double fv = s_f[sj][c];
+    // g <- B (backward with the carry), then x_i = (B_i + r F_{i-1}) / D, F_i = B_i + r (F_{i-1} - B_{i+1})
+    {
+        double bv = bin;
+#pragma unroll
+        for (int i = SEG - 1; i >= 0; --i) {
+            bv = fma(r, bv, g[i]);
+            g[i] = bv;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < SEG; ++i) {
+        const double gn = i + 1 < SEG ? g[i + 1] : bin;
+        __builtin_nontemporal_store(sd * fma(r, fv, g[i]), a.out + base + (uint32_t(i) << a.ls));
+        fv = fma(r, fv - gn, g[i]);
+    }
+}
+
 // k_trig: the same solve for any line length m = (NSEG - 1) * s + sr (segment length s <= SMAX chosen at launch,
 // NSEG <= NS, the last segment sr <= s rows) and any line stride (FastDiv addressing): the last-dimension pass of
 // the mixed-radix and prime-length meshes. Rows past a segment's length in the fixed-size register arrays are
@@ -2766,6 +2917,147 @@ __global__ __launch_bounds__(1024) void k_trig(const SpecArgs a, int sl, int nse
         if (i < ln) {
             const double h = lastseg ? t_h2[i][c] : t_h[i][c], kk = lastseg ? t_k2[i][c] : t_k[i][c];
             __builtin_nontemporal_store(sc * (g[i] + h * Lj + kk * Rj), a.out + base + uint32_t(i) * a.stride);
+        }
+}
+
+// (r^k, 1 - r^k) pairs: products and powers keep 1 - r^k free of cancellation (1 - r^(a+b) = t_a + r^a t_b)
+struct PowT {
+    double p, t;
+};
+__device__ __forceinline__ PowT powt_mul(PowT a, PowT b) { return {a.p * b.p, fma(a.p, b.t, a.t)}; }
+__device__ __forceinline__ PowT powt_pow(PowT x, uint32_t n) {
+    PowT y{1.0, 0.0};
+    while (n) {
+        if (n & 1u) y = powt_mul(y, x);
+        x = powt_mul(x, x);
+        n >>= 1;
+    }
+    return y;
+}
+
+// k_trigr: k_trir's factorised solve for k_trig's lines (any length m = (nseg - 1) sl + sr, any stride; a shorter
+// last segment sr <= sl). Segment j's carries go through r^len_j; the mirror closure through r^m.
+template <int SMAX, int TQ, int NS>
+__global__ __launch_bounds__(1024) void k_trigr(const SpecArgs a, int sl, int nseg, int sr) {
+    double sigma = a.sigma;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+    }
+    __shared__ double s_f[NS][TQ], s_b[NS][TQ];
+    __shared__ double s_r[TQ], s_sd[TQ];
+    const int t = threadIdx.x, c = t % TQ, sj = t / TQ;
+    const int ln = sj == nseg - 1 ? sr : sl;   // this thread's segment length
+    const uint32_t m = a.m[a.d];
+    const uint32_t q0 = (a.xrun ? xcd_run(blockIdx.x, gridDim.x) : blockIdx.x) * uint32_t(TQ);
+    const uint32_t q = q0 + uint32_t(c);
+    const bool valid = q < a.nlines;
+    const uint32_t qq = valid ? q : q0;
+    const uint32_t hi = a.fds.div(qq);
+    const uint32_t base = (qq - hi * a.stride) + hi * a.stride * m + uint32_t(sj * sl) * a.stride;
+
+    double lamv[kMaxDims] = {0, 0, 0, 0};
+    if (t < TQ) {
+        uint32_t rest = a.q_off + qq;
+        const int jlast = a.d == a.p - 1 ? a.p - 2 : a.p - 1;
+        for (int jj = 0; jj < a.p; ++jj) {
+            if (jj == a.d) continue;
+            const uint32_t qd = (jj < jlast) ? a.fd[jj].div(rest) : 0u;
+            lamv[jj] = a.lam[a.lam_off[jj] + (rest - qd * a.m[jj])];
+            rest = qd;
+        }
+    }
+    double g[SMAX];
+    {
+        const double* pin = a.in + base;
+#pragma unroll
+        for (int i = 0; i < SMAX; ++i) {
+            g[i] = (valid && i < ln) ? __builtin_nontemporal_load(pin) : 0.0;
+            pin += a.stride;
+        }
+    }
+
+    double rsl = 0.0, rsr = 0.0, rm = 0.0, idet = 1.0;   // t < TQ: r^sl, r^sr, r^m, 1 / (1 - r^2m)
+    if (t < TQ) {
+        double c0 = a.w0, c1 = 0.0;
+        for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
+            if (a.cS[Sm] == 0.0) continue;
+            double prod = sigma * a.cS[Sm];
+            for (int jj = 0; jj < a.p; ++jj)
+                if (jj != a.d && ((Sm >> jj) & 1)) prod *= lamv[jj];
+            if ((Sm >> a.d) & 1) c1 += prod;
+            else c0 += prod;
+        }
+        const double D = sqrt(c0 * (c0 + 4.0 * c1));
+        const double den = 1.0 / (c0 + 2.0 * c1 + D);
+        const PowT r1{2.0 * c1 * den, (c0 + D) * den};
+        const PowT ps = powt_pow(r1, uint32_t(sl)), pr = powt_pow(r1, uint32_t(sr));
+        const PowT pm = powt_mul(powt_pow(ps, uint32_t(nseg - 1)), pr);
+        rsl = ps.p;
+        rsr = pr.p;
+        rm = pm.p;
+        idet = 1.0 / powt_mul(pm, pm).t;
+        s_r[c] = r1.p;
+        s_sd[c] = a.inv_n * double(m) / D;
+    }
+    __syncthreads();
+
+    const double r = s_r[c];
+    {
+        double fl = 0.0, bl = 0.0;
+#pragma unroll
+        for (int i = 0; i < SMAX; ++i) {
+            if (i < ln) fl = fma(r, fl, g[i]);
+            bl = fma(r, bl, g[SMAX - 1 - i]);   // rows past ln are 0: bl stays 0 until row ln - 1
+        }
+        s_f[sj][c] = fl;
+        s_b[sj][c] = bl;
+    }
+    __syncthreads();
+
+    if (t < TQ) {
+        double acc = 0.0, bcc = 0.0;
+        for (int k = 0; k < nseg; ++k) {
+            const int kb = nseg - 1 - k;
+            const double fk = s_f[k][c], bk = s_b[kb][c];
+            s_f[k][c] = acc;
+            s_b[kb][c] = bcc;
+            acc = fma(acc, k == nseg - 1 ? rsr : rsl, fk);
+            bcc = fma(bcc, k == 0 ? rsr : rsl, bk);
+        }
+        const double fm1 = (bcc + rm * acc) * idet, bm = (acc + rm * bcc) * idet;
+        double pf = 1.0, pb = 1.0;
+        for (int k = 0; k < nseg; ++k) {
+            const int kb = nseg - 1 - k;
+            s_f[k][c] = fma(pf, fm1, s_f[k][c]);
+            s_b[kb][c] = fma(pb, bm, s_b[kb][c]);
+            pf *= rsl;
+            pb *= k == 0 ? rsr : rsl;
+        }
+    }
+    __syncthreads();
+
+    if (!valid) return;
+    const double sd = s_sd[c], bin = s_b[sj][c];
+    double fv = s_f[sj][c];
+    {
+        double bv = bin;
+#pragma unroll
+        for (int i = SMAX - 1; i >= 0; --i)
+            if (i < ln) {
+                bv = fma(r, bv, g[i]);
+                g[i] = bv;
+            }
+    }
+    double* pout = a.out + base;
+#pragma unroll
+    for (int i = 0; i < SMAX; ++i)
+        if (i < ln) {
+            const double gn = i + 1 < ln ? g[i + 1] : bin;
+            __builtin_nontemporal_store(sd * fma(r, fv, g[i]), pout);
+            pout += a.stride;
+            fv = fma(r, fv - gn, g[i]);
         }
 }
 
@@ -3124,9 +3416,15 @@ static void launch_trig(const SpecArgs& a, hipStream_t s, int sl, int nseg, int 
     auto go = [&](auto kern, uint32_t tq) {
         klaunch(kern, dim3((a.nlines + tq - 1) / tq), dim3(tq * uint32_t(nseg)), 0, s, a, sl, nseg, sr);
     };
+    // the factorised solve (k_trigr, round 6) unless a probe build asks for k_trig (MVTV_TRI_IIR=0)
+    static const bool thomas = [] {
+        const char* e = probe_env("MVTV_TRI_IIR");
+        return e && std::atoi(e) == 0;
+    }();
 #define MVTV_TRIG(SM, TQ, NS)                                                                                   \
     do {                                                                                                        \
-        if (sr != sl) go(k_trig<SM, TQ, NS, true>, uint32_t(TQ));                                               \
+        if (!thomas) go(k_trigr<SM, TQ, NS>, uint32_t(TQ));                                                     \
+        else if (sr != sl) go(k_trig<SM, TQ, NS, true>, uint32_t(TQ));                                          \
         else go(k_trig<SM, TQ, NS, false>, uint32_t(TQ));                                                       \
         return;                                                                                                 \
     } while (0)
@@ -3188,8 +3486,68 @@ static void launch_tri_seg(SpecArgs& a, hipStream_t s) {
     }
 }
 
+template <int L, int SEG, int TQL>
+static bool launch_trir_l(SpecArgs& a, hipStream_t s) {
+    if constexpr (trir::Shape<L, SEG, TQL>::NT <= 1024 && trir::Shape<L, SEG, TQL>::NSEG >= 2) {
+        klaunch(k_trir<L, SEG, TQL>, dim3((a.nlines + uint32_t(TQL) - 1) / uint32_t(TQL)),
+                dim3(trir::Shape<L, SEG, TQL>::NT), 0, s, a);
+        return true;
+    }
+    return false;
+}
+
+template <int SEG, int TQL>
+static bool launch_trir_seg(SpecArgs& a, hipStream_t s) {
+    if (a.stride < uint32_t(TQL)) return false;
+    a.tq = TQL;
+    a.xcd = 0;
+    switch (a.L) {
+        case 6: return launch_trir_l<6, SEG, TQL>(a, s);
+        case 7: return launch_trir_l<7, SEG, TQL>(a, s);
+        case 8: return launch_trir_l<8, SEG, TQL>(a, s);
+        case 9: return launch_trir_l<9, SEG, TQL>(a, s);
+        case 10: return launch_trir_l<10, SEG, TQL>(a, s);
+    }
+    return false;
+}
+
+// The last-dimension pass of 3-D / 4-D meshes (16-line tiles in tri_tiles) by the factorised line solve. Tiles, where
+// the lines fill >= 256 workgroups of 64: 64 lines (512-B rows per wave load) of 32-row segments up to 256-point lines
+// (256 / 512 threads), 32 lines of 16-row segments (1024 threads, 64 VGPRs: two workgroups a CU) at 512, 32 lines of
+// 32-row segments at 1024; 16 lines of 16-row segments otherwise. Against k_tri (round 6, one box, kernel trace,
+// profiles/r06/v1_trir): 512^3 441 -> 392 us, 256^3 73 -> 49 us, 128^4 948 -> 797 us. Probe builds: MVTV_TRI_IIR=0
+// takes k_tri, "SEG,TQ" forces a tile.
+static bool launch_trir(SpecArgs& a, hipStream_t s) {
+    static const int cfg = [] {
+        const char* e = probe_env("MVTV_TRI_IIR");
+        if (!e) return -1;
+        int sg = 0, tq = 0;
+        if (std::sscanf(e, "%d,%d", &sg, &tq) != 2) return 0;
+        return sg * 1000 + tq;
+    }();
+    switch (cfg) {
+        case -1: break;
+        case 32064: return launch_trir_seg<32, 64>(a, s);
+        case 16064: return launch_trir_seg<16, 64>(a, s);
+        case 16032: return launch_trir_seg<16, 32>(a, s);
+        case 32032: return launch_trir_seg<32, 32>(a, s);
+        case 32016: return launch_trir_seg<32, 16>(a, s);
+        case 16016: return launch_trir_seg<16, 16>(a, s);
+        default: return false;
+    }
+    if (a.nlines / 64u >= 256u && a.stride >= 64u) {
+        if (a.L <= 8) return launch_trir_seg<32, 64>(a, s);
+        if (a.L == 9) return launch_trir_seg<16, 32>(a, s);
+        return launch_trir_seg<32, 32>(a, s);
+    }
+    return launch_trir_seg<16, 16>(a, s);
+}
+
 static void launch_tri(SpecArgs& a, hipStream_t s, int tq) {
     a.tq = tq;
+    if (tq == tri::TQ && launch_trir(a, s)) return;
+    a.tq = tq;
+    a.xcd = 0;
     if (tq == tri::TQ) {
         a.xcd = 0;
         static const int seg = [] {
