@@ -3,7 +3,7 @@
 one-GPU run of the same mesh (rcpp-code/MultivarTV/src/solvers.cpp:110-133 decomposed):
 iterations and rho exact, theta to 1e-11 of max|theta| (only the order of the global sums differs), the norms
 to 1e-9. Shapes: the metric's 512^3 over 2 processes (256 planes each), config 5's 128^4 over 4 (32 planes of
-dim 3 each), a weighted CV fold (the distributed PCG-spectral solve: one all-reduce per dot product) and a
+dim 3 each), world 8 as the driver's 8-GPU runs use it (a 3-D and a 4-D mesh, 8 and 4 planes per rank), a weighted CV fold (the distributed PCG-spectral solve: one all-reduce per dot product) and a
 tolerance-mode run to convergence over 3. A rank whose loop fails ends its peers' waits with an error.
 
 The children are started with multiprocessing's spawn (a fresh interpreter each) and use gloo only to hand over
@@ -149,8 +149,9 @@ def test_failing_rank_ends_its_peers(tmp_path):
 
 
 @pytest.mark.parametrize("m,world,iters", [([48, 48, 40], 3, 6), ([80, 80, 33], 2, 0), ([128, 128, 128, 128], 4, 2),
-                                           ([512, 512, 512], 2, 2)],
-                         ids=["3d_3proc", "tolerance_2proc", "config5_128_4d_4proc", "metric_512cubed_2proc"])
+                                           ([512, 512, 512], 2, 2), ([96, 96, 64], 8, 5), ([32, 32, 32, 32], 8, 3)],
+                         ids=["3d_3proc", "tolerance_2proc", "config5_128_4d_4proc", "metric_512cubed_2proc",
+                              "3d_8proc", "4d_8proc"])
 def test_slab_processes_match_one_gpu(tmp_path, m, world, iters):
     lam = 1.0 if iters else 0.4
     th, rho, st, t0 = _one_gpu(m, lam, iters)
