@@ -344,8 +344,15 @@ hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, in
                            const AdmmCtl* ctl, double sigma = 1.0, double w0 = 1.0, const int32_t* skip = nullptr);
 // a block of n planes splits into k_tris segments (<= 64 of <= 32 rows): false for e.g. a prime n > 64
 bool tri_slab_ok(uint32_t n);
-hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint32_t chunk, int G, const AdmmCtl* ctl,
-                            const int32_t* skip = nullptr);
+// The factorised form (k_trisr, the default; round 6): phase 1 writes 2 numbers per line [chunk s][2][line in chunk]
+// (the block's F at its last row, B at its first), the interface gives every block its 2 carries, phase 3 reads them
+// from lr; the Thomas form (k_tris, probe builds with MVTV_TRI_IIR=0) exchanges 6 and 2. tri_slab_ncoef(): the phase-1
+// numbers per line (the first all-to-all's count). launch_tri_iface: og = the owned planes' geometry (its dims
+// 0..p-2 and the line constants), rank = the chunk's owner, mg = the global plane count.
+int tri_slab_ncoef();
+hipError_t launch_tri_iface(const SpecPlan& sp, const Geom& og, hipStream_t s, double* coef_in, double* lr_out,
+                            uint32_t chunk, int G, int rank, uint32_t mg, const AdmmCtl* ctl, double sigma = 1.0,
+                            double w0 = 1.0, const int32_t* skip = nullptr);
 // z-marching 3-D edge kernels (mvtv_admm3d.hip); same partials layout as launch_edge_update /
 // launch_gather, *nparts workgroup rows
 bool edge3d_ok(const Geom& g);

@@ -878,9 +878,9 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
     const bool fold_path = fused ? P->g.p == 3 : (P->g.p == 4 && P->e3d && P->g4 != nullptr && gather4_ok(P->g));
     const bool fold = fold_path && !wd && m0 >= 8 && m0 <= 4096 && (m0 & (m0 - 1)) == 0 &&
                       !probe_env("MVTV_FOLD_OFF") && !probe_env("MVTV_DCT_LDS");
-    // interface buffers of the distributed line solves (16 numbers per line): the 6 coefficients of this
-    // rank's blocks by chunk, the chunk's coefficients from every rank, the (L, R) values by rank, and the
-    // values of this rank's lines by chunk. One rank: the line solves are local, no buffers, no transfers,
+    // interface buffers of the distributed line solves (16 numbers per line): the phase-1 numbers of this rank's
+    // blocks by chunk (2 per line, the factorised form; 6 with the Thomas form of probe builds), the chunk's from
+    // every rank, the 2 carries (Thomas: L, R values) by rank, and those of this rank's lines by chunk. One rank: the line solves are local, no buffers, no transfers,
     // unless MVTV_SLAB_DISTRIBUTED=1 asks for the distributed path at one rank (its transfers to itself),
     // which runs every collective call of the G-rank loop on one GPU
     const char* force = std::getenv("MVTV_SLAB_DISTRIBUTED");
@@ -1077,8 +1077,9 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
         } else {
             HIP_TRY(launch_tri_slab(P->spec, og, s, 1, z, co_send, nullptr, uint32_t(ch), rk > 0, rk < G - 1, scale,
                                     nullptr, sigma, w0, skip));
-            MVTV_TRY(crit_a2a(co_send, co_recv, 6, EV_CO, EV_COD));
-            HIP_TRY(launch_tri_iface(s, co_recv, lr_send, uint32_t(ch), G, nullptr, skip));
+            MVTV_TRY(crit_a2a(co_send, co_recv, size_t(tri_slab_ncoef()), EV_CO, EV_COD));
+            HIP_TRY(launch_tri_iface(P->spec, og, s, co_recv, lr_send, uint32_t(ch), G, rk, sg.mg, nullptr, sigma, w0,
+                                     skip));
             MVTV_TRY(crit_a2a(lr_send, lr_recv, 2, EV_LR, EV_LRD));
             HIP_TRY(launch_tri_slab(P->spec, og, s, 3, z, nullptr, lr_recv, uint32_t(ch), rk > 0, rk < G - 1, scale,
                                     nullptr, sigma, w0, skip));
@@ -1195,8 +1196,8 @@ mvtv_status slab_run(mvtv_problem* P, mvtv_comm* C, const mvtv_admm_opts* opts, 
                 HIP_TRY(launch_tri_slab(P->spec, og, s, 1, th, co_send, nullptr, uint32_t(ch), rk > 0, rk < G - 1, scale,
                                         P->ctl));
                 P->tstop(h);
-                MVTV_TRY(crit_a2a(co_send, co_recv, 6, EV_CO, EV_COD));
-                HIP_TRY(launch_tri_iface(s, co_recv, lr_send, uint32_t(ch), G, P->ctl));
+                MVTV_TRY(crit_a2a(co_send, co_recv, size_t(tri_slab_ncoef()), EV_CO, EV_COD));
+                HIP_TRY(launch_tri_iface(P->spec, og, s, co_recv, lr_send, uint32_t(ch), G, rk, sg.mg, P->ctl));
                 MVTV_TRY(crit_a2a(lr_send, lr_recv, 2, EV_LR, EV_LRD));
                 h = P->tstart(MVTV_K_DCT);
                 HIP_TRY(launch_tri_slab(P->spec, og, s, 3, th, nullptr, lr_recv, uint32_t(ch), rk > 0, rk < G - 1, scale,

@@ -3308,6 +3308,193 @@ __global__ __launch_bounds__(256) void k_tris_iface(double* __restrict__ co, dou
     lr[l] = 0.0;   // L of rank 0 (the mesh's end)
 }
 
+// ---------------------------------------------------------------------------------------------
+// The slab line solves by the factorised operator (round 6; k_trir's recursions F_i = f_i + r F_{i-1},
+// B_i = f_i + r B_{i+1}, x = (F + B - f) / D). A rank's block of a line enters the global recursions only through
+// two numbers: F at its last row and B at its first row, each from zero carries (phase 1). The chunk owner combines
+// the ranks' pairs with the multipliers r^n_r of the block lengths and closes the mirror (k_trisr_iface): every
+// block's carries, F into its first row and B into its last. Phase 3 reruns the block's recursions from them. Two
+// numbers per line cross the ranks each way (6 + 2 with the Thomas responses of k_tris), and no step divides per row.
+template <int PHASE, int SMAX, int TQ = tris::TQ, int NS = tris::NSMAX>
+__global__ __launch_bounds__(1024) void k_trisr(const SpecArgs a, int sl, int nseg, double* __restrict__ x,
+                                                double* __restrict__ coef, const double* __restrict__ lr,
+                                                uint32_t chunk, int, int, double scale) {
+    double sigma = a.sigma;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+    }
+    __shared__ double s_f[NS][TQ], s_b[NS][TQ];
+    __shared__ double s_r[TQ], s_sd[TQ];
+    const int t = threadIdx.x, c = t % TQ, sj = t / TQ;
+    const uint32_t q0 = blockIdx.x * uint32_t(TQ);
+    const uint32_t q = q0 + uint32_t(c);
+    const bool valid = q < a.nlines;
+    const uint32_t qq = valid ? q : q0;
+    const size_t base = size_t(qq) + size_t(sj * sl) * a.stride;   // lines are contiguous: stride = plane
+
+    double lamv[kMaxDims] = {0, 0, 0, 0};
+    if (t < TQ) {
+        uint32_t rest = qq;
+        for (int jj = 0; jj < a.p - 1; ++jj) {
+            const uint32_t qd = (jj < a.p - 2) ? a.fd[jj].div(rest) : 0u;
+            lamv[jj] = a.lam[a.lam_off[jj] + (rest - qd * a.m[jj])];
+            rest = qd;
+        }
+    }
+    double g[SMAX];
+#pragma unroll
+    for (int i = 0; i < SMAX; ++i)
+        g[i] = (valid && i < sl) ? __builtin_nontemporal_load(x + base + size_t(i) * a.stride) : 0.0;
+    double fin = 0.0, bout = 0.0, rsl = 0.0;   // t < TQ, phase 3: the block's carries; r^sl
+    if (t < TQ) {
+        if (PHASE == 3) {
+            const uint32_t s = qq / chunk, l = qq - s * chunk;
+            fin = lr[(size_t(s) * 2) * chunk + l];
+            bout = lr[(size_t(s) * 2 + 1) * chunk + l];
+        }
+        double c0 = a.w0, c1 = 0.0;
+        for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
+            if (a.cS[Sm] == 0.0) continue;
+            double prod = sigma * a.cS[Sm];
+            for (int jj = 0; jj < a.p - 1; ++jj)
+                if ((Sm >> jj) & 1) prod *= lamv[jj];
+            if ((Sm >> (a.p - 1)) & 1) c1 += prod;
+            else c0 += prod;
+        }
+        const double D = sqrt(c0 * (c0 + 4.0 * c1));
+        const double den = 1.0 / (c0 + 2.0 * c1 + D);
+        const PowT r1{2.0 * c1 * den, (c0 + D) * den};
+        rsl = powt_pow(r1, uint32_t(sl)).p;
+        s_r[c] = r1.p;
+        s_sd[c] = scale / D;
+    }
+    __syncthreads();
+
+    const double r = s_r[c];
+    {
+        double fl = 0.0, bl = 0.0;
+#pragma unroll
+        for (int i = 0; i < SMAX; ++i) {
+            if (i < sl) fl = fma(r, fl, g[i]);
+            bl = fma(r, bl, g[SMAX - 1 - i]);   // rows past sl are 0
+        }
+        s_f[sj][c] = fl;
+        s_b[sj][c] = bl;
+    }
+    __syncthreads();
+
+    if (t < TQ) {
+        // phase 1: the block's F at its last row and B at its first row from zero carries; phase 3: every
+        // segment's carries from the block's
+        double acc = PHASE == 3 ? fin : 0.0, bcc = PHASE == 3 ? bout : 0.0;
+        for (int k = 0; k < nseg; ++k) {
+            const int kb = nseg - 1 - k;
+            const double fk = s_f[k][c], bk = s_b[kb][c];
+            if (PHASE == 3) {
+                s_f[k][c] = acc;
+                s_b[kb][c] = bcc;
+            }
+            acc = fma(acc, rsl, fk);
+            bcc = fma(bcc, rsl, bk);
+        }
+        if (PHASE == 1 && valid) {   // [chunk s][2][line in chunk]: F_last, B_first
+            const uint32_t s = q / chunk, l = q - s * chunk;
+            coef[(size_t(s) * 2) * chunk + l] = acc;
+            coef[(size_t(s) * 2 + 1) * chunk + l] = bcc;
+        }
+    }
+    if constexpr (PHASE == 3) {
+        __syncthreads();
+        if (!valid) return;
+        const double sd = s_sd[c], bin = s_b[sj][c];
+        double fv = s_f[sj][c];
+        {
+            double bv = bin;
+#pragma unroll
+            for (int i = SMAX - 1; i >= 0; --i)
+                if (i < sl) {
+                    bv = fma(r, bv, g[i]);
+                    g[i] = bv;
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < SMAX; ++i)
+            if (i < sl) {
+                const double gn = i + 1 < sl ? g[i + 1] : bin;
+                __builtin_nontemporal_store(sd * fma(r, fv, g[i]), x + base + size_t(i) * a.stride);
+                fv = fma(r, fv - gn, g[i]);
+            }
+    }
+}
+
+// the chunk owner's lines (global line q = rank * chunk + l): from every rank's (F_last, B_first) [r][2][chunk] the
+// carries of every rank's block, (F into its first row, B into its last) [r][2][chunk], with the mirror closure at the
+// mesh's ends. Rank k's block: planes [floor(mg k / G), floor(mg (k + 1) / G)).
+__global__ __launch_bounds__(256) void k_trisr_iface(const SpecArgs a, const double* __restrict__ co,
+                                                     double* __restrict__ lr, uint32_t chunk, int G, int rank,
+                                                     uint32_t mg) {
+    double sigma = a.sigma;
+    if (a.skip && *a.skip) return;
+    if (a.ctl) {
+        if (a.ctl->done) return;
+        sigma = a.ctl->sigma;
+    }
+    const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= chunk) return;
+    const size_t C = chunk;
+    double lamv[kMaxDims] = {0, 0, 0, 0};
+    uint32_t rest = uint32_t(rank) * chunk + l;
+    for (int jj = 0; jj < a.p - 1; ++jj) {
+        const uint32_t qd = (jj < a.p - 2) ? a.fd[jj].div(rest) : 0u;
+        lamv[jj] = a.lam[a.lam_off[jj] + (rest - qd * a.m[jj])];
+        rest = qd;
+    }
+    double c0 = a.w0, c1 = 0.0;
+    for (int Sm = 1; Sm < (1 << a.p); ++Sm) {
+        if (a.cS[Sm] == 0.0) continue;
+        double prod = sigma * a.cS[Sm];
+        for (int jj = 0; jj < a.p - 1; ++jj)
+            if ((Sm >> jj) & 1) prod *= lamv[jj];
+        if ((Sm >> (a.p - 1)) & 1) c1 += prod;
+        else c0 += prod;
+    }
+    const double D = sqrt(c0 * (c0 + 4.0 * c1));
+    const double den = 1.0 / (c0 + 2.0 * c1 + D);
+    const PowT r1{2.0 * c1 * den, (c0 + D) * den};
+    // the multipliers r^n_k of the blocks: n_k = floor(mg (k + 1) / G) - floor(mg k / G) takes two values at most
+    const uint32_t nlo = mg / uint32_t(G);
+    const PowT plo = powt_pow(r1, nlo);
+    const double rlo = plo.p, rhi = plo.p * r1.p;
+    auto rblk = [&](int k) {
+        const uint32_t n = uint32_t(uint64_t(mg) * uint64_t(k + 1) / uint64_t(G) - uint64_t(mg) * uint64_t(k) / uint64_t(G));
+        return n == nlo ? rlo : rhi;
+    };
+    // forward: F into block k's first row from the blocks before it (zero at the mesh's start)
+    double acc = 0.0;
+    for (int k = 0; k < G; ++k) {
+        lr[(size_t(k) * 2) * C + l] = acc;
+        acc = fma(acc, rblk(k), co[(size_t(k) * 2) * C + l]);
+    }
+    double bcc = 0.0;
+    for (int k = G - 1; k >= 0; --k) {
+        lr[(size_t(k) * 2 + 1) * C + l] = bcc;
+        bcc = fma(bcc, rblk(k), co[(size_t(k) * 2 + 1) * C + l]);
+    }
+    const PowT pm = powt_pow(r1, mg);
+    const double idet = 1.0 / powt_mul(pm, pm).t;
+    const double fm1 = (bcc + pm.p * acc) * idet, bm = (acc + pm.p * bcc) * idet;
+    double pf = 1.0, pb = 1.0;
+    for (int k = 0; k < G; ++k) {
+        const int kb = G - 1 - k;
+        lr[(size_t(k) * 2) * C + l] = fma(pf, fm1, lr[(size_t(k) * 2) * C + l]);
+        lr[(size_t(kb) * 2 + 1) * C + l] = fma(pb, bm, lr[(size_t(kb) * 2 + 1) * C + l]);
+        pf *= rblk(k);
+        pb *= rblk(kb);
+    }
+}
+
 static void tris_seg(uint32_t n, int* sl, int* nseg) {
     // >= 4 segments when the block allows it, segments of <= 16 rows (32 past 1024 rows), <= 64 segments
     uint32_t s = std::max<uint32_t>(1u, std::min<uint32_t>(n > 1024u ? 32u : 16u, n / 4u));
@@ -3321,6 +3508,15 @@ bool tri_slab_ok(uint32_t n) {
     tris_seg(n, &sl, &nseg);
     return n >= 1 && sl <= 32 && nseg <= tris::NSMAX;
 }
+
+static bool tris_thomas() {   // probe builds: MVTV_TRI_IIR=0 keeps the Thomas form (k_tris, 6 + 2 numbers per line)
+    static const bool th = [] {
+        const char* e = probe_env("MVTV_TRI_IIR");
+        return e && std::atoi(e) == 0;
+    }();
+    return th;
+}
+int tri_slab_ncoef() { return tris_thomas() ? 6 : 2; }
 
 hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, int phase, double* x, double* coef,
                            const double* lr, uint32_t chunk, int lo_ext, int hi_ext, double scale,
@@ -3351,6 +3547,7 @@ hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, in
     // 64-line tiles with the segment arrays sized to the block (<= 16 segments: <= 1024 threads) where the lines
     // fill >= 128 such workgroups; otherwise 16-line tiles sized for any block (<= 64 segments)
     static const bool wide_off = probe_env("MVTV_TRIS_NARROW") != nullptr;
+    const bool thomas = tris_thomas();
     auto go = [&](auto kern, uint32_t tq) {
         klaunch(kern, dim3((a.nlines + tq - 1) / tq), dim3(tq * uint32_t(nseg)), 0, s, a, sl, nseg, x, coef, lr, chunk,
                 lo_ext, hi_ext, scale);
@@ -3360,29 +3557,52 @@ hipError_t launch_tri_slab(const SpecPlan& sp, const Geom& og, hipStream_t s, in
         // segments of <= 16 rows keep the row registers at 16 (blocks up to 256 planes here); <= 4 rows (blocks of
         // <= 16 planes: a 4-D rank at G = 8) size the line constants for 4
         const int ns = nseg <= 4 ? 4 : (nseg <= 8 ? 8 : 16);
-        if (sl <= 4 && ns == 4) return phase == 1 ? go(k_tris<1, 4, 64, 4>, 64u) : go(k_tris<3, 4, 64, 4>, 64u);
+        if (sl <= 4 && ns == 4) {
+            if (phase == 1) return thomas ? go(k_tris<1, 4, 64, 4>, 64u) : go(k_trisr<1, 4, 64, 4>, 64u);
+            return thomas ? go(k_tris<3, 4, 64, 4>, 64u) : go(k_trisr<3, 4, 64, 4>, 64u);
+        }
         if (sl <= 16) {
             if (phase == 1) {
-                if (ns == 4) return go(k_tris<1, 16, 64, 4>, 64u);
-                if (ns == 8) return go(k_tris<1, 16, 64, 8>, 64u);
-                return go(k_tris<1, 16, 64, 16>, 64u);
+                if (ns == 4) return thomas ? go(k_tris<1, 16, 64, 4>, 64u) : go(k_trisr<1, 16, 64, 4>, 64u);
+                if (ns == 8) return thomas ? go(k_tris<1, 16, 64, 8>, 64u) : go(k_trisr<1, 16, 64, 8>, 64u);
+                return thomas ? go(k_tris<1, 16, 64, 16>, 64u) : go(k_trisr<1, 16, 64, 16>, 64u);
             }
-            if (ns == 4) return go(k_tris<3, 16, 64, 4>, 64u);
-            if (ns == 8) return go(k_tris<3, 16, 64, 8>, 64u);
-            return go(k_tris<3, 16, 64, 16>, 64u);
+            if (ns == 4) return thomas ? go(k_tris<3, 16, 64, 4>, 64u) : go(k_trisr<3, 16, 64, 4>, 64u);
+            if (ns == 8) return thomas ? go(k_tris<3, 16, 64, 8>, 64u) : go(k_trisr<3, 16, 64, 8>, 64u);
+            return thomas ? go(k_tris<3, 16, 64, 16>, 64u) : go(k_trisr<3, 16, 64, 16>, 64u);
         }
     }
     const uint32_t tq = uint32_t(tris::TQ);
-    if (phase == 1 && sl <= 16) return go(k_tris<1, 16>, tq);
-    if (phase == 1) return go(k_tris<1, 32>, tq);
-    if (sl <= 16) return go(k_tris<3, 16>, tq);
-    return go(k_tris<3, 32>, tq);
+    if (phase == 1 && sl <= 16) return thomas ? go(k_tris<1, 16>, tq) : go(k_trisr<1, 16>, tq);
+    if (phase == 1) return thomas ? go(k_tris<1, 32>, tq) : go(k_trisr<1, 32>, tq);
+    if (sl <= 16) return thomas ? go(k_tris<3, 16>, tq) : go(k_trisr<3, 16>, tq);
+    return thomas ? go(k_tris<3, 32>, tq) : go(k_trisr<3, 32>, tq);
 }
 
-hipError_t launch_tri_iface(hipStream_t s, double* coef_in, double* lr_out, uint32_t chunk, int G, const AdmmCtl* ctl,
+
+hipError_t launch_tri_iface(const SpecPlan& sp, const Geom& og, hipStream_t s, double* coef_in, double* lr_out,
+                            uint32_t chunk, int G, int rank, uint32_t mg, const AdmmCtl* ctl, double sigma, double w0,
                             const int32_t* skip) {
     if (G < 1 || chunk == 0) return hipErrorInvalidValue;
-    klaunch(k_tris_iface, dim3((chunk + 255) / 256), dim3(256), 0, s, coef_in, lr_out, chunk, G, ctl, skip);
+    if (tris_thomas()) {
+        klaunch(k_tris_iface, dim3((chunk + 255) / 256), dim3(256), 0, s, coef_in, lr_out, chunk, G, ctl, skip);
+        return hipGetLastError();
+    }
+    SpecArgs a{};
+    a.ctl = ctl;
+    a.skip = skip;
+    a.sigma = sigma;
+    a.w0 = w0;
+    a.lam = sp.lam;
+    for (int j = 0; j < kMaxDims; ++j) {
+        a.lam_off[j] = sp.lam_off[j];
+        a.m[j] = og.m[j];
+    }
+    for (int j = 0; j < kMaxDims - 1; ++j) a.fd[j] = og.fd[j];
+    for (int S = 0; S < 16; ++S) a.cS[S] = og.cS[S];
+    a.p = og.p;
+    a.d = og.p - 1;
+    klaunch(k_trisr_iface, dim3((chunk + 255) / 256), dim3(256), 0, s, a, coef_in, lr_out, chunk, G, rank, mg);
     return hipGetLastError();
 }
 

@@ -2,7 +2,7 @@
 # --kernel-trace only beside --pmc), plus the list of counters this GPU exposes.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/${CTR_OUT:-gpurun_out}
+O=$R/gpurun_out/${CTR_OUT:-ctr}   # always under gpurun_out (merged back)
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 60 rocprofv3 -L > $O/counters_list.txt 2>&1
