@@ -412,7 +412,7 @@ def slab_main(a, D, comm=None):
                    "theta_solver": "spectral (local transforms; the last dimension's line solves substructured "
                                    "over the ranks)" if distributed else "spectral (one rank: the whole lines local)",
                    "parallelism": f"slab x{nranks} ({transport}: halo planes, "
-                                  f"{'6+2 numbers per line all-to-all, ' if distributed else ''}7-sum all-reduce)"},
+                                  f"{'2+2 numbers per line all-to-all, ' if distributed else ''}7-sum all-reduce)"},
         "rccl_ranks": rccl_ranks, "rccl_library": slab.Comm.library() if rccl_ranks else None,
         "transport": transport,
         "roofline": _roofline(tim), "kernels_rank0": per,

@@ -3676,7 +3676,10 @@ static void launch_trig(const SpecArgs& a, hipStream_t s, int sl, int nseg, int 
 // for <= 64 (16 rows per segment up to 1024 points, 32 at 2048), the stride holds the tile's lines, and
 // either 16-line tiles fill the chip (>= 256 workgroups: 3-D and 4-D meshes) or, for the few 2048-point
 // lines of a 2-D mesh, 8-line tiles in XCD runs (2048^2: 4844 -> 5145 ADMM it/s on one box; at 1024^2 the
-// FFT pass stays faster: 9866 against 9381 with 8-line and 9050 with 4-line tiles, profiles/r02/v19_tri2d).
+// FFT pass stays faster: 9866 against 9381 with 8-line and 9050 with 4-line tiles, profiles/r02/v19_tri2d). Round 6, with
+// the factorised line solve (k_trir): 1024- and 512-point lines take it too, on 4-line tiles (one box, two reps each,
+// profiles/r06/v8_tri2d: 1024^2 12928 / 12925 -> 14312 / 14249 ADMM it/s, 512^2 18185 / 18166 -> 20543 / 20357; 8-line
+// tiles 14173 / 20397; 2048^2 keeps 8-line tiles: 6279 / 6226, 4-line 5319).
 // Probe builds: MVTV_DCT_TRI2D=0 / 4 / 8 forces the 2-D choice.
 static int tri_tiles(const SpecArgs& a, int mode, bool formb) {
     if (mode != SPEC_MID || a.d == 0 || formb) return 0;
@@ -3688,7 +3691,7 @@ static int tri_tiles(const SpecArgs& a, int mode, bool formb) {
         const char* v = probe_env("MVTV_DCT_TRI2D");
         return v ? std::atoi(v) : -1;
     }();
-    const int t2d = t2d_env >= 0 ? t2d_env : (a.L == 11 ? 8 : 0);
+    const int t2d = t2d_env >= 0 ? t2d_env : (a.L == 11 ? 8 : (a.L >= 9 ? 4 : 0));
     if (t2d != 4 && t2d != 8) return 0;
     if (uint32_t(t2d) > a.stride || (a.nlines / uint32_t(t2d)) % 8u != 0u) return 0;
     return t2d;
@@ -3799,6 +3802,30 @@ static void launch_tri(SpecArgs& a, hipStream_t s, int tq) {
     }
     a.xcd = 1;   // 2-D: narrow tiles in XCD runs (grid a multiple of 8, tri_tiles)
     const dim3 grid(a.nlines / uint32_t(tq));
+    static const bool thomas = [] {
+        const char* e = probe_env("MVTV_TRI_IIR");
+        return e && std::atoi(e) == 0;
+    }();
+    if (!thomas) {   // the factorised solve (k_trir): 2048-point lines in 64 segments of 32 rows, else 16-row segments
+        if (a.L == 11) {
+            if (tq == 4) klaunch(k_trir<11, 32, 4>, grid, dim3(trir::Shape<11, 32, 4>::NT), 0, s, a);
+            else klaunch(k_trir<11, 32, 8>, grid, dim3(trir::Shape<11, 32, 8>::NT), 0, s, a);
+            return;
+        }
+        switch (a.L * 16 + tq) {
+            case 6 * 16 + 4: klaunch(k_trir<6, 16, 4>, grid, dim3(trir::Shape<6, 16, 4>::NT), 0, s, a); return;
+            case 6 * 16 + 8: klaunch(k_trir<6, 16, 8>, grid, dim3(trir::Shape<6, 16, 8>::NT), 0, s, a); return;
+            case 7 * 16 + 4: klaunch(k_trir<7, 16, 4>, grid, dim3(trir::Shape<7, 16, 4>::NT), 0, s, a); return;
+            case 7 * 16 + 8: klaunch(k_trir<7, 16, 8>, grid, dim3(trir::Shape<7, 16, 8>::NT), 0, s, a); return;
+            case 8 * 16 + 4: klaunch(k_trir<8, 16, 4>, grid, dim3(trir::Shape<8, 16, 4>::NT), 0, s, a); return;
+            case 8 * 16 + 8: klaunch(k_trir<8, 16, 8>, grid, dim3(trir::Shape<8, 16, 8>::NT), 0, s, a); return;
+            case 9 * 16 + 4: klaunch(k_trir<9, 16, 4>, grid, dim3(trir::Shape<9, 16, 4>::NT), 0, s, a); return;
+            case 9 * 16 + 8: klaunch(k_trir<9, 16, 8>, grid, dim3(trir::Shape<9, 16, 8>::NT), 0, s, a); return;
+            case 10 * 16 + 4: klaunch(k_trir<10, 16, 4>, grid, dim3(trir::Shape<10, 16, 4>::NT), 0, s, a); return;
+            case 10 * 16 + 8: klaunch(k_trir<10, 16, 8>, grid, dim3(trir::Shape<10, 16, 8>::NT), 0, s, a); return;
+            default: break;
+        }
+    }
     if (a.L == 11) {   // 2048-point lines: 64 segments of 32 rows
         if (tq == 4) klaunch(k_tri<11, 32, 4>, grid, dim3(tri::Shape<11, 32, 4>::NT), 0, s, a);
         else klaunch(k_tri<11, 32, 8>, grid, dim3(tri::Shape<11, 32, 8>::NT), 0, s, a);
