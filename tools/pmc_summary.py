@@ -20,7 +20,8 @@ from collections import defaultdict
 
 NAMES = {"k_plane8": "dct_plane", "k_admm3d": "admm_fused", "k_admm3a": "admm_fused", "k_admm4a": "admm_fused4",
          "k_gather4a": "gather_Dt", "k_gather4b": "gather4_b", "k_edge3d": "edge_update", "k_gather3d": "gather_Dt", "k_dct8": "dct",
-         "k_dct": "dct", "k_dctg": "dct", "k_tri": "dct_tri", "k_trig": "dct_tri",
+         "k_dct": "dct", "k_dctg": "dct", "k_tri": "dct_tri", "k_trig": "dct_tri", "k_trir": "dct_tri", "k_trigr": "dct_tri",
+         "k_trisr": "dct_tris", "k_tris": "dct_tris",
          "k_cg3d": "pcg_fused3d", "k_edge_update": "edge_update", "k_gather": "gather_Dt",
          "k_apply_A": "pcg_apply_A", "k_pcg_update": "pcg_update", "k_pcg_pupdate": "pcg_direction",
          "k_pcg_init": "pcg_init", "copy8": "copy8", "copy16": "copy16"}
