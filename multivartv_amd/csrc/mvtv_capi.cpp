@@ -496,12 +496,16 @@ mvtv_status spectral_solve(mvtv_problem* P, double sigma, const double* oty, con
         P->tstop(h);
         return MVTV_OK;
     }
+    // probe builds: MVTV_DCT_REV=1 takes the other dims in descending order (the first pass, b formed on load, and the
+    // last inverse pass then run along dim p - 2 instead of the contiguous dim 0)
+    static const bool rev = probe_env("MVTV_DCT_REV") != nullptr;
     int order[MVTV_MAX_DIMS], n = 0;
     for (int d = 0; d < p; ++d)
         if (d != mid) order[n++] = d;
+    if (rev) std::reverse(order, order + n);
     order[n++] = mid;
     // m0 = m1 <= 128: dims 0 and 1 in one pass each way (k_plane8: the plane stays on chip between them)
-    const bool plane = mid >= 2 && plane_pass_ok(P->g);
+    const bool plane = !rev && mid >= 2 && plane_pass_ok(P->g);
     if (plane) {
         const int h = P->tstart(ga ? (fold ? MVTV_K_DCT_FOLD : MVTV_K_DCT_FIRST) : MVTV_K_DCT);
         if (ga && fold)

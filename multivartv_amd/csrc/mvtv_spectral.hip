@@ -80,6 +80,7 @@ struct SpecArgs {
     int32_t xrun;             // k_dctg / k_dctm / k_dctb / k_dctb8 / k_trig: the same for any grid (xcd_run)
     PcgFuse pf;               // k_dct8 PC = 1 / 2: the PCG vector work of the preconditioner's d = 0 passes
     int32_t fold;             // FORMB from the folded s (k_dct8, ctl): b = in + fold_ka ga [+ fold_kb gb if ctl->fix]
+    int32_t pair16;           // k_dct8 d = 0 forward / inverse: coefficients through LDS as 16-B pairs (dct_pair16)
     // Bluestein lengths (k_dctb; L = log2 M then, tw = the length-M FFT twiddles): the chirp c[n] = e^{-i pi n^2/m}
     // and the transforms / M of the forward / inverse convolution kernels
     const double2* bchirp;
@@ -704,15 +705,45 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
     // ---- spectrum <-> DCT coefficients for the pairs (k, M-k); k = 0 also takes M/2 -------------
     // the inverse pass issues all 8 coefficient loads before the first LDS write (issued inside the loop,
     // each group waited for its loads before writing LDS: four HBM round trips per workgroup instead of one)
+    // d = 0 with a.pair16: the coefficients of the two real lines cross LDS (the line's exchange slots as M + M doubles)
+    // so that they arrive / leave as 16-B pairs (k, k + 1) of one line, as the other side of these passes does; read or
+    // written directly they are 8-B accesses at positions k and M - k (round 6: the d = 0 forward pass 540 us for 2N
+    // words against 383 for a strided one at 512^3)
+    double* const Xd = reinterpret_cast<double*>(X);
     double2 pre[8];
     if constexpr (MODE == SPEC_INV) {
+        if (D0 && a.pair16) {
+            double2 qa[4], qb[4];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int k = j + s * TPL;
-            pre[2 * s] = ld2(uint32_t(k));
-            pre[2 * s + 1] = ld2(uint32_t(k ? M - k : M / 2));
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const uint32_t i2 = uint32_t(2 * (j + s4 * TPL));
+                qa[s4] = va ? ldnt2(a.in + gaddr(la, i2)) : make_double2(0.0, 0.0);
+                qb[s4] = vb ? ldnt2(a.in + gaddr(lb, i2)) : make_double2(0.0, 0.0);
+            }
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int i2 = 2 * (j + s4 * TPL);
+                *reinterpret_cast<double2*>(Xd + i2) = qa[s4];
+                *reinterpret_cast<double2*>(Xd + M + i2) = qb[s4];
+            }
+            xbar<BAR>();
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = j + s * TPL, kb = k ? M - k : M / 2;
+                pre[2 * s] = make_double2(Xd[k], Xd[M + k]);
+                pre[2 * s + 1] = make_double2(Xd[kb], Xd[M + kb]);
+            }
+            xbar<BAR>();   // every coefficient read before the IFFT input is written over them
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = j + s * TPL;
+                pre[2 * s] = ld2(uint32_t(k));
+                pre[2 * s + 1] = ld2(uint32_t(k ? M - k : M / 2));
+            }
         }
     }
+    double2 fco[8];   // d = 0 forward with a.pair16: the coefficient pairs, written after the loop
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int k = j + s * TPL;
@@ -736,8 +767,13 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
             Xmk = pre[2 * s + 1];
         }
         if (MODE == SPEC_FWD) {
-            st2(uint32_t(ka), Xk);
-            st2(uint32_t(kb), Xmk);
+            if (D0 && a.pair16) {
+                fco[2 * s] = Xk;
+                fco[2 * s + 1] = Xmk;
+            } else {
+                st2(uint32_t(ka), Xk);
+                st2(uint32_t(kb), Xmk);
+            }
             continue;
         }
         if (MODE == SPEC_MID) {
@@ -763,7 +799,27 @@ __global__ __launch_bounds__((spec8::ShapeK<L, TQW>::NT)) void k_dct8(const Spec
             X[spec8::slot(kb, cx)] = make_double2(va2.x - vb2.y, va2.y + vb2.x);
         }
     }
-    if (MODE == SPEC_FWD) return;
+    if (MODE == SPEC_FWD) {
+        if (D0 && a.pair16) {
+            xbar<BAR>();   // every spectrum read before the coefficients are written over it
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = j + s * TPL, kb = k ? M - k : M / 2;
+                Xd[k] = fco[2 * s].x;
+                Xd[M + k] = fco[2 * s].y;
+                Xd[kb] = fco[2 * s + 1].x;
+                Xd[M + kb] = fco[2 * s + 1].y;
+            }
+            xbar<BAR>();
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const int i2 = 2 * (j + s4 * TPL);
+                if (va) stnt2(a.out + gaddr(la, uint32_t(i2)), *reinterpret_cast<const double2*>(Xd + i2));
+                if (vb) stnt2(a.out + gaddr(lb, uint32_t(i2)), *reinterpret_cast<const double2*>(Xd + M + i2));
+            }
+        }
+        return;
+    }
     xbar<BAR>();
 
     // ---- inverse FFT, natural in; the last stage's outputs go straight to HBM, un-permuted ------
@@ -4106,6 +4162,11 @@ hipError_t launch_dct_pass(const SpecPlan& sp, const Geom& g, hipStream_t s, int
     while ((1u << a.L) < m) ++a.L;
     const bool formb = ga != nullptr;
     a.fold = fold ? 1 : 0;   // b from the folded s: k_dct8 (power-of-two m >= 8), asynchronous loop only
+    static const bool pair16 = [] {   // probe builds: MVTV_DCT_P16=0 keeps the d = 0 passes' 8-B coefficient accesses
+        const char* e = probe_env("MVTV_DCT_P16");
+        return !(e && std::atoi(e) == 0);
+    }();
+    a.pair16 = pair16 ? 1 : 0;
     if (m > 4096) return hipErrorInvalidValue;
     if (a.fold && (!formb || !gb || !ctl || (1u << a.L) != m || (1u << a.ls) != a.stride || a.L < 3 ||
                    probe_env("MVTV_DCT_LDS") || mode == SPEC_MID))
