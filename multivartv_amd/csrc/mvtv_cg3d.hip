@@ -575,6 +575,133 @@ hipError_t launch_apply3d(const Geom& g, hipStream_t s, double sigma, int wmode,
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------ k_apply4d
+// The same for p = 4 (config 5's run start g_alpha = D^T D theta_0, rcpp…/solvers.cpp:101, and the PCG operator step
+// of a 4-D W != I solve): a thread owns an (x, y, z) cell and marches dim 3. D^T D's 81-point stencil is even in every
+// offset, so with K[|dx| + 2|dy| + 4|dz| + 8|dw|] a w-plane contributes one 27-point sum s0 (dw = 0 weights) to its own
+// output and one s1 (dw = 1 weights) to the outputs w - 1 and w + 1: q(w) = s1(w - 1) + s0(w) + s1(w + 1), mirrored
+// at the ends. The 27 neighbours of a plane come through L1 / L2 (a 64 x 4 tile's rows are whole 512-B runs);
+// 2N words of HBM traffic against the generic grid-stride k_apply_A's 81 L2 reads per cell (10.2 ms at 128^4).
+struct Apply4dArgs {
+    const double* x;
+    double* q;
+    const double* wdiag;
+    double* partials;
+    const PcgState* st;
+    double K[16];
+    int m0, m1, m2, m3, tiles_x, tiles_y, wchunk, nblocks;
+};
+
+template <int WM, bool DOT>
+__global__ __launch_bounds__(256) void k_apply4d(const Apply4dArgs a) {
+    if (DOT && a.st->done) return;
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const int nxy = a.tiles_x * a.tiles_y, per_w = nxy * a.m2;
+    const int tw = bid / per_w, rem = bid - tw * per_w;
+    const int z = rem / nxy, rxy = rem - z * nxy;
+    const int ty = rxy / a.tiles_x, tx = rxy - ty * a.tiles_x;
+    const int x = tx * 64 + int(threadIdx.x & 63), y = ty * 4 + int(threadIdx.x >> 6);
+    const int m0 = a.m0, m1 = a.m1, m2 = a.m2, m3 = a.m3;
+    double red[1] = {0.0};
+    const bool act = bid < a.nblocks && x < m0 && y < m1;
+    if (!DOT && !act) return;   // no barriers below without DOT
+    const int w0 = tw * a.wchunk, w1 = act ? min(m3, w0 + a.wchunk) : w0;
+    const size_t pl = size_t(m0) * size_t(m1), pl3 = pl * size_t(m2);
+    const int xs[3] = {mirror(x - 1, m0), x, mirror(x + 1, m0)};
+    const size_t ys[3] = {size_t(mirror(y - 1, m1)) * m0, size_t(y) * m0, size_t(mirror(y + 1, m1)) * m0};
+    const size_t zs[3] = {size_t(mirror(z - 1, m2)) * pl, size_t(z) * pl, size_t(mirror(z + 1, m2)) * pl};
+    double K[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) K[t] = a.K[t];
+    // in-plane (x, y, z) sums of plane w by offset class c = |dx| + 2|dy| + 4|dz|
+    auto sums = [&](int w, double& s0, double& s1) {
+        const double* P = a.x + size_t(w) * pl3;
+        double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+                const double* R = P + zs[dz] + ys[dy];
+                const int c = (dy != 1 ? 2 : 0) + (dz != 1 ? 4 : 0);
+                v[c] += R[xs[1]];
+                v[c | 1] += R[xs[0]] + R[xs[2]];
+            }
+        s0 = 0.0;
+        s1 = 0.0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            s0 = fma(K[c], v[c], s0);
+            s1 = fma(K[8 + c], v[c], s1);
+        }
+    };
+    double s0c = 0.0, s1c = 0.0, s0n = 0.0, s1n = 0.0, s1m = 0.0;
+    if (act) {
+        sums(w0, s0c, s1c);
+        if (w0 > 0) sums(w0 - 1, s0n, s1m);
+        else s1m = s1c;
+    }
+    const size_t cell = zs[1] + ys[1] + size_t(x);
+    for (int w = w0; w < w1; ++w) {
+        if (w + 1 < m3) sums(w + 1, s0n, s1n);
+        else s1n = s1c, s0n = s0c;
+        const size_t i = size_t(w) * pl3 + cell;
+        double out = s1m + s0c + s1n;
+        if (WM == W_DIAG) out = fma(a.wdiag[i], a.x[i], out);
+        __builtin_nontemporal_store(out, a.q + i);
+        if constexpr (DOT) red[0] = fma(a.x[i], out, red[0]);
+        s1m = s1c;
+        s0c = s0n;
+        s1c = s1n;
+    }
+    if constexpr (DOT) block_reduce_store<1, 0>(red, a.partials);
+}
+
+hipError_t launch_apply4d(const Geom& g, hipStream_t s, double sigma, int wmode, const double* wdiag,
+                          const double* x, double* q, double* partials, const PcgState* st, int* nparts) {
+    Apply4dArgs a{};
+    a.m0 = int(g.m[0]);
+    a.m1 = int(g.m[1]);
+    a.m2 = int(g.m[2]);
+    a.m3 = int(g.m[3]);
+    a.tiles_x = (a.m0 + 63) / 64;
+    a.tiles_y = (a.m1 + 3) / 4;
+    const long items = long(a.tiles_x) * a.tiles_y * a.m2;   // (tile, z) columns, each marching dim 3
+    int nw = int(std::max<long>(1, std::min<long>(a.m3, 8192 / std::max<long>(1, items))));
+    a.wchunk = (a.m3 + nw - 1) / nw;
+    nw = (a.m3 + a.wchunk - 1) / a.wchunk;
+    if (items * nw > long(kMaxCgBlocks) * kMaxRed) return hipErrorInvalidValue;
+    a.nblocks = int(items * nw);
+    const int grid = (a.nblocks + 7) / 8 * 8;
+    for (int t = 0; t < 16; ++t) {   // K(o) = sigma sum_S cS[S] prod_j f_j(o_j), t = |dx| + 2|dy| + 4|dz| + 8|dw|
+        double kk = 0.0;
+        for (int S = 1; S < 16; ++S) {
+            double prod = g.cS[S];
+            for (int j = 0; j < 4; ++j) {
+                const bool off = (t >> j) & 1;
+                prod *= ((S >> j) & 1) ? (off ? -1.0 : 2.0) : (off ? 0.0 : 1.0);
+            }
+            kk += prod;
+        }
+        a.K[t] = sigma * kk;
+    }
+    if (wmode == W_IDENTITY) a.K[0] += 1.0;
+    a.x = x;
+    a.q = q;
+    a.wdiag = wdiag;
+    a.partials = partials;
+    a.st = st;
+    if (partials) {
+        if (!st || !nparts) return hipErrorInvalidValue;
+        *nparts = grid;
+        if (wmode == W_DIAG) klaunch(k_apply4d<W_DIAG, true>, dim3(grid), dim3(256), 0, s, a);
+        else klaunch(k_apply4d<W_NONE, true>, dim3(grid), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
+    if (wmode == W_DIAG) klaunch(k_apply4d<W_DIAG, false>, dim3(grid), dim3(256), 0, s, a);
+    else klaunch(k_apply4d<W_NONE, false>, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------ k_apply2d
 // The same for p = 2 (configs 2 and 4: the PCG operator step of a CV fold): a thread owns one dim-0
 // column over a chunk of >= 8 rows and marches dim 1; a row contributes s0 = K0 c + K1 (l + r) to its own

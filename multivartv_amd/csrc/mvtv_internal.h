@@ -250,6 +250,10 @@ hipError_t launch_apply2d(const Geom& g, hipStream_t s, double sigma, int wmode,
 hipError_t launch_apply3d(const Geom& g, hipStream_t s, double sigma, int wmode, const double* wdiag,
                           const double* x, double* q, double* partials = nullptr, const PcgState* st = nullptr,
                           int* nparts = nullptr);
+// w-marching q = (W + sigma D^T D) x for p = 4, same contract as launch_apply3d
+hipError_t launch_apply4d(const Geom& g, hipStream_t s, double sigma, int wmode, const double* wdiag,
+                          const double* x, double* q, double* partials = nullptr, const PcgState* st = nullptr,
+                          int* nparts = nullptr);
 hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int wmode, const double* wdiag,
                        double* x, const double* r_in, const double* p_in, double* r_out, double* p_out,
                        const double* oty, const double* ga, double ca,

@@ -855,6 +855,12 @@ hipError_t launch_apply_A(const Geom& g, const Launch& L, double sigma, int wmod
         return launch_apply3d(g, L.stream, sigma, wmode, wdiag, x, q, partials, st, nparts);
     if (a3d && g.p == 2 && g.ibeg == 0 && g.iend == g.N && (!partials || (st && nparts)))
         return launch_apply2d(g, L.stream, sigma, wmode, wdiag, x, q, partials, st, nparts);
+    // 4-D: the w-marching kernel (128^4 run start 10.2 ms with the generic one); falls through when its grid would
+    // overrun the partials rows
+    if (a3d && g.p == 4 && g.ibeg == 0 && g.iend == g.N && (!partials || (st && nparts))) {
+        const hipError_t e = launch_apply4d(g, L.stream, sigma, wmode, wdiag, x, q, partials, st, nparts);
+        if (e != hipErrorInvalidValue) return e;
+    }
     if (nparts) *nparts = L.grid;
     const StencilK sk = make_stencil(g);
     return dispatch_p(g.p, [&](auto pc) {
