@@ -80,6 +80,7 @@ struct Cg3dArgs {
     double acc[8];   // sigma * diag(D^T D) by boundary pattern (bit j: interior along dim j)
     double ca, cb;
     int m0, m1, m2, tiles_x, tiles_y, zchunk, nblocks;
+    int full_sync;   // probe builds (MVTV_CG3D_SYNC=1): __syncthreads in the plane loop instead of LDS-only barriers
 };
 
 // Half-sample mirror into [0, m): -1 -> 0, -2 -> 1, m -> m-1, m+1 -> m-2; clamped beyond.
@@ -126,6 +127,14 @@ __global__ __launch_bounds__(cg3d::Shape<NWV>::NT, 32 / NWV) void k_cg3d(const C
     const double alpha_prev = MODE == 3 ? a.st->alpha_prev : 0.0;
     const double beta = MODE >= 2 ? a.st->beta : 0.0;
     if (threadIdx.x < 8) sD[threadIdx.x] = WM == W_DIAG ? a.acc[threadIdx.x] : 1.0 / (1.0 + a.acc[threadIdx.x]);
+    // the plane loop's barriers order the LDS images only: nothing this launch writes to HBM is read in it (r, p
+    // ping-pong; x is written only where the same thread read it), so they need not wait for the global loads and
+    // stores in flight — with __syncthreads the second barrier of a plane waited for the next plane's loads
+    const bool full_sync = a.full_sync != 0;
+    auto bar = [&]() {
+        if (full_sync) __syncthreads();
+        else lds_barrier();
+    };
 
     const int m0 = a.m0, m1 = a.m1, m2 = a.m2;
     const size_t pl = size_t(m0) * size_t(m1);
@@ -224,7 +233,7 @@ __global__ __launch_bounds__(cg3d::Shape<NWV>::NT, 32 / NWV) void k_cg3d(const C
                 red[2] = fma(rn, rn, red[2]);
             }
         }
-        __syncthreads();
+        bar();
         double k0v[RPW], k1v[RPW], ctr[RPW];
         wave_rows(sU + li, a.K, k0v, k1v, ctr);
         const bool prev_own = e - 1 >= z0 && e - 1 < z1;   // w(e-1) is complete
@@ -301,7 +310,7 @@ __global__ __launch_bounds__(cg3d::Shape<NWV>::NT, 32 / NWV) void k_cg3d(const C
     for (int z = zs; z <= ze; ++z) {
         // ---------------- stage A: plane z of p_i (x_0 in the prologue) on tile + 2
         commit(z);
-        __syncthreads();
+        bar();
         if (z + 1 <= ze) issue(z + 1);
         // ---------------- stage B: plane z feeds s at outputs z-1 (k1), z (k0), z+1 (k1); clamped
         // dim-2 neighbours: plane 0 is its own dz=-1 layer, plane m2-1 its own dz=+1 layer
@@ -320,11 +329,11 @@ __global__ __launch_bounds__(cg3d::Shape<NWV>::NT, 32 / NWV) void k_cg3d(const C
             synced = true;
         }
         if (z == m2 - 1 && z >= ulo && z <= uhi) {
-            if (synced) __syncthreads();   // sU is still being read by the previous plane's stage C
+            if (synced) bar();   // sU is still being read by the previous plane's stage C
             finish_plane(z, true);
             synced = true;
         }
-        if (!synced) __syncthreads();   // stage B's reads of sP before the next commit
+        if (!synced) bar();   // stage B's reads of sP before the next commit
 #pragma unroll
         for (int k = 0; k < RPW; ++k) {
             bm1[k] = b0[k];
@@ -348,6 +357,8 @@ hipError_t launch_cg3d(const Geom& g, hipStream_t s, int mode, double sigma, int
     }();
     const int TY = nwv == 16 ? Shape<16>::TY : Shape<8>::TY;
     Cg3dArgs a{};
+    static const bool full_sync = probe_env("MVTV_CG3D_SYNC") != nullptr;
+    a.full_sync = full_sync ? 1 : 0;
     a.m0 = int(g.m[0]);
     a.m1 = int(g.m[1]);
     a.m2 = int(g.m[2]);
