@@ -201,7 +201,7 @@ mvtv_status mvtv_solve_spectral(mvtv_problem* prob, double sigma, const double* 
  * desc->oty (and desc->wdiag, if any) cover them (ghost values are not used). Rank r owns planes
  * [floor(m r / G), floor(m (r+1) / G)). mvtv_slab_run is the whole variant-B loop of one rank
  * (rcpp…/solvers.cpp:110-133) with its collectives on a communication stream: the substructured line solves'
- * two all-to-alls of 6 and 2 numbers per line, halo planes of theta and of the edge state, one 7-value
+ * two all-to-alls of 2 and 2 numbers per line (each block's two recursion sums, then its two carries), halo planes of theta and of the edge state, one 7-value
  * all-reduce per iteration feeding the device-side adapt_step / stopping decision. With W != I (desc->wdiag)
  * the theta-solve is PCG with the spectral preconditioner of mean(W) I + sigma D^T D (opts pcg_rtol,
  * pcg_max_iter, pcg_strict as mvtv_admm_run), distributed: a halo of the search direction per iteration and
@@ -218,8 +218,10 @@ typedef struct mvtv_slab_desc {
 typedef struct mvtv_comm mvtv_comm;
 mvtv_status mvtv_problem_create_slab(const mvtv_problem_desc* desc, const mvtv_slab_desc* slab, mvtv_problem** out);
 /* RCCL transport (one process per GPU): rank 0 makes the id, every rank passes the same 128 bytes. The first
- * mvtv_slab_run on a communicator splits off a second RCCL communicator (ncclCommSplit, collective) for the halos, so
- * they can run beside the critical-path collectives issued on the problem's stream; MVTV_RCCL_ONE_COMM=1 keeps one */
+ * mvtv_slab_run on a communicator with MVTV_RCCL_SPLIT=1 splits off a second RCCL communicator (ncclCommSplit,
+ * collective) for the halos, so they can run beside the critical-path collectives issued on the problem's stream; the
+ * ranks all-reduce the split's outcome before use and all keep one communicator unless every split succeeded.
+ * Without it (the default) every collective goes on the communication stream. */
 mvtv_status mvtv_comm_unique_id(uint8_t* id128);
 mvtv_status mvtv_comm_create_rccl(const uint8_t* id128, int32_t nranks, int32_t rank, int32_t device, mvtv_comm** out);
 /* in-process loopback group of nranks handles (comms[0..nranks-1]): each rank's mvtv_slab_run on its own
