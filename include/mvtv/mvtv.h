@@ -201,8 +201,9 @@ mvtv_status mvtv_solve_spectral(mvtv_problem* prob, double sigma, const double* 
  * desc->oty (and desc->wdiag, if any) cover them (ghost values are not used). Rank r owns planes
  * [floor(m r / G), floor(m (r+1) / G)). mvtv_slab_run is the whole variant-B loop of one rank
  * (rcpp…/solvers.cpp:110-133) with its collectives on a communication stream: the substructured line solves'
- * two all-to-alls of 2 and 2 numbers per line (each block's two recursion sums, then its two carries), halo planes of theta and of the edge state, one 7-value
- * all-reduce per iteration feeding the device-side adapt_step / stopping decision. With W != I (desc->wdiag)
+ * two all-to-alls of 2 and 2 numbers per line (each block's two recursion sums, then its two carries), halo
+ * planes of theta and of the edge state, one 7-value all-reduce per iteration feeding the device-side
+ * adapt_step / stopping decision. With W != I (desc->wdiag)
  * the theta-solve is PCG with the spectral preconditioner of mean(W) I + sigma D^T D (opts pcg_rtol,
  * pcg_max_iter, pcg_strict as mvtv_admm_run), distributed: a halo of the search direction per iteration and
  * one all-reduce per dot product; the loop then polls once per ADMM iteration. Supported: variant B, W = I
