@@ -120,7 +120,7 @@ def test_3d_solve_residual_extreme_sigma(m):
     1009 = 63 x 16 + 1 (a one-row last segment; 16-line tiles, 4096 lines). Round 6 (the factorised line solve,
     k_trir / k_trigr): 1024-point lines on 16-line tiles of 64 segments (64 x 64 x 1024) and on the few-lines 4-line
     tiles (32 x 64 x 1024), the 512-point 32-line tiles (128 x 128 x 512), 64-point lines (96 x 64 x 64: 16-line tiles
-    of 4 segments) and a tile that leaves some lines of the last workgroup invalid (40 x 48 x 256)."""
+    of 4 segments) and k_trigr's few-lines tiles over a line stride that is not a power of two (40 x 48 x 256)."""
     p = len(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     N = int(np.prod(m))
