@@ -110,7 +110,7 @@ def test_spectral_residual_baseline_sizes(m):
 
 @pytest.mark.parametrize("m", [[256, 256, 128], [512, 512, 128], [1024, 1024, 128], [256, 256, 300], [512, 512, 135],
                                [256, 256, 48], [96, 96, 400], [128, 128, 37], [256, 256, 101], [64, 64, 1009],
-                               [64, 64, 1024], [32, 64, 1024], [128, 128, 512], [96, 64, 64], [40, 48, 256]])
+                               [64, 64, 1024], [32, 32, 1024], [128, 128, 512], [64, 64, 64], [48, 48, 256]])
 def test_3d_solve_residual_extreme_sigma(m):
     """3-D spectral solves (k_dct8 / k_dctg passes, k_tri along the last dimension) from sigma = 0 (the identity) to a
     dominant coupling (cond ~ 1e7): residual through the stencil operator within the backward-stable bound;
@@ -119,8 +119,8 @@ def test_3d_solve_residual_extreme_sigma(m):
     lengths k_trig splits with a shorter last segment: 37 = 3 x 10 + 7, 101 = 6 x 16 + 5 (64-line tiles), the prime
     1009 = 63 x 16 + 1 (a one-row last segment; 16-line tiles, 4096 lines). Round 6 (the factorised line solve,
     k_trir / k_trigr): 1024-point lines on 16-line tiles of 64 segments (64 x 64 x 1024) and on the few-lines 4-line
-    tiles (32 x 64 x 1024), the 512-point 32-line tiles (128 x 128 x 512), 64-point lines (96 x 64 x 64: 16-line tiles
-    of 4 segments) and k_trigr's few-lines tiles over a line stride that is not a power of two (40 x 48 x 256)."""
+    tiles (32 x 32 x 1024), the 512-point 32-line tiles (128 x 128 x 512), 64-point lines (64^3: 16-line tiles of 4
+    segments) and k_trigr's few-lines tiles over a line stride that is not a power of two (48 x 48 x 256)."""
     p = len(m)
     deltas = [(1.0 + 2e-4) / v for v in m]
     N = int(np.prod(m))
