@@ -507,17 +507,30 @@ __global__ __launch_bounds__(256) void k_apply3d(const Apply3dArgs a) {
     if (!DOT && !act) return;   // no barriers below without DOT
     const int z0 = tz * a.zchunk, z1 = act ? min(m2, z0 + a.zchunk) : z0;
     const size_t pl = size_t(m0) * size_t(m1);
-    const int xl = mirror(x - 1, m0), xr = mirror(x + 1, m0);
     const size_t yd = size_t(mirror(y - 1, m1)) * m0, yc = size_t(y) * m0, yu = size_t(mirror(y + 1, m1)) * m0;
     const double K0 = a.K[0], K1 = a.K[1], K2 = a.K[2], K3 = a.K[3];
     const double K4 = a.K[4], K5 = a.K[5], K6 = a.K[6], K7 = a.K[7];
+    // a wave is one 64-cell x-run of a row: the x +- 1 neighbours come from the adjacent lanes (wave
+    // shuffles), only lanes 0 / 63 load the cell past the run; a mirrored neighbour is the cell itself.
+    // Exited lanes (x >= m0) are never read: their active neighbour takes the mirror (itself).
+    const int lane = int(threadIdx.x & 63);
+    const bool has_l = x > 0, has_r = x + 1 < m0;
+    const bool hload = (lane == 0 && has_l) || (lane == 63 && has_r);
+    const int xh = lane == 0 ? x - 1 : x + 1;
+    auto hsum = [&](const double* R, double c) {   // x-1 + x+1 neighbours of this lane's cell in row R
+        const double e = hload ? R[xh] : 0.0;
+        const double up = __shfl_up(c, 1), dn = __shfl_down(c, 1);
+        const double l = has_l ? (lane == 0 ? e : up) : c;
+        const double r = has_r ? (lane == 63 ? e : dn) : c;
+        return l + r;
+    };
     // in-plane sums of plane e: s0 (dz = 0 weights), s1 (dz = +-1 weights)
     auto sums = [&](int e, double& s0, double& s1) {
         const double* P = a.x + size_t(e) * pl;
-        const double c = P[yc + x];
-        const double h = P[yc + xl] + P[yc + xr];
-        const double v = P[yd + x] + P[yu + x];
-        const double d = (P[yd + xl] + P[yd + xr]) + (P[yu + xl] + P[yu + xr]);
+        const double c = P[yc + x], cd = P[yd + x], cu = P[yu + x];
+        const double h = hsum(P + yc, c);
+        const double v = cd + cu;
+        const double d = hsum(P + yd, cd) + hsum(P + yu, cu);
         s0 = fma(K0, c, fma(K1, h, fma(K2, v, K3 * d)));
         s1 = fma(K4, c, fma(K5, h, fma(K6, v, K7 * d)));
     };

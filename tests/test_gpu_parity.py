@@ -63,6 +63,21 @@ def test_operators(m, deltas, order, unit):
     P.close()
 
 
+@pytest.mark.parametrize("m,order", [([130, 130, 3], "cpp"), ([65, 65, 65], "py"), ([64, 64, 5], "cpp"),
+                                     ([200, 200, 2], "cpp"), ([127, 127, 4], "cpp"), ([70, 70, 70], "py")])
+def test_apply_A_3d_multi_run(m, order):
+    """the 3-D z-marching operator (k_apply3d) with dim-0 runs past one 64-lane wave: the x +- 1 neighbours
+    cross wave boundaries (lanes 0 / 63 load them) and ragged last runs (m_0 = m_1: the S' rule of test_dim_mismatch)."""
+    rng = np.random.default_rng(sum(m))
+    N = int(np.prod(m))
+    w = rng.uniform(0.0, 3.0, N).round()
+    P, D, _ = _problem(m, [0.5, 0.25, 0.125], order, False, wdiag=w)
+    th = rng.standard_normal(N)
+    for sigma in (0.0, 0.37, 25.6):
+        assert _rel(P.apply_A(sigma, th), O.apply_A(D, w, sigma, th)) <= RTOL_OP
+    P.close()
+
+
 @pytest.mark.parametrize("m,deltas,order,unit", SHAPES[:6])
 def test_pcg_solve(m, deltas, order, unit):
     rng = np.random.default_rng(2)
