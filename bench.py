@@ -366,15 +366,23 @@ def slab_main(a, D, comm=None):
         del y
         if a.warmup > 0:
             S.run(lam, fixed_iters=a.warmup)
+        # the value from an event-free region (a rank's ~1 ms iteration at G = 8 runs ~16 launches: per-launch
+        # HIP events would cost several %), the per-kernel table from a second region of the same length with them
         D.barrier()
-        S.P.timing(True)
+        S.P.timing(False)
         t0 = time.perf_counter()
         st = S.run(lam, fixed_iters=a.steps)   # returns after the stream drained
         t1 = time.perf_counter()
         D.barrier()
+        g_elapsed, = D.allreduce([t1 - t0], "max")
+        S.P.timing(True)
+        t2 = time.perf_counter()
+        S.run(lam, fixed_iters=a.steps)
+        t3 = time.perf_counter()
+        D.barrier()
         tim = S.P.timings()
         S.P.timing(False)
-        g_elapsed, = D.allreduce([t1 - t0], "max")
+        ev_elapsed, = D.allreduce([t3 - t2], "max")
         nranks = D.world
         rccl_ranks = comm.size if comm.kind == "rccl" else 0
         if comm.kind == "ipc":
@@ -396,6 +404,7 @@ def slab_main(a, D, comm=None):
         st, tim = outs[0], {}
         transport = f"in-process loopback, {R} ranks on one GPU"
         g_elapsed, nranks, rccl_ranks = t1 - t0, R, 0
+        ev_elapsed = None
     per = {k: dict(avg_ms=round(v["ms"] / v["launches"], 4), launches=v["launches"]) for k, v in tim.items()
            if v["launches"]}
     # the line solves cross the ranks (substructured) unless one rank holds the whole lines
@@ -416,6 +425,9 @@ def slab_main(a, D, comm=None):
         "rccl_ranks": rccl_ranks, "rccl_library": slab.Comm.library() if rccl_ranks else None,
         "transport": transport,
         "roofline": _roofline(tim), "kernels_rank0": per,
+        "timing": ("value from an event-free region; kernels_rank0 / roofline from a second region of the same "
+                   f"length with per-launch HIP events ({a.steps / ev_elapsed:.2f} it/s with them)")
+        if ev_elapsed else "no per-kernel events (in-process ranks)",
         "residuals": {"r_norm": st["r_norm"], "s_norm": st["s_norm"]}, "cpu_baseline": None}
 
 
@@ -563,8 +575,9 @@ def independent_main(a, D, comm=None):
     # Meshes up to 2^24 nodes run 0.07-0.9 ms iterations, where the per-launch timing events cost 7-30 % (1024^2:
     # 14.1k against 10.1k ADMM it/s, profiles/r04/v1_launch_gap; 256^3: 1166-1174 against 1086-1113): the value comes
     # from an event-free timed region and the per-kernel table from a second region of the same length right after
-    # it. Larger meshes (the 512^3 headline: ~1 %) time one region with the events in it.
-    event_free = P.N <= (1 << 24)
+    # it. Round 6: every mesh (the 512^3 headline's events cost ~1 %; MVTV_BENCH_EVENTS_IN_VALUE=1: one region
+    # with the events in it for meshes above 2^24 nodes, the round-5 timing)
+    event_free = P.N <= (1 << 24) or os.environ.get("MVTV_BENCH_EVENTS_IN_VALUE", "0") in ("", "0")
     D.barrier()
     P.timing(not event_free)
     t0 = time.perf_counter()
