@@ -555,16 +555,104 @@ __global__ __launch_bounds__(256) void k_apply3d(const Apply3dArgs a) {
     if constexpr (DOT) block_reduce_store<1, 0>(red, a.partials);
 }
 
+// The same with two adjacent cells a lane (m0 even, 16-B aligned vectors): a wave covers a 128-cell x-run with 16-B
+// loads and stores, so each of its march steps keeps twice the bytes in flight (the one-cell kernel waits a full
+// memory latency per plane step: 0.72 ms at 512^3 for 2N words). The sums per cell are the one-cell kernel's, in the
+// same order.
+typedef double a3v2 __attribute__((ext_vector_type(2)));
+
+template <int WM, bool DOT>
+__global__ __launch_bounds__(256) void k_apply3d2(const Apply3dArgs a) {
+    if (DOT && a.st->done) return;
+    const int bid = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const int nt = a.tiles_x * a.tiles_y;
+    const int tz = bid / nt, rem = bid - tz * nt;
+    const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
+    const int lane = int(threadIdx.x & 63);
+    const int x = tx * 128 + 2 * lane, y = ty * 4 + int(threadIdx.x >> 6);   // cells x, x + 1 (m0 even)
+    const int m0 = a.m0, m1 = a.m1, m2 = a.m2;
+    double red[1] = {0.0};
+    const bool act = bid < a.nblocks && x < m0 && y < m1;
+    if (!DOT && !act) return;   // no barriers below without DOT
+    const int z0 = tz * a.zchunk, z1 = act ? min(m2, z0 + a.zchunk) : z0;
+    const size_t pl = size_t(m0) * size_t(m1);
+    const size_t yd = size_t(mirror(y - 1, m1)) * m0, yc = size_t(y) * m0, yu = size_t(mirror(y + 1, m1)) * m0;
+    const double K0 = a.K[0], K1 = a.K[1], K2 = a.K[2], K3 = a.K[3];
+    const double K4 = a.K[4], K5 = a.K[5], K6 = a.K[6], K7 = a.K[7];
+    // cell x's right neighbour and cell x + 1's left one are the lane's own pair; x - 1 is the previous lane's
+    // second cell, x + 2 the next lane's first (lanes 0 / 63 load them past the run); mirrored: the cell itself
+    const bool has_l = x > 0, has_r = x + 2 < m0;
+    const bool hload = (lane == 0 && has_l) || (lane == 63 && has_r);
+    const int xh = lane == 0 ? x - 1 : x + 2;
+    auto ld = [](const double* p) { return *reinterpret_cast<const a3v2*>(p); };
+    auto hsum = [&](const double* R, a3v2 c) {
+        const double e = hload ? R[xh] : 0.0;
+        const double up = __shfl_up(c.y, 1), dn = __shfl_down(c.x, 1);
+        const double l = has_l ? (lane == 0 ? e : up) : c.x;
+        const double r = has_r ? (lane == 63 ? e : dn) : c.y;
+        a3v2 h;
+        h.x = l + c.y;
+        h.y = c.x + r;
+        return h;
+    };
+    auto comb = [](double k0, double k1, double k2, double k3, a3v2 c, a3v2 h, a3v2 v, a3v2 d) {
+        a3v2 s;
+        s.x = fma(k0, c.x, fma(k1, h.x, fma(k2, v.x, k3 * d.x)));
+        s.y = fma(k0, c.y, fma(k1, h.y, fma(k2, v.y, k3 * d.y)));
+        return s;
+    };
+    auto sums = [&](int e, a3v2& s0, a3v2& s1) {
+        const double* P = a.x + size_t(e) * pl;
+        const a3v2 c = ld(P + yc + x), cd = ld(P + yd + x), cu = ld(P + yu + x);
+        const a3v2 h = hsum(P + yc, c);
+        const a3v2 v = cd + cu;
+        const a3v2 d = hsum(P + yd, cd) + hsum(P + yu, cu);
+        s0 = comb(K0, K1, K2, K3, c, h, v, d);
+        s1 = comb(K4, K5, K6, K7, c, h, v, d);
+    };
+    a3v2 s0c = 0.0, s1c = 0.0, s0n = 0.0, s1n = 0.0, s1m = 0.0;
+    if (act) {
+        sums(z0, s0c, s1c);
+        if (z0 > 0) sums(z0 - 1, s0n, s1m);
+        else s1m = s1c;
+    }
+    for (int z = z0; z < z1; ++z) {
+        if (z + 1 < m2) sums(z + 1, s0n, s1n);
+        else s1n = s1c, s0n = s0c;
+        const size_t i = size_t(z) * pl + yc + x;
+        a3v2 out = s1m + s0c + s1n;
+        if (WM == W_DIAG) {
+            const a3v2 w = ld(a.wdiag + i), xv = ld(a.x + i);
+            out.x = fma(w.x, xv.x, out.x);
+            out.y = fma(w.y, xv.y, out.y);
+        }
+        __builtin_nontemporal_store(out, reinterpret_cast<a3v2*>(a.q + i));
+        if constexpr (DOT) {
+            const a3v2 xv = ld(a.x + i);
+            red[0] = fma(xv.y, out.y, fma(xv.x, out.x, red[0]));
+        }
+        s1m = s1c;
+        s0c = s0n;
+        s1c = s1n;
+    }
+    if constexpr (DOT) block_reduce_store<1, 0>(red, a.partials);
+}
+
 hipError_t launch_apply3d(const Geom& g, hipStream_t s, double sigma, int wmode, const double* wdiag,
                           const double* x, double* q, double* partials, const PcgState* st, int* nparts) {
     Apply3dArgs a{};
     a.m0 = int(g.m[0]);
     a.m1 = int(g.m[1]);
     a.m2 = int(g.m[2]);
-    a.tiles_x = (a.m0 + 63) / 64;
+    // two cells a lane where every row starts 16-B aligned (MVTV_APPLY3D_V1=1 in probe builds: one cell a lane)
+    static const bool v1_env = probe_env("MVTV_APPLY3D_V1") != nullptr;
+    const bool two = !v1_env && a.m0 % 2 == 0 &&
+                     ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(q) |
+                       reinterpret_cast<uintptr_t>(wmode == W_DIAG ? wdiag : nullptr)) & 15) == 0;
+    a.tiles_x = two ? (a.m0 + 127) / 128 : (a.m0 + 63) / 64;
     a.tiles_y = (a.m1 + 3) / 4;
     const int tiles = a.tiles_x * a.tiles_y;
-    int nz = std::max(1, std::min(a.m2, 8192 / std::max(1, tiles)));
+    int nz = std::max(1, std::min(a.m2, (two ? 4096 : 8192) / std::max(1, tiles)));
     a.zchunk = (a.m2 + nz - 1) / nz;
     nz = (a.m2 + a.zchunk - 1) / a.zchunk;
     a.nblocks = tiles * nz;
@@ -590,11 +678,15 @@ hipError_t launch_apply3d(const Geom& g, hipStream_t s, double sigma, int wmode,
     if (partials) {
         if (!st || !nparts) return hipErrorInvalidValue;
         *nparts = grid;
-        if (wmode == W_DIAG) klaunch(k_apply3d<W_DIAG, true>, dim3(grid), dim3(256), 0, s, a);
+        if (two && wmode == W_DIAG) klaunch(k_apply3d2<W_DIAG, true>, dim3(grid), dim3(256), 0, s, a);
+        else if (two) klaunch(k_apply3d2<W_NONE, true>, dim3(grid), dim3(256), 0, s, a);
+        else if (wmode == W_DIAG) klaunch(k_apply3d<W_DIAG, true>, dim3(grid), dim3(256), 0, s, a);
         else klaunch(k_apply3d<W_NONE, true>, dim3(grid), dim3(256), 0, s, a);
         return hipGetLastError();
     }
-    if (wmode == W_DIAG) klaunch(k_apply3d<W_DIAG, false>, dim3(grid), dim3(256), 0, s, a);
+    if (two && wmode == W_DIAG) klaunch(k_apply3d2<W_DIAG, false>, dim3(grid), dim3(256), 0, s, a);
+    else if (two) klaunch(k_apply3d2<W_NONE, false>, dim3(grid), dim3(256), 0, s, a);
+    else if (wmode == W_DIAG) klaunch(k_apply3d<W_DIAG, false>, dim3(grid), dim3(256), 0, s, a);
     else klaunch(k_apply3d<W_NONE, false>, dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
