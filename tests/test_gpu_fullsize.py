@@ -139,6 +139,29 @@ def test_config4_fold_path_2048_vs_c_oracle(solver):
         assert stats[k]["s_norm"] == pytest.approx(st["s_norm"], rel=1e-9)
 
 
+@pytest.mark.parametrize("m", [[160, 160, 8], [256, 256, 4]], ids=["160x160x8", "256x256x4"])
+def test_fold_3d_pcg_spectral_multi_run_vs_c_oracle(m):
+    """A 3-D CV-fold mask (W != I) on meshes whose dim-0 rows span more than one 128-cell run of the two-cell
+    operator (k_apply3d2's W-diagonal, dot-product form inside the spectrally preconditioned PCG, pcgs_solve):
+    3 fixed iterations against the C oracle's variant-B loop on the same inputs, rho exact, theta 1e-9."""
+    from oracle import c_oracle
+    y = towers(m)
+    deltas = [(1.0 + 2e-4) / v for v in m]
+    W = (cv.kfoldinds(y.size, 5, seed=1) != 0).astype(np.float64)
+    oty = W * y
+    th0 = np.full(y.size, float(y[W > 0].mean()))
+    lam, rho0, iters = 0.8, 0.16, 3
+    with mv.Problem(m, oty, wdiag=W, deltas=deltas, order=mv.ORDER_CPP) as P:
+        th, u, rho, st = P.admm(lam, th0, u=np.zeros(P.E), rho=rho0, fixed_iters=iters, pcg_rtol=1e-13,
+                                theta_solver=mv.SOLVER_PCG_SPECTRAL)
+    ref_th, ref_u = th0.copy(), np.zeros(c_oracle.num_edges(m))
+    ref = c_oracle.admm_rcpp(m, oty, lam, ref_th, ref_u, rho0, deltas, W=W, fixed_iters=iters, pcg_rtol=1e-13)
+    assert st["iters"] == iters and st["theta_solver"] == mv.SOLVER_PCG_SPECTRAL
+    assert rho == ref["rho"]
+    assert np.max(np.abs(th - ref_th)) <= 1e-9 * np.max(np.abs(ref_th))
+    assert st["r_norm"] == pytest.approx(ref["r_norm"], rel=1e-8)
+
+
 def test_metric_512_cubed_eight_rank_decomposition():
     """The metric at 8 GPUs as bench.py runs it (one 512^3 mesh, 64 planes per rank), rehearsed with the
     loopback transport on one GPU: 2 fixed iterations against the one-GPU run, rho exact, theta 1e-11."""
